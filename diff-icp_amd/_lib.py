@@ -1,0 +1,292 @@
+"""ctypes binding of the C-ABI library ``libdifficp_hip.so`` (declared in include/difficp_hip.h).
+
+This is the only place that talks to the native library.  It marshals device pointers of
+torch tensors, the current HIP stream and a scratch workspace; it never computes anything
+itself and there is no CPU fallback: if the library is missing or a tensor is not on a
+HIP device the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdifficp_hip.so")
+
+# enum dicp_red_op (include/difficp_hip.h)
+KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRADKSCAL, \
+    GRADLAPKSCAL, MIN_SQDIST = range(13)
+# enum dicp_ws_kind
+WS_RED, WS_ODE_SELF_FWD, WS_ODE_SELF_BWD, WS_ODE_EXT_FWD, WS_ODE_EXT_BWD, WS_GMM_ESTEP, \
+    WS_GMM_MSTEP, WS_GMM_TARGETS = range(8)
+
+_lock = threading.Lock()
+_lib = None
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_INT = ctypes.c_int
+_DBL = ctypes.c_double
+_SZ = ctypes.c_size_t
+
+_SIGNATURES = {
+    "dicp_gauss_red_f32": [_INT, _P, _I64, _P, _I64, _INT, _P, _P, _DBL, _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_self_fwd_f32": [_P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_self_bwd_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_ext_fwd_f32": [_P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_ext_bwd_f32": [_P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
+                                   _P, _SZ, _P],
+    "dicp_gmm_estep_f32": [_P, _I64, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _SZ, _P],
+    "dicp_gmm_mstep_f32": [_P, _P, _I64, _P, _P, _I64, _INT, _DBL, _P, _P, _SZ, _P],
+    "dicp_gmm_targets_f32": [_P, _P, _I64, _P, _P, _DBL, _P, _P, _I64, _INT, _P, _P, _SZ, _P],
+    "dicp_workspace_bytes": [_INT, _I64, _I64, _INT],
+    "dicp_last_error": [],
+    "dicp_version": [],
+    "dicp_supports_dim": [_INT],
+    "dicp_num_splits": [_INT, _I64, _I64],
+}
+_RESTYPES = {"dicp_workspace_bytes": _SZ, "dicp_last_error": ctypes.c_char_p,
+             "dicp_version": ctypes.c_char_p}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+
+class HipExtensionMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the native library; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipExtensionMissing(
+                    f"difficp_amd: native library {LIB_PATH} is not built. Run "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                    "`make -C diff-icp_amd/csrc`. There is no CPU fallback.")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, args in _SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPES.get(name, _INT)
+            _lib = handle
+    return _lib
+
+
+def version() -> str:
+    return lib().dicp_version().decode()
+
+
+def supports_dim(D: int) -> bool:
+    return bool(lib().dicp_supports_dim(int(D)))
+
+
+def num_splits(kind: int, M: int, N: int) -> int:
+    return int(lib().dicp_num_splits(int(kind), int(M), int(N)))
+
+
+def _check_rc(rc: int, what: str):
+    if rc != 0:
+        msg = lib().dicp_last_error().decode()
+        if rc == 2:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"difficp_amd HIP kernels need device tensors; {name} is on {t.device} "
+                           "(no CPU fallback)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    return t.contiguous()
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _workspace(kind: int, M: int, N: int, D: int, device):
+    nbytes = int(lib().dicp_workspace_bytes(kind, int(M), int(N), int(D)))
+    if nbytes == 0:
+        return None, 0
+    return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
+
+
+# ---------------------------------------------------------------------------------------
+# Gaussian-kernel reductions
+# ---------------------------------------------------------------------------------------
+_RED_OUT_VEC = {KRED, GRADK, DDK, GENDK, HESSK, GRADLAPK, GRADKSCAL, GRADLAPKSCAL}
+
+
+def gauss_red(op: int, x, y, sigma: float, b=None, c=None):
+    """One Gaussian-kernel reduction (dicp_gauss_red_f32). Returns (M,D) or (M,)."""
+    x = _dev(x, "x")
+    y = _dev(y, "y")
+    b = None if b is None else _dev(b, "b")
+    c = None if c is None else _dev(c, "c")
+    M, D = x.shape
+    N = y.shape[0]
+    if y.shape[1] != D:
+        raise ValueError("x and y must have the same dimension")
+    out = torch.empty((M, D) if op in _RED_OUT_VEC else (M,), device=x.device, dtype=torch.float32)
+    if M == 0:
+        return out
+    ws, nb = _workspace(WS_RED, M, N, D, x.device)
+    rc = lib().dicp_gauss_red_f32(int(op), _ptr(x), M, _ptr(y), N, D, _ptr(b), _ptr(c),
+                                  float(sigma), _ptr(out), _ptr(ws), nb, _stream(x.device))
+    _check_rc(rc, f"gauss_red(op={op})")
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Fused LDDMM ODE
+# ---------------------------------------------------------------------------------------
+def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = False):
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    M, D = q.shape
+    dev = q.device
+    v = torch.empty_like(q)
+    mG = torch.empty_like(q)
+    g = torch.empty(M, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
+    h = torch.empty(M, device=dev, dtype=torch.float32) if want_h else None
+    if M == 0:
+        return v, mG, g, h
+    ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, dev)
+    rc = lib().dicp_lddmm_ode_self_fwd_f32(_ptr(q), _ptr(p), M, D, float(sigma), float(eta),
+                                           _ptr(v), _ptr(mG), _ptr(g), _ptr(h), _ptr(ws), nb,
+                                           _stream(dev))
+    _check_rc(rc, "ode_self_fwd")
+    return v, mG, g, h
+
+
+def ode_self_bwd(q, p, gv, gmG, gdiv, sigma: float, eta: float):
+    """gdiv: None or a device tensor with one element (cotangent of sum_i g_i)."""
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    gv = _dev(gv, "gv")
+    gmG = _dev(gmG, "gmG")
+    gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
+    M, D = q.shape
+    gq = torch.empty_like(q)
+    gp = torch.empty_like(q)
+    if M == 0:
+        return gq, gp
+    ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
+    rc = lib().dicp_lddmm_ode_self_bwd_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv), M,
+                                           D, float(sigma), float(eta), _ptr(gq), _ptr(gp),
+                                           _ptr(ws), nb, _stream(q.device))
+    _check_rc(rc, "ode_self_bwd")
+    return gq, gp
+
+
+def ode_ext_fwd(x, q, p, sigma: float, eta: float, want_div: bool):
+    x = _dev(x, "x")
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    N, D = x.shape
+    M = q.shape[0]
+    vx = torch.empty_like(x)
+    gx = torch.empty(N, device=x.device, dtype=torch.float32) if want_div else None
+    if N == 0:
+        return vx, gx
+    ws, nb = _workspace(WS_ODE_EXT_FWD, M, N, D, x.device)
+    rc = lib().dicp_lddmm_ode_ext_fwd_f32(_ptr(x), N, _ptr(q), _ptr(p), M, D, float(sigma),
+                                          float(eta), _ptr(vx), _ptr(gx), _ptr(ws), nb,
+                                          _stream(x.device))
+    _check_rc(rc, "ode_ext_fwd")
+    return vx, gx
+
+
+def ode_ext_bwd(x, q, p, gvx, gdiv, sigma: float, eta: float, gq, gp):
+    """Returns gx; ACCUMULATES the (q, p) gradients into gq, gp (contiguous, in place)."""
+    x = _dev(x, "x")
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    gvx = _dev(gvx, "gvx")
+    gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
+    if not (gq.is_contiguous() and gp.is_contiguous()):
+        raise ValueError("gq/gp accumulators must be contiguous")
+    N, D = x.shape
+    M = q.shape[0]
+    gx = torch.empty_like(x)
+    if N == 0:
+        return gx
+    ws, nb = _workspace(WS_ODE_EXT_BWD, M, N, D, x.device)
+    rc = lib().dicp_lddmm_ode_ext_bwd_f32(_ptr(x), N, _ptr(q), _ptr(p), M, D, float(sigma),
+                                          float(eta), _ptr(gvx), _ptr(gdiv), _ptr(gx), _ptr(gq),
+                                          _ptr(gp), _ptr(ws), nb, _stream(x.device))
+    _check_rc(rc, "ode_ext_bwd")
+    return gx
+
+
+# ---------------------------------------------------------------------------------------
+# GMM EM passes
+# ---------------------------------------------------------------------------------------
+def gmm_estep(X, mu, w2, mu2, sigma: float, lgn: float, want_stats: bool):
+    X = _dev(X, "X")
+    mu = _dev(mu, "mu")
+    w2 = _dev(w2, "w2")
+    mu2 = _dev(mu2, "mu2")
+    N, D = X.shape
+    C = mu.shape[0]
+    dev = X.device
+    T = torch.empty(N, device=dev, dtype=torch.float32)
+    T2 = torch.empty(N, device=dev, dtype=torch.float32)
+    stats = torch.empty((N, D + 4), device=dev, dtype=torch.float32) if want_stats else None
+    if N == 0:
+        return T, T2, stats
+    ws, nb = _workspace(WS_GMM_ESTEP, N, C, D, dev)
+    rc = lib().dicp_gmm_estep_f32(_ptr(X), N, _ptr(mu), _ptr(w2), _ptr(mu2), C, D, float(sigma),
+                                  float(lgn), _ptr(T), _ptr(T2), _ptr(stats), _ptr(ws), nb,
+                                  _stream(dev))
+    _check_rc(rc, "gmm_estep")
+    return T, T2, stats
+
+
+def gmm_mstep(X, T2, mu, w2, sigma: float):
+    X = _dev(X, "X")
+    T2 = _dev(T2, "T2")
+    mu = _dev(mu, "mu")
+    w2 = _dev(w2, "w2")
+    N, D = X.shape
+    C = mu.shape[0]
+    colstats = torch.empty((C, D + 1), device=X.device, dtype=torch.float32)
+    ws, nb = _workspace(WS_GMM_MSTEP, N, C, D, X.device)
+    rc = lib().dicp_gmm_mstep_f32(_ptr(X), _ptr(T2), N, _ptr(mu), _ptr(w2), C, D, float(sigma),
+                                  _ptr(colstats), _ptr(ws), nb, _stream(X.device))
+    _check_rc(rc, "gmm_mstep")
+    return colstats
+
+
+def gmm_targets(X, T2, mu_old, w2_old, sigma_old: float, mu_new, lpi_new):
+    X = _dev(X, "X")
+    T2 = _dev(T2, "T2")
+    mu_old = _dev(mu_old, "mu_old")
+    w2_old = _dev(w2_old, "w2_old")
+    mu_new = _dev(mu_new, "mu_new")
+    lpi_new = _dev(lpi_new, "lpi_new")
+    N, D = X.shape
+    C = mu_old.shape[0]
+    rows = torch.empty((N, D + 4), device=X.device, dtype=torch.float32)
+    if N == 0:
+        return rows
+    ws, nb = _workspace(WS_GMM_TARGETS, N, C, D, X.device)
+    rc = lib().dicp_gmm_targets_f32(_ptr(X), _ptr(T2), N, _ptr(mu_old), _ptr(w2_old),
+                                    float(sigma_old), _ptr(mu_new), _ptr(lpi_new), C, D,
+                                    _ptr(rows), _ptr(ws), nb, _stream(X.device))
+    _check_rc(rc, "gmm_targets")
+    return rows

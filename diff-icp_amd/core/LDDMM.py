@@ -1,0 +1,213 @@
+"""LDDMM model for point sets (classic / hybrid / logdet), HIP-backed.
+
+Mirror of diffICP/core/LDDMM.py:28-398 (`LDDMMModel`): same constructor, attributes and
+methods (v, mdivsum, Hamiltonian, dtrajcost, ODE, v2p, random_p, Shoot, trajloss,
+BasicQuadLossFunctor, Optimize), same return conventions.  The vector field is
+    v(x) = sum_j [p_j K(x - q_j) - eta (grad K)(x - q_j)],  eta = 1/lambda or 0.
+What changes is where the arithmetic happens: Shoot() runs the fused trajectory of
+core/shooting.py (one fused HIP pass per ODE evaluation, exact discrete adjoint for the
+backward) instead of the reference's per-reduction integrator loop.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..tools.integrators import EulerIntegrator, RalstonIntegrator
+from ..tools.kernel import GaussKernel, SVDpow
+from ..tools.optim import LBFGS_optimization
+from ..tools.spec import defspec, getspec
+from .shooting import HamiltonianFn, OdeExtFn, OdeFn, ShootFn
+
+
+class Shoot(list):
+    """A "shoot" variable: list of (q, p, cost[, x]) states at the nt+1 integration times
+    (LDDMM.py:286-299).  The states are views into stacked trajectory tensors Q, P, C[, X]
+    that stay resident on the device."""
+
+    def __init__(self, Q, P, C, X=None):
+        nt1 = Q.shape[0]
+        if X is None:
+            super().__init__((Q[t], P[t], C[t]) for t in range(nt1))
+        else:
+            super().__init__((Q[t], P[t], C[t], X[t]) for t in range(nt1))
+        self.Q, self.P, self.C, self.X = Q, P, C, X
+
+
+class LDDMMModel:
+
+    def __init__(self, sigma=1.0, D=2, lambd=2.0, spec=defspec, gradcomponent=True,
+                 withlogdet=True, version=None, computversion="hip", scheme="Ralston",
+                 nonsupprev=False, nt=10):
+        """Same arguments as LDDMM.py:33-65.  `version` in {classic, logdet, hybrid}
+        overrides (gradcomponent, withlogdet)."""
+        self.Kernel = GaussKernel(sigma, D, computversion=computversion, spec=spec)
+        self.D = D
+        self.lam = lambd
+        self.nt = nt
+        if version == "classic":
+            gradcomponent, withlogdet = False, False
+        elif version == "logdet":
+            gradcomponent, withlogdet = True, True
+        elif version == "hybrid":
+            gradcomponent, withlogdet = False, True
+        self.withlogdet = withlogdet
+        self.gradcomponent = gradcomponent
+        self.eta = 1.0 / lambd if gradcomponent else 0
+        self.nonsupprev = nonsupprev
+        self.scheme, self.Integrator = None, None
+        self.set_integration_scheme(scheme)
+        self.try_trajcost_optim = False
+
+    def set_integration_scheme(self, scheme: str):
+        self.scheme = scheme
+        if scheme == "Euler":
+            self.Integrator = EulerIntegrator
+        elif scheme == "Ralston":
+            self.Integrator = RalstonIntegrator
+        else:
+            raise ValueError(f"Unkown numerical scheme : {scheme}")
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self.Kernel = GaussKernel(self.Kernel.sigma, self.Kernel.D, self.Kernel.computversion,
+                                  spec=defspec)
+
+    @property
+    def sigma(self):
+        return self.Kernel.sigma
+
+    # ------------------------------------------------------------------------------------
+    def v(self, x, q, p):
+        """v(x) = KRed(x,q,p) - eta GradKRed(x,q)   (LDDMM.py:100-116)."""
+        spec = getspec(x, q, p)
+        if x.numel() == 0:
+            return torch.empty(x.shape, **spec)
+        if self.gradcomponent:
+            return self.Kernel.KRed(x, q, p) - self.eta * self.Kernel.GradKRed(x, q)
+        return self.Kernel.KRed(x, q, p)
+
+    def mdivsum(self, x, q, p, rev=False):
+        """-sum_k div v(x_k), shape (1,)-compatible scalar (LDDMM.py:120-138)."""
+        spec = getspec(x, q, p)
+        if x.numel() == 0:
+            return torch.tensor([0.0], **spec)
+        if rev:
+            r = self.Kernel.GradKRed_rev(q, x, p).sum()
+        else:
+            r = (p * self.Kernel.GradKRed(q, x)).sum()
+        if self.gradcomponent:
+            r = r + self.eta * self.Kernel.LapKRed(q, x).sum()
+        return r
+
+    def Hamiltonian(self, q, p):
+        """H(q,p) = 1/2 sum_ij [p_i.p_j K - eta (p_i-p_j).gradK - eta^2 LapK]  (LDDMM.py:142-159),
+        one fused HIP pass."""
+        getspec(q, p)
+        return HamiltonianFn.apply(q.contiguous(), p.contiguous(), self.Kernel.sigma, float(self.eta))
+
+    def dtrajcost(self, q, p):
+        """lambda*H(q,p) + mdivsum(q,q,p) variant (LDDMM.py:163-172)."""
+        getspec(q, p)
+        return 0.5 * self.lam * (p * self.Kernel.KRed(q, q, p)).sum() \
+            + 0.5 * self.eta * self.Kernel.LapKRed(q, q).sum()
+
+    def ODE(self, q, p, cost, x=None):
+        """d/dt (q, p, cost[, x]) (LDDMM.py:176-227); one fused HIP pass (+1 for x)."""
+        spec = getspec(q, p, cost, x)
+        want_div = bool(self.withlogdet)
+        if self.try_trajcost_optim and self.withlogdet and self.gradcomponent and x is None:
+            vq, mG, _ = OdeFn.apply(q.contiguous(), p.contiguous(), self.Kernel.sigma,
+                                    float(self.eta), False)
+            return vq, mG, self.dtrajcost(q, p).reshape(1)
+        if x is None:
+            vq, mG, dcost = OdeFn.apply(q.contiguous(), p.contiguous(), self.Kernel.sigma,
+                                        float(self.eta), want_div)
+            if not want_div:
+                dcost = torch.tensor([0.0], **spec)
+            return vq, mG, dcost
+        vq, mG, dcost, vx = OdeExtFn.apply(q.contiguous(), p.contiguous(), x.contiguous(),
+                                           self.Kernel.sigma, float(self.eta), want_div)
+        if not want_div:
+            dcost = torch.tensor([0.0], **spec)
+        return vq, mG, dcost, vx
+
+    # ------------------------------------------------------------------------------------
+    def v2p(self, q, v, rcond=1e-3, alpha=1e-4, version="pinv"):
+        """Momenta p with v(q,q,p) ~= v (LDDMM.py:235-253)."""
+        getspec(q, v)
+        rhs = v if self.eta == 0 else v + self.eta * self.Kernel.GradKRed(q, q)
+        if version == "pinv":
+            return self.Kernel.KpinvSolve(q, rhs, rcond)
+        elif version in ("ridge_keops", "ridge_pytorch", "ridge_hip"):
+            return self.Kernel.KridgeSolve(q, rhs, alpha)
+        raise ValueError("unknown version")
+
+    def random_p(self, q, rcond=1e-3, alpha=1e-4, version="svd"):
+        """Momenta drawn from exp(-lambda H(q,p)) (LDDMM.py:257-280)."""
+        spec = getspec(q)
+        if self.eta != 0:
+            raise ValueError("random_p not implemented yet when gradcomponent=True.")
+        K = (-(q[:, None, :] - q[None, :, :]) ** 2 / (2 * self.Kernel.sigma ** 2)).sum(-1).exp()
+        zeta = torch.randn(q.shape, **spec) / math.sqrt(self.lam)
+        if version == "svd":
+            return (SVDpow(K, -0.5, rcond) @ zeta).contiguous()
+        elif version == "ridge":
+            return torch.linalg.solve(torch.linalg.cholesky(
+                K + alpha * torch.eye(K.shape[0], **spec)), zeta).contiguous()
+        raise ValueError("Unknown version")
+
+    # ------------------------------------------------------------------------------------
+    def Shoot(self, q0, p0, x0=None):
+        """Geodesic shooting from (q0, p0[, x0]); returns the list of (q, p, cost[, x])
+        at the nt+1 times (LDDMM.py:286-299)."""
+        getspec(q0, p0, x0)
+        if self.try_trajcost_optim and self.withlogdet and self.gradcomponent and x0 is None:
+            # rarely used reference variant: generic integrator over the per-step ODE
+            cost0 = torch.zeros(1, dtype=q0.dtype, device=q0.device)
+            return self.Integrator(self.ODE, (q0, p0, cost0), self.nt)
+        outs = ShootFn.apply(q0.contiguous(), p0.contiguous(),
+                             None if x0 is None else x0.contiguous(), self.Kernel.sigma,
+                             float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet))
+        return Shoot(*outs)
+
+    def BasicQuadLossFunctor(self, y, cmul=1):
+        y = y.detach()
+
+        def dataloss(x):
+            return ((x - y) ** 2).sum() * cmul / 2
+        return dataloss
+
+    def trajloss(self, shoot):
+        """lambda*H(q0,p0) + cost_1  (LDDMM.py:318-334)."""
+        arrival = shoot[-1]
+        cost = arrival[2]
+        is_x = len(arrival) == 4
+        if not is_x and self.withlogdet and self.gradcomponent and self.try_trajcost_optim:
+            return cost
+        q0, p0 = shoot[0][:2]
+        return self.lam * self.Hamiltonian(q0, p0) + cost
+
+    def Optimize(self, dataloss, q0, p0, x0=None, nmax=10, tol=1e-3, errthresh=1e8):
+        """min_p0 trajloss + dataloss(q1 or x1) with L-BFGS (LDDMM.py:338-398).
+        Returns (p0, shoot, trajl, datal, nsteps, change)."""
+        getspec(q0, p0, x0)
+        is_x = x0 is not None
+        q0 = q0.detach()
+        if is_x:
+            x0 = x0.detach()
+
+        def lossfunc(p0):
+            shoot = self.Shoot(q0, p0, x0)
+            last = shoot[-1][-1] if is_x else shoot[-1][0]
+            return self.trajloss(shoot) + dataloss(last)
+
+        p0, _, nsteps, change = LBFGS_optimization([p0], lossfunc, nmax=nmax, tol=tol,
+                                                   errthresh=errthresh)
+        p0 = p0[0]
+        with torch.no_grad():
+            shoot = self.Shoot(q0, p0, x0)
+            trajl = self.trajloss(shoot).item()
+            datal = dataloss(shoot[-1][-1] if is_x else shoot[-1][0]).item()
+        return p0, shoot, trajl, datal, nsteps, change

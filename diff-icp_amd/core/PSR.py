@@ -1,0 +1,300 @@
+"""diff-ICP point-set registration driver (mirror of diffICP/core/PSR.py MultiPSR :42-346 and
+DiffPSR :354-569), the caller of the HIP hot path.
+
+Same attributes (x0, x1, y, N, GMMi, LMi, q0, a0, allx0, Cfe, regloss, quadloss, FE, shoot)
+and methods (reinitialize_GMM, update_GMM_targets, update_quadloss, update_FE, GMM_opt,
+Reg_opt, Registration, initialize_a0, update_a0, set_support_scheme, QuadLossFunctor).
+
+MI355X addition -- frame sharding (`comm`): with a torch.distributed group of W ranks
+(one process per GPU, RCCL over xGMI), rank r owns the frames {k : k mod W == r}.
+Reg_opt runs only the local frames (no communication: each frame's L-BFGS is
+independent, PSR.py:528-569); GMM_opt runs EM on the local points and exchanges the
+per-component sufficient statistics (see core/GMM.py), so every rank holds the same GMM;
+free-energy bookkeeping sums regloss / quadloss across ranks.  Frames not owned by a rank
+keep their initial values there (x1, y, a0 are only meaningful on the owning rank).
+"""
+from __future__ import annotations
+
+import copy
+import warnings
+
+import numpy as np
+import torch
+
+from .GMM import GaussianMixtureUnif, _comm_active, _gather_rows, _sum_ranks
+from .LDDMM import LDDMMModel
+from .registrations import LDDMMRegistration
+from ..tools.in_out import read_point_sets
+from ..tools.spec import defspec
+
+
+def _rank_world(comm):
+    if not _comm_active(comm):
+        return 0, 1
+    import torch.distributed as dist
+    g = None if comm is True else comm
+    return dist.get_rank(g), dist.get_world_size(g)
+
+
+class MultiPSR:
+
+    def __init__(self, x, GMMi, dataspec=defspec, compspec=defspec, comm=None):
+        self.dataspec, self.compspec = dataspec, compspec
+        self.printstuff = True
+        self.comm = comm
+        self.rank, self.world = _rank_world(comm)
+        x, self.K, self.S, self.D = read_point_sets(x)
+        # local frames of this rank (all frames when not sharded)
+        self.frames = [k for k in range(self.K) if k % self.world == self.rank]
+        self.x0 = np.empty((self.K, self.S), dtype=object)
+        self.x1 = np.empty((self.K, self.S), dtype=object)
+        self.y = np.empty((self.K, self.S), dtype=object)
+        for k in range(self.K):
+            for s in range(self.S):
+                self.x0[k, s] = x[k][s].contiguous().detach().to(**self.dataspec)
+                self.x1[k, s] = self.x0[k, s].clone()
+                self.y[k, s] = self.x0[k, s].clone()
+        self.N = np.array([[self.x0[k, s].shape[0] for s in range(self.S)] for k in range(self.K)])
+
+        if isinstance(GMMi, GaussianMixtureUnif):
+            self.GMMi = [copy.deepcopy(GMMi) for _ in range(self.S)]
+        else:
+            if not isinstance(GMMi, list) or len(GMMi) != self.S:
+                raise ValueError("GMMi should be a single GMM model, or a list with S GMM models")
+            self.GMMi = [copy.deepcopy(g) for g in GMMi]
+        if any(g.spec != compspec for g in self.GMMi):
+            raise ValueError("Spec (dtype+device) error : GMM 'spec' and multiPSR 'compspec' "
+                             "attributes should be the same")
+        for g in self.GMMi:
+            g.comm = comm if self.world > 1 else None
+
+        self.Cfe = [None] * self.S
+        self.regloss = [0] * self.K
+        self.quadloss = np.zeros((self.K, self.S))
+        self.FE = None
+        self.update_GMM_targets()
+        self.shoot = [None] * self.K
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self.dataspec = defspec
+        self.compspec = defspec
+
+    # ------------------------------------------------------------------------------------
+    def _local_cat(self, arr, s):
+        parts = tuple(arr[k, s] for k in self.frames)
+        if len(parts) == 0:
+            return torch.empty((0, self.D), **self.compspec)
+        return torch.cat(parts, dim=0).to(**self.compspec)
+
+    def reinitialize_GMM(self, s=None, do_mu=True, do_sigma=True):
+        """mu = mean + 0.05 std randn, sigma = 0.25 std over all unwarped points (PSR.py:143-167).
+        Sharded: global mean/std from per-rank sums; the randn draw is made on rank 0's
+        stream of numbers and shared, so all ranks hold the same centroids."""
+        slist = range(self.S) if s is None else [s]
+        for s in slist:
+            if self.world == 1:
+                allx0s = torch.cat(tuple(self.x0[:, s]), dim=0)
+                mean, std = allx0s.mean(dim=0), allx0s.std()
+            else:
+                loc = torch.cat(tuple(self.x0[k, s] for k in self.frames), dim=0).double()
+                n = _sum_ranks(float(loc.shape[0]), self.comm).item()
+                s1 = _gather_rows(loc.sum(0).to(**self.compspec).double(), self.comm).sum(0)
+                s2 = _sum_ranks((loc ** 2).sum().to(self.compspec["device"]), self.comm)
+                mean = (s1 / n)
+                ntot = n * self.D
+                tot1 = s1.sum()
+                std = torch.sqrt((s2 - tot1 ** 2 / ntot) / (ntot - 1))
+                mean = mean.to(**self.dataspec)
+                std = std.to(**self.dataspec)
+            g = self.GMMi[s]
+            if do_mu and g.to_optimize["mu"]:
+                noise = torch.randn(g.C, self.D, **self.dataspec)
+                if self.world > 1:
+                    import torch.distributed as dist
+                    nz = noise.to(self.compspec["device"])
+                    dist.broadcast(nz, 0, group=None if self.comm is True else self.comm)
+                    noise = nz.to(**self.dataspec)
+                g.mu = (mean + 0.05 * std * noise).to(**self.compspec)
+            if do_sigma and g.to_optimize["sigma"]:
+                g.sigma = 0.25 * float(std)
+        self.update_GMM_targets()
+
+    def get_data_points(self, k=0, s=0):
+        return self.x0[k, s]
+
+    def get_warped_data_points(self, k=0, s=0):
+        return self.x1[k, s]
+
+    def get_template(self, s=0):
+        return self.GMMi[s].mu
+
+    # ------------------------------------------------------------------------------------
+    def _assign_targets(self, s, allys):
+        last = 0
+        for k in self.frames:
+            first, last = last, last + int(self.N[k, s])
+            self.y[k, s] = allys[first:last].to(**self.dataspec)
+            self.update_quadloss(k, s)
+
+    def update_GMM_targets(self):
+        """y, Cfe, quadloss, FE from an E-step without parameter update (PSR.py:197-213)."""
+        for s in range(self.S):
+            allx1s = self._local_cat(self.x1, s)
+            allys, self.Cfe[s], _ = self.GMMi[s].EM_step(allx1s, skip_M=True)
+            self._assign_targets(s, allys)
+        self.update_FE()
+
+    def update_quadloss(self, k, s):
+        """quadloss[k,s] = |x1 - y|^2 / (2 sigma_s^2)  (PSR.py:217-222)."""
+        self.quadloss[k, s] = ((self.x1[k, s] - self.y[k, s]) ** 2).sum() / (2 * self.GMMi[s].sigma ** 2)
+
+    def update_FE(self, message=None):
+        """FE = sum Cfe + sum regloss + sum quadloss (PSR.py:226-236); global when sharded."""
+        local_reg = sum(float(self.regloss[k]) for k in self.frames)
+        local_quad = float(sum(self.quadloss[k, s] for k in self.frames for s in range(self.S)))
+        if self.world > 1:
+            dev = self.compspec["device"]
+            local_reg = float(_sum_ranks(torch.tensor(local_reg, device=dev), self.comm))
+            local_quad = float(_sum_ranks(torch.tensor(local_quad, device=dev), self.comm))
+        FE = float(sum(float(c) for c in self.Cfe)) + local_reg + local_quad
+        if self.printstuff and message is not None and self.rank == 0:
+            print(message.ljust(70) + f"Total free energy = {FE:.8}")
+        if self.FE is not None and FE > self.FE and self.rank == 0:
+            print("WARNING: measured increase in free energy ! Should not happen.")
+        self.FE = FE
+
+    def GMM_opt(self, max_iterations=100, tol=1e-5):
+        """EM per structure on all (local) warped points, then targets back per frame
+        (PSR.py:242-271)."""
+        for s in range(self.S):
+            allx1s = self._local_cat(self.x1, s)
+            allys, self.Cfe[s], _, i = self.GMMi[s].EM_optimization(allx1s, max_iterations=max_iterations, tol=tol)
+            self._assign_targets(s, allys)
+            message = f"GMM optim (structure {s}) : {i} EM steps"
+            if self.GMMi[s].outliers:
+                p0 = 1 / (1 + np.exp(-self.GMMi[s].outliers["eta0"]))
+                message += f", p_outlier={p0:.4}"
+            else:
+                message += "."
+            self.update_FE(message=message)
+
+    def Reg_opt(self, tol=1e-5):
+        raise NotImplementedError("function Reg_opt must be written in derived classes.")
+
+    def Registration(self, k=0):
+        if isinstance(self, DiffPSR):
+            return LDDMMRegistration(self.LMi, self.q0[k], self.a0[k])
+        raise NotImplementedError
+
+
+class DiffPSR(MultiPSR):
+    """MultiPSR with LDDMM registrations (PSR.py:354-569)."""
+
+    def __init__(self, x, GMMi, LMi: LDDMMModel, dataspec=defspec, compspec=defspec, comm=None):
+        super().__init__(x, GMMi, dataspec=dataspec, compspec=compspec, comm=comm)
+        if LMi.Kernel.spec != compspec:
+            raise ValueError("Spec (dtype+device) error : LDDMMmodel kernel 'spec' and diffPSR "
+                             "'compspec' attributes should be the same")
+        self.LMi = LMi
+        self.allx0 = [None] * self.K
+        for k in range(self.K):
+            self.allx0[k] = torch.cat(tuple(self.x0[k, :]), dim=0).to(**self.compspec).contiguous()
+        self.support_scheme, self.rho = None, None
+        self.q0 = self.allx0
+        self.a0 = [None] * self.K
+        self.initialize_a0()
+
+    def initialize_a0(self, **v2p_args):
+        """a0 giving zero initial speeds (PSR.py:406-413)."""
+        for k in range(self.K):
+            v0 = torch.zeros(self.q0[k].shape, **self.compspec)
+            self.a0[k] = self.LMi.v2p(self.q0[k], v0, **v2p_args)
+
+    def update_a0(self, q0_prev, a0_prev=None, **v2p_args):
+        if a0_prev is None:
+            a0_prev = self.a0
+        for k in range(self.K):
+            v0 = self.LMi.v(self.q0[k], q0_prev[k], a0_prev[k])
+            self.a0[k] = self.LMi.v2p(self.q0[k], v0, **v2p_args)
+
+    def set_support_scheme(self, scheme="decim", rho=1.0, xticks=None, yticks=None, q0=None):
+        """Support points: "grid" (2D, PSR.py:472-482) or "custom" (:484-487).
+        "decim" (greedy O(N^2) host decimation, point_sets.py:102-133) is a next-row item."""
+        self.rho = rho
+        Rcover = rho * self.LMi.Kernel.sigma
+        self.support_scheme = scheme
+        q0_prev = self.q0
+        if scheme == "grid":
+            if self.D != 2:
+                raise ValueError("grid support scheme is 2D only (as in the reference)")
+            if xticks is None or yticks is None:
+                # get_bounds(*allx0, relmargin=0.1) (visualization/visu.py:35-50), same float32 ops
+                xs = [a.detach().cpu() for a in self.allx0 if len(a) > 0]
+                mins = torch.cat(tuple(a.min(0).values.reshape(1, 2) for a in xs), 0).min(0).values.numpy()
+                maxs = torch.cat(tuple(a.max(0).values.reshape(1, 2) for a in xs), 0).max(0).values.numpy()
+                gmin = (1 + 0.1) * mins - 0.1 * maxs
+                gmax = (1 + 0.1) * maxs - 0.1 * mins
+                xmin, xmax, ymin, ymax = gmin[0], gmax[0], gmin[1], gmax[1]
+            if xticks is None:
+                xticks = np.arange(xmin - Rcover / 2, xmax + Rcover / 2, Rcover)
+            if yticks is None:
+                yticks = np.arange(ymin - Rcover / 2, ymax + Rcover / 2, Rcover)
+            gp = np.stack(np.meshgrid(xticks, yticks), axis=2)
+            gp = torch.tensor(gp.reshape((-1, 2), order="F"), **self.compspec).contiguous()
+            self.q0 = [gp] * self.K
+        elif scheme == "custom":
+            assert q0 is not None, "For a custom support scheme, please specify argument q0"
+            self.q0 = [q0.clone().detach().to(**self.compspec).contiguous()] * self.K
+        elif scheme == "decim":
+            raise NotImplementedError("support scheme 'decim' is not provided yet (use 'grid' or 'custom')")
+        else:
+            raise ValueError(f"Unknown value of support point scheme : {scheme}.")
+        self.update_a0(q0_prev, rcond=1e-1)
+
+    def QuadLossFunctor(self, k):
+        """dataloss(x) = sum (x - y)^2 / (2 sigma_s^2) over frame k (PSR.py:498-516)."""
+        y = torch.cat(tuple(self.y[k, :]), dim=0).to(**self.compspec).contiguous()
+        sig2 = torch.cat(tuple(self.GMMi[s].sigma ** 2 * torch.ones(int(self.N[k, s]))
+                               for s in range(self.S))).to(**self.compspec).contiguous()
+
+        def dataloss_func(x):
+            return ((x - y) ** 2 / (2 * sig2[:, None])).sum()
+        return dataloss_func
+
+    def Reg_opt(self, nmax=10, tol=1e-3):
+        """Per-frame LDDMM optimisation (PSR.py:521-569), local frames only when sharded."""
+        for k in self.frames:
+            if self.support_scheme is None:
+                self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
+                    self.LMi.Optimize(self.QuadLossFunctor(k), self.q0[k], self.a0[k], tol=tol, nmax=nmax)
+                allx1k = self.shoot[k][-1][0]
+            else:
+                self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
+                    self.LMi.Optimize(self.QuadLossFunctor(k), self.q0[k], self.a0[k],
+                                      self.allx0[k], tol=tol, nmax=nmax)
+                allx1k = self.shoot[k][-1][-1]
+            last = 0
+            for s in range(self.S):
+                first, last = last, last + int(self.N[k, s])
+                self.x1[k, s] = allx1k[first:last].to(**self.dataspec)
+            for s in range(self.S):
+                self.update_quadloss(k, s)
+            if self.support_scheme is not None:
+                Rw = 2.0
+                for t in range(len(self.shoot[k])):
+                    qk, xk = self.shoot[k][t][0], self.shoot[k][t][-1]
+                    unc = self.LMi.Kernel.check_coverage(xk, qk, Rw)
+                    if unc.any():
+                        print(f"WARNING : shooting, time step {t} : {unc.sum()} uncovered points "
+                              f"({unc.sum() / xk.shape[0]:.2%})")
+                        warnings.warn("Uncovered points during LDDMM shooting. Choose a smaller rho "
+                                      "when defining the support scheme.", RuntimeWarning)
+            chg = change if isinstance(change, str) else f"{change:.4}"
+            msg = f"Frame {k} : {isteps} optim steps, loss={self.regloss[k] + datal:.4}, change={chg}."
+            if self.world == 1:
+                self.update_FE(message=msg)
+            elif self.printstuff:
+                print(f"[rank {self.rank}] " + msg)
+        if self.world > 1:
+            self.update_FE(message="Reg_opt (all frames)")

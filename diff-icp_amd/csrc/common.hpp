@@ -1,0 +1,188 @@
+// Shared machinery of the diff-ICP gfx950 kernels: the tiled "row reduction over column
+// tiles staged in LDS" skeleton that every N x M pass (Gaussian-kernel sums, fused LDDMM
+// ODE, GMM E/M/targets passes) is built from, plus the deterministic split-column merge.
+//
+// Design (MI355X-first):
+//  * one workgroup = 256 threads = 4 wave64; each thread owns R target rows held in VGPRs;
+//  * the column range [j0, j1) of this workgroup is swept in tiles of 256 column records
+//    staged in LDS (one record per thread, float4-packed); every lane of a wave reads the
+//    SAME record address -> LDS broadcast, conflict-free; each record read serves R rows;
+//  * per-tile partial accumulators are folded into running totals once per tile
+//    (two-level summation: fp32 error ~ (sqrt(256)+sqrt(N/256)) ulp instead of ~sqrt(N));
+//  * when M alone cannot fill 256 CUs x several waves, the column range is split over
+//    gridDim.y chunks; each chunk writes its own partial slab and a second tiny kernel
+//    sums the slabs in chunk order: no float atomics, bitwise-deterministic results;
+//  * the Gaussian exponential is one v_exp_f32 (exp2) with log2(e)/(2 sigma^2) folded
+//    into a single multiplier.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dicp {
+
+constexpr int kBlock = 256;       // threads per workgroup (4 waves)
+constexpr int kTile = 256;        // column records per LDS tile (one per thread)
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+
+// Scalars every pair op may need.  nc = -log2(e)/(2 sigma^2): K = exp2(nc * |z|^2).
+struct Scal {
+  float nc;    // exp2 multiplier
+  float s;     // 1/sigma^2
+  float eta;   // gradcomponent weight (0 or 1/lambda)
+  float aux0;  // op-specific
+  float aux1;  // op-specific
+  const float* dev0;  // op-specific device scalar (e.g. cotangent of the divergence sum)
+};
+
+// Row / column pointers of one pass (meaning fixed per op).
+struct Args {
+  const float* r0;
+  const float* r1;
+  const float* r2;
+  const float* r3;
+  const float* c0;
+  const float* c1;
+  const float* c2;
+  const float* c3;
+};
+
+// Output descriptor: up to 4 output arrays, each (rows, width) row-major.
+// In split mode the kernel writes partial slab `blockIdx.y` of each output at
+// out[k] + blockIdx.y * rows * width[k]; accumulate[k] = 1 means out[k] += value
+// (only honoured when not split; the merge kernel honours it otherwise).
+struct Outs {
+  float* ptr[4];
+  int accumulate[4];
+};
+
+template <int W>
+struct Vec {
+  float v[W];
+};
+
+// ------------------------------------------------------------------------------------
+// Generic tiled row-reduction kernel.
+//   Op::D, Op::CW4 (float4 per column record), Op::NACC (accumulators per row)
+//   Op::Row                        -- per-row state (registers)
+//   Op::load_row(args, i, Row&)    -- read row i
+//   Op::load_col(args, j, float* rec)  -- write column j's record (CW4*4 floats) into LDS
+//   Op::pair(const Scal&, const Row&, const float* rec, float* acc)
+//   Op::store(const Scal&, const Row&, const float* tot, float* vals) -> per-output values;
+//       vals laid out as the concatenation of the outputs' widths Op::kOutW[0..kNOut).
+//   Op::kMin -> accumulate by min instead of sum.
+// ------------------------------------------------------------------------------------
+template <class Op, int R>
+__global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
+                                                        int64_t M, int64_t N, int64_t chunk,
+                                                        Outs outs) {
+  constexpr int CW4 = Op::CW4;
+  constexpr int NACC = Op::NACC;
+  constexpr bool MIN = Op::kMin;
+  __shared__ float4 lds[kTile * CW4];
+  if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];  // device-resident scalar (no host sync)
+
+  const int tid = threadIdx.x;
+  const int64_t ibase = (int64_t)blockIdx.x * (kBlock * R) + tid;
+
+  typename Op::Row row[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int64_t i = ibase + (int64_t)r * kBlock;
+    if (i >= M) i = M - 1;
+    Op::load_row(args, i, row[r]);
+  }
+
+  float tot[R][NACC];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) tot[r][k] = MIN ? __builtin_huge_valf() : 0.f;
+
+  const int64_t j0 = (int64_t)blockIdx.y * chunk;
+  int64_t j1 = j0 + chunk;
+  if (j1 > N) j1 = N;
+
+  for (int64_t jt = j0; jt < j1; jt += kTile) {
+    const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
+    if (tid < cnt) Op::load_col(args, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+    __syncthreads();
+    float acc[R][NACC];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int k = 0; k < NACC; ++k) acc[r][k] = MIN ? __builtin_huge_valf() : 0.f;
+
+#pragma unroll 2
+    for (int t = 0; t < cnt; ++t) {
+      float rec[CW4 * 4];
+#pragma unroll
+      for (int k = 0; k < CW4; ++k) {
+        const float4 q = lds[t * CW4 + k];
+        rec[4 * k + 0] = q.x;
+        rec[4 * k + 1] = q.y;
+        rec[4 * k + 2] = q.z;
+        rec[4 * k + 3] = q.w;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) Op::pair(sc, row[r], rec, acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int k = 0; k < NACC; ++k)
+        tot[r][k] = MIN ? fminf(tot[r][k], acc[r][k]) : tot[r][k] + acc[r][k];
+    __syncthreads();
+  }
+
+  const bool split = gridDim.y > 1;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = ibase + (int64_t)r * kBlock;
+    if (i >= M) continue;
+    float vals[Op::kOutW[0] + Op::kOutW[1] + Op::kOutW[2] + Op::kOutW[3]];
+    Op::store(sc, row[r], tot[r], vals);
+    int off = 0;
+#pragma unroll
+    for (int k = 0; k < Op::kNOut; ++k) {
+      const int w = Op::kOutW[k];
+      float* base = outs.ptr[k];
+      if (base != nullptr) {
+        if (split) {
+          float* dst = base + (int64_t)blockIdx.y * M * w + i * w;
+#pragma unroll
+          for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
+        } else if (outs.accumulate[k]) {
+          float* dst = base + i * w;
+#pragma unroll
+          for (int e = 0; e < w; ++e) dst[e] += vals[off + e];
+        } else {
+          float* dst = base + i * w;
+#pragma unroll
+          for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
+        }
+      }
+      off += w;
+    }
+  }
+}
+
+// Fixed-order merge of split partial slabs: dst[e] (+)= sum_{s<S} slab[s][e]  (or min).
+template <bool MIN>
+__global__ __launch_bounds__(kBlock) void merge_slabs_kernel(const float* __restrict__ slab,
+                                                             int64_t n, int S, float* dst,
+                                                             int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  float a = slab[e];
+  for (int s = 1; s < S; ++s) {
+    const float b = slab[(int64_t)s * n + e];
+    a = MIN ? fminf(a, b) : a + b;
+  }
+  dst[e] = accumulate ? dst[e] + a : a;
+}
+
+}  // namespace dicp

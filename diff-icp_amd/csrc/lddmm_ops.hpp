@@ -1,0 +1,597 @@
+// Pair operators of the Gaussian-kernel reductions and of the fused LDDMM ODE, plugged
+// into dicp::rowred_kernel (common.hpp).  Each struct states the reference formula it
+// computes (diffICP/tools/kernel.py, diffICP/core/LDDMM.py) and its per-pair algorithmic
+// cost (FMA = 2 flop, exp2 = 1 transcendental) used by the roofline accounting.
+//
+// Row i carries x_i (and row weights), column j carries y_j (and column weights);
+// z = x_i - y_j, r2 = |z|^2, K = exp2(nc r2) = exp(-r2/(2 sigma^2)), s = 1/sigma^2.
+#pragma once
+#include "common.hpp"
+
+namespace dicp {
+
+template <int D>
+__device__ __forceinline__ float diff_sq(const float* __restrict__ x, const float* __restrict__ y,
+                                         float* __restrict__ z) {
+  float r2 = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    z[d] = x[d] - y[d];
+    r2 = fmaf(z[d], z[d], r2);
+  }
+  return r2;
+}
+
+template <int D>
+__device__ __forceinline__ float dot(const float* __restrict__ a, const float* __restrict__ b) {
+  float r = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) r = fmaf(a[d], b[d], r);
+  return r;
+}
+
+template <int W>
+__device__ __forceinline__ void ld(const float* __restrict__ p, int64_t i, float* dst) {
+#pragma unroll
+  for (int d = 0; d < W; ++d) dst[d] = p[i * W + d];
+}
+
+constexpr int cw4(int floats) { return (floats + 3) / 4; }
+
+// -------------------------------------------------------------------------------------
+// The ten GenKernel reductions (kernel.py:127-168 KeOps, :177-215/:259-292 torch).
+// -------------------------------------------------------------------------------------
+
+// KBase: X_i = sum_j K(x_i - y_j)                         kernel.py:131 / :178-179
+template <int D>
+struct OpKBase {
+  static constexpr int CW4 = cw4(D), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) { ld<D>(a.c0, j, rec); }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float r2 = diff_sq<D>(r.x, rec, z);
+    acc[0] += fast_exp2(sc.nc * r2);
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) { v[0] = t[0]; }
+};
+
+// KRedScal: X_i = sum_j K d_j                              kernel.py:135 / :182-183
+template <int D>
+struct OpKRedScal {
+  static constexpr int CW4 = cw4(D + 1), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    rec[D] = a.c1[j];
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float r2 = diff_sq<D>(r.x, rec, z);
+    acc[0] = fmaf(fast_exp2(sc.nc * r2), rec[D], acc[0]);
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) { v[0] = t[0]; }
+};
+
+// KRed: X_i = sum_j K b_j  (the velocity field v, LDDMM.py:114/116)   kernel.py:138 / :186-187
+// 3D cost: 3 sub + 3 fma (r2) + 1 mul + 1 exp + 3 fma = 15 flop + 1 T
+template <int D>
+struct OpKRed {
+  static constexpr int CW4 = cw4(2 * D), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + d], acc[d]);
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = t[d];
+  }
+};
+
+// GradKRed: X_i = sum_j (grad K)(x_i - y_j) = -s sum_j z K    kernel.py:142 / :190-191, :262-263
+template <int D>
+struct OpGradK {
+  static constexpr int CW4 = cw4(D), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) { ld<D>(a.c0, j, rec); }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, z[d], acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = -sc.s * t[d];
+  }
+};
+
+// GradKScal: X_i = sum_j -s z K d_j  (gradient of KBase / KRedScal w.r.t. x)
+template <int D>
+struct OpGradKScal {
+  static constexpr int CW4 = cw4(D + 1), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    rec[D] = a.c1[j];
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float Kd = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z)) * rec[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(Kd, z[d], acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = -sc.s * t[d];
+  }
+};
+
+// GradKRed_rev (column reduction, kernel.py:147 / :194-195) evaluated as a row reduction
+// over the former columns: Y_j = sum_i gradK(x_i - y_j).d_i = sum_i s ((y_j - x_i).d_i) K.
+// Called with rows = y, cols = (x, d):  X_i = s sum_j (z . b_j) K.
+template <int D>
+struct OpZDotB {
+  static constexpr int CW4 = cw4(2 * D), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+    acc[0] = fmaf(K, dot<D>(z, rec + D), acc[0]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+    v[0] = sc.s * t[0];
+  }
+};
+
+// DDKRed: X_i^d = sum_j -s z^d K b_j^d                  kernel.py:151 / :198-199
+template <int D>
+struct OpDDK {
+  static constexpr int CW4 = cw4(2 * D), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K * z[d], rec[D + d], acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = -sc.s * t[d];
+  }
+};
+
+// GenDKRed: X_i = sum_j -s z K (c_i . b_j)   (momentum update Gq, LDDMM.py:199)
+// kernel.py:155 / :202-203.  3D cost ~21 flop + 1 T.
+template <int D>
+struct OpGenDK {
+  static constexpr int CW4 = cw4(2 * D), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; float c[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.x);
+    ld<D>(a.r1, i, r.c);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+    const float w = K * dot<D>(r.c, rec + D);
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(w, z[d], acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = -sc.s * t[d];
+  }
+};
+
+// HessKRed: X_i = sum_j [s^2 (z.u) z - s u] K,  u = c_i - b_j     kernel.py:160 / :284-286
+template <int D>
+struct OpHessK {
+  static constexpr int CW4 = cw4(2 * D), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; float c[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.x);
+    ld<D>(a.r1, i, r.c);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D], u[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+#pragma unroll
+    for (int d = 0; d < D; ++d) u[d] = r.c[d] - rec[D + d];
+    const float zu = sc.s * dot<D>(z, u);
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, fmaf(zu, z[d], -u[d]), acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = sc.s * t[d];
+  }
+};
+
+// LapKRed: X_i = sum_j (s^2 r2 - D s) K                 kernel.py:164 / :206-207, :265-267
+template <int D>
+struct OpLapK {
+  static constexpr int CW4 = cw4(D), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) { ld<D>(a.c0, j, rec); }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float r2 = diff_sq<D>(r.x, rec, z);
+    const float K = fast_exp2(sc.nc * r2);
+    acc[0] = fmaf(K, fmaf(sc.s, r2, -(float)D), acc[0]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+    v[0] = sc.s * t[0];
+  }
+};
+
+// GradLapKRed: X_i = sum_j -z (s^3 r2 - (D+2) s^2) K     kernel.py:168 / :289-292
+// (aux0 = 1: plain; GradLapKScal multiplies by a column weight d_j)
+template <int D, bool SCAL>
+struct OpGradLapK {
+  static constexpr int CW4 = cw4(D + (SCAL ? 1 : 0)), NACC = D, kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    if (SCAL) rec[D] = a.c1[j];
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float r2 = diff_sq<D>(r.x, rec, z);
+    float w = fast_exp2(sc.nc * r2) * fmaf(sc.s, r2, -(float)(D + 2));
+    if (SCAL) w *= rec[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(w, z[d], acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+    const float s2 = sc.s * sc.s;
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = -s2 * t[d];
+  }
+};
+
+// min_j |x_i - y_j|^2  (GaussKernel.check_coverage, kernel.py:324-329)
+template <int D>
+struct OpMinSqDist {
+  static constexpr int CW4 = cw4(D), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = true;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) { ld<D>(a.c0, j, rec); }
+  __device__ static void pair(const Scal&, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    acc[0] = fminf(acc[0], diff_sq<D>(r.x, rec, z));
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) { v[0] = t[0]; }
+};
+
+// -------------------------------------------------------------------------------------
+// Fused LDDMM ODE right-hand side on the support points (LDDMMModel.ODE, LDDMM.py:176-227).
+// Rows and columns are both (q, p).  One exp per pair feeds every term.
+//
+// ETA=false (classic / hybrid, eta = 0):
+//   V = sum K p_j,  Z = sum K z,  Gs = sum K z (p_i.p_j)
+//   v = V ; mG = -GenDKRed = s Gs ; g = p_i . GradKRed_i = -s p_i.Z ; h = 1/2 p_i.V
+// ETA=true (logdet, eta = 1/lambda), additionally with u = p_i - p_j:
+//   Hs = sum K [s (z.u) z - u]   (HessKRed = s Hs),   GL = sum K z (s r2 - (D+2))
+//   (GradLapKRed = -s^2 GL),  L = sum K (s r2 - D)  (LapKRed = s L)
+//   v  = V + eta s Z                                             (LDDMM.py:114)
+//   mG = s Gs + eta s Hs - eta^2 s^2 GL                          (LDDMM.py:201-203)
+//   g  = -s p_i.Z + eta s L                                      (LDDMM.py:135)
+//   h  = 1/2 p_i.V + eta s p_i.Z - 1/2 eta^2 s L                 (LDDMM.py:151-153)
+// 3D cost (ETA=false, DIV=true): ~36 flop + 1 T per pair.
+// -------------------------------------------------------------------------------------
+template <int D, bool ETA, bool DIV>
+struct OpOdeSelfFwd {
+  static constexpr int CW4 = cw4(2 * D);
+  static constexpr int NACC = ETA ? (5 * D + 1) : (DIV ? 3 * D : 2 * D);
+  static constexpr int kNOut = 4;
+  static constexpr int kOutW[4] = {D, D, 1, 1};
+  static constexpr bool kMin = false;
+  struct Row { float q[D]; float p[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.q);
+    ld<D>(a.r1, i, r.p);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float r2 = diff_sq<D>(r.q, rec, z);
+    const float K = fast_exp2(sc.nc * r2);
+    const float* pj = rec + D;
+    const float Kpp = K * dot<D>(r.p, pj);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, pj[d], acc[d]);           // V
+      acc[D + d] = fmaf(Kpp, z[d], acc[D + d]);  // Gs
+    }
+    if (ETA || DIV) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[2 * D + d] = fmaf(K, z[d], acc[2 * D + d]);  // Z
+    }
+    if (ETA) {
+      float u[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) u[d] = r.p[d] - pj[d];
+      const float szu = sc.s * dot<D>(z, u);
+      const float sr2 = sc.s * r2;
+      const float KGL = K * (sr2 - (float)(D + 2));
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        acc[3 * D + d] = fmaf(K, fmaf(szu, z[d], -u[d]), acc[3 * D + d]);  // Hs
+        acc[4 * D + d] = fmaf(KGL, z[d], acc[4 * D + d]);                   // GL
+      }
+      acc[5 * D] = fmaf(K, sr2 - (float)D, acc[5 * D]);  // L
+    }
+  }
+  __device__ static void store(const Scal& sc, const Row& r, const float* t, float* v) {
+    const float s = sc.s, eta = sc.eta;
+    const float* V = t;
+    const float* Gs = t + D;
+    const float* Z = t + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (ETA) {
+        v[d] = fmaf(eta * s, Z[d], V[d]);
+        v[D + d] = s * Gs[d] + eta * s * t[3 * D + d] - eta * eta * s * s * t[4 * D + d];
+      } else {
+        v[d] = V[d];
+        v[D + d] = s * Gs[d];
+      }
+    }
+    const float pV = dot<D>(r.p, V);
+    if (ETA) {
+      const float pZ = dot<D>(r.p, Z);
+      const float L = t[5 * D];
+      v[2 * D] = -s * pZ + eta * s * L;
+      v[2 * D + 1] = 0.5f * pV + eta * s * pZ - 0.5f * eta * eta * s * L;
+    } else {
+      v[2 * D] = DIV ? -s * dot<D>(r.p, Z) : 0.f;
+      v[2 * D + 1] = 0.5f * pV;
+    }
+  }
+};
+
+// -------------------------------------------------------------------------------------
+// VJP of OpOdeSelfFwd (eta = 0): cotangents a = dL/dv, bm = dL/dmG, gam = dL/d(sum g).
+// Row m, column j, z = q_m - q_j (derivation in DESIGN.md, verified against torch
+// autograd of the reference formulas in tests/test_ode_grad.py):
+//   gp_m = sum_j K [ a_j + s ((bm_m - bm_j).z) p_j - s gam z ]
+//   gq_m = s sum_j K [ (p_m.p_j)(bm_m - bm_j) - gam (p_m - p_j)
+//                      + z ( s (gam (p_m-p_j).z - (p_m.p_j)(bm_m-bm_j).z) - (a_m.p_j + a_j.p_m) ) ]
+// 3D cost ~80 flop + 1 T per pair.
+// -------------------------------------------------------------------------------------
+template <int D>
+struct OpOdeSelfBwd {
+  static constexpr int CW4 = cw4(4 * D);
+  static constexpr int NACC = 2 * D;
+  static constexpr int kNOut = 2;
+  static constexpr int kOutW[4] = {D, D, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float q[D]; float p[D]; float a[D]; float b[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.q);
+    ld<D>(a.r1, i, r.p);
+    ld<D>(a.r2, i, r.a);
+    ld<D>(a.r3, i, r.b);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+    ld<D>(a.c2, j, rec + 2 * D);
+    ld<D>(a.c3, j, rec + 3 * D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    const float s = sc.s, gam = sc.aux0;
+    float z[D], db[D], dp[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.q, rec, z));
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      db[d] = r.b[d] - bj[d];
+      dp[d] = r.p[d] - pj[d];
+    }
+    const float pp = dot<D>(r.p, pj);
+    const float ap = dot<D>(r.a, pj) + dot<D>(aj, r.p);
+    const float zb = dot<D>(z, db);
+    const float zp = dot<D>(z, dp);
+    const float t1 = K * s * zb;
+    const float t2 = K * s * gam;
+    const float w = s * (gam * zp - pp * zb) - ap;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, aj[d], fmaf(t1, pj[d], fmaf(-t2, z[d], acc[d])));            // gp
+      const float e = fmaf(pp, db[d], fmaf(-gam, dp[d], w * z[d]));
+      acc[D + d] = fmaf(K, e, acc[D + d]);                                           // gq / s
+    }
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      v[d] = sc.s * t[D + d];  // gq
+      v[D + d] = t[d];         // gp
+    }
+  }
+};
+
+// -------------------------------------------------------------------------------------
+// External points x carried by the flow (LDDMM.py:219-227): rows x_i, columns (q_j, p_j).
+//   vx = sum K p_j + eta s sum K z                           (v(x,q,p), LDDMM.py:114)
+//   gx = s sum K (z.p_j) + eta s sum K (s r2 - D)            (row form of mdivsum(x,q,p),
+//        LDDMM.py:135: sum_j p_j.sum_k gradK(q_j - x_k) = sum_k sum_j s ((x_k-q_j).p_j) K)
+// -------------------------------------------------------------------------------------
+template <int D, bool ETA, bool DIV>
+struct OpOdeExtFwd {
+  static constexpr int CW4 = cw4(2 * D);
+  static constexpr int NACC = D + (DIV ? 1 : 0) + (ETA ? D + 1 : 0);
+  static constexpr int kNOut = 2;
+  static constexpr int kOutW[4] = {D, 1, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float r2 = diff_sq<D>(r.x, rec, z);
+    const float K = fast_exp2(sc.nc * r2);
+    const float* pj = rec + D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, pj[d], acc[d]);
+    if (DIV) acc[D] = fmaf(K, dot<D>(z, pj), acc[D]);
+    if (ETA) {
+      constexpr int o = D + (DIV ? 1 : 0);
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[o + d] = fmaf(K, z[d], acc[o + d]);
+      acc[o + D] = fmaf(K, fmaf(sc.s, r2, -(float)D), acc[o + D]);
+    }
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+    const float s = sc.s, eta = sc.eta;
+    constexpr int o = D + (DIV ? 1 : 0);
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = ETA ? fmaf(eta * s, t[o + d], t[d]) : t[d];
+    float g = DIV ? s * t[D] : 0.f;
+    if (ETA && DIV) g += eta * s * t[o + D];
+    v[D] = g;
+  }
+};
+
+// VJP of OpOdeExtFwd w.r.t. x (eta = 0): rows x_i (+ cotangent a_i), columns (q_j, p_j).
+//   gx_i = s sum_j K [ gam p_j - z ( a_i.p_j + s gam (z.p_j) ) ]
+template <int D>
+struct OpOdeExtBwdX {
+  static constexpr int CW4 = cw4(2 * D);
+  static constexpr int NACC = D;
+  static constexpr int kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; float a[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.x);
+    ld<D>(a.r1, i, r.a);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    const float gam = sc.aux0;
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.x, rec, z));
+    const float* pj = rec + D;
+    const float w = dot<D>(r.a, pj) + sc.s * gam * dot<D>(z, pj);
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, fmaf(gam, pj[d], -w * z[d]), acc[d]);
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = sc.s * t[d];
+  }
+};
+
+// VJP of OpOdeExtFwd w.r.t. (q, p) (eta = 0), as a row reduction over the support rows
+// q_j (+ p_j) against columns (x_i, a_i); z' = q_j - x_i:
+//   gp_j = sum_i K [ a_i - s gam z' ]
+//   gq_j = -s sum_i K [ z' (a_i.p_j - s gam (z'.p_j)) + gam p_j ]
+template <int D>
+struct OpOdeExtBwdQ {
+  static constexpr int CW4 = cw4(2 * D);
+  static constexpr int NACC = 2 * D;
+  static constexpr int kNOut = 2;
+  static constexpr int kOutW[4] = {D, D, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float q[D]; float p[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.q);
+    ld<D>(a.r1, i, r.p);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    const float s = sc.s, gam = sc.aux0;
+    float z[D];
+    const float K = fast_exp2(sc.nc * diff_sq<D>(r.q, rec, z));
+    const float* ai = rec + D;
+    const float sg = s * gam;
+    const float w = dot<D>(ai, r.p) - sg * dot<D>(z, r.p);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, fmaf(-sg, z[d], ai[d]), acc[d]);                 // gp
+      acc[D + d] = fmaf(K, fmaf(w, z[d], gam * r.p[d]), acc[D + d]);    // -gq/s
+    }
+  }
+  __device__ static void store(const Scal& sc, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      v[d] = -sc.s * t[D + d];  // gq
+      v[D + d] = t[d];          // gp
+    }
+  }
+};
+
+}  // namespace dicp

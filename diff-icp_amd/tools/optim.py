@@ -1,0 +1,70 @@
+"""L-BFGS wrapper with divergence fallback (semantics of diffICP/tools/optim.py:10-110).
+
+Kept on torch.optim.LBFGS (host-side optimizer logic, O(M) vector ops on the device); the
+closure's cost is the HIP shooting + its fused backward.
+"""
+import math
+
+import torch
+
+
+def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
+    """Returns (best_p list, best_L, nsteps, change) exactly as optim.py:10-110:
+    L-BFGS(max_iter=20, max_eval=100, history_size=100, strong_wolfe) steps; on NaN /
+    increase / > errthresh fall back to the best parameters seen (or a 1% random
+    perturbation) and restart without line search; stop when the RMS parameter change is
+    below tol x RMS parameter value."""
+    p = [a.clone().contiguous().detach().requires_grad_(True) for a in p0]
+    optimizer = torch.optim.LBFGS(p, max_iter=20, max_eval=100, history_size=100,
+                                  line_search_fn="strong_wolfe")
+    iter_L, best_L, best_p = [], math.inf, None
+
+    def closure():
+        nonlocal best_L, best_p
+        optimizer.zero_grad()
+        L = lossfunc(*p)
+        Ld = L.detach().item()
+        iter_L.append(Ld)
+        if Ld < best_L:
+            best_L = Ld
+            best_p = [a.clone().detach() for a in p]
+        L.backward()
+        return L
+
+    i, keepOn, L = 0, True, math.inf
+    change = None
+    while i < nmax and keepOn:
+        i += 1
+        p_prev = [a.clone().detach() for a in p]
+        optimizer.step(closure)
+        Lprev, L = L, iter_L[-1]
+        if L > Lprev or L > errthresh or math.isnan(L):
+            if math.isnan(L):
+                print("WARNING: NaN value for loss L during L-BFGS optimization.")
+            elif L > errthresh:
+                print("WARNING: Aberrantly large value for loss L during L-BFGS optimization.")
+            elif L > Lprev:
+                print("WARNING: Increase of loss L during L-BGFS optimization.")
+            if best_L < Lprev:
+                p = [a.clone() for a in best_p]
+                L = best_L
+                print("L-BFGS optimization. Found an intermediate 'best_p' value for this iteration.")
+            else:
+                rmod = 0.01
+                p = [a + rmod * a.std() * torch.randn(a.shape, dtype=a.dtype, device=a.device)
+                     for a in best_p]
+                L = lossfunc(*p)
+                print("L-BFGS optimization. Trying a random perturbation of parameter from its "
+                      f"current value, with relative strength {rmod}.")
+            change = "None (divergent iteration step)"
+            p = [a.detach().requires_grad_(True) for a in p]
+            optimizer = torch.optim.LBFGS(p, max_iter=20, max_eval=100, history_size=100,
+                                          line_search_fn=None)
+        else:
+            changes = [((a - a_prev) ** 2).mean().sqrt().detach().cpu().numpy()
+                       for a, a_prev in zip(p, p_prev)]
+            refs = [(a_prev ** 2).mean().sqrt().detach().cpu().numpy() for a_prev in p_prev]
+            keepOn = any(c > tol * r for c, r in zip(changes, refs))
+            change = max(changes)
+    best_p = [a.detach() for a in best_p]
+    return best_p, best_L, i, change

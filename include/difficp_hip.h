@@ -1,0 +1,170 @@
+/*
+ * difficp_hip.h -- C-ABI of the MI355X (gfx950) hot path of diff-ICP.
+ *
+ * This library replaces the KeOps-generated (JIT CUDA) reductions that the reference
+ * binds at two seams:
+ *   - GenKernel.set_computversion (diffICP/tools/kernel.py:91-110) which binds the ten
+ *     Gaussian-kernel reductions KBase ... GradKRed_rev (kernel.py:127-168 KeOps formulas,
+ *     :177-215 torch restatement);
+ *   - GaussianMixtureUnif.set_computversion (diffICP/core/GMM.py:126-144) which binds
+ *     EM_step (torch: GMM.py:236-325, KeOps: GMM.py:402-529).
+ * plus the LDDMM ODE right-hand side that the reference builds from those reductions
+ * (LDDMMModel.ODE, diffICP/core/LDDMM.py:176-227) and its autograd backward
+ * (optim.py:46 `L.backward()`), which the reference gets from KeOps autodiff.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a caller-owned DEVICE buffer, row-major float32, contiguous;
+ *   - nothing is allocated inside; scratch space is passed in `ws` (size from
+ *     dicp_workspace_bytes) -- the call is hipGraph-capturable;
+ *   - every call is stream-ordered on `stream` and never synchronises the host;
+ *   - return 0 on success, else a nonzero code; dicp_last_error() gives a message
+ *     (thread-local).  Unsupported D or op -> DICP_ERR_UNSUPPORTED.
+ *   - results are deterministic: no float atomics; split-column partial sums are
+ *     reduced in a fixed order.
+ *
+ * Notation: i = row ("target", KeOps Vi), j = column ("source", KeOps Vj);
+ *   z = x_i - y_j,  K = exp(-|z|^2 / (2 sigma^2)),  s = 1/sigma^2.
+ */
+#ifndef DIFFICP_HIP_H
+#define DIFFICP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dicp_stream_t; /* a hipStream_t (NULL = legacy default stream) */
+
+enum dicp_status {
+  DICP_OK = 0,
+  DICP_ERR_INVALID = 1,     /* bad sizes / null pointers */
+  DICP_ERR_UNSUPPORTED = 2, /* D or op not compiled in */
+  DICP_ERR_WORKSPACE = 3,   /* ws too small */
+  DICP_ERR_HIP = 4          /* a HIP launch error (message has hipGetErrorString) */
+};
+
+/* ------------------------------------------------------------------------------------
+ * Gaussian-kernel reductions (GenKernel aliases, kernel.py:100-107).
+ * ---------------------------------------------------------------------------------- */
+enum dicp_red_op {
+  DICP_KBASE = 0,      /* out_i   = sum_j K                          (M,)  kernel.py:131,178 */
+  DICP_KREDSCAL = 1,   /* out_i   = sum_j K d_j        b=d (N,)      (M,)  kernel.py:135,182 */
+  DICP_KRED = 2,       /* out_i   = sum_j K b_j        b (N,D)       (M,D) kernel.py:138,186 */
+  DICP_GRADK = 3,      /* out_i   = sum_j -s z K                     (M,D) kernel.py:142,190 */
+  DICP_GRADK_REV = 4,  /* out_j   = sum_i grad K(x_i-y_j).d_i; call with (x=y_rows, y=x_cols,
+                          b=d (N,D)); computes out_i = sum_j s (z.b_j) K  (M,) kernel.py:147,194 */
+  DICP_DDK = 5,        /* out_i^d = sum_j -s z^d K b_j^d             (M,D) kernel.py:151,198 */
+  DICP_GENDK = 6,      /* out_i   = sum_j -s z K (c_i.b_j)  c (M,D)  (M,D) kernel.py:155,202 */
+  DICP_HESSK = 7,      /* out_i   = sum_j [s^2 (z.u) z - s u] K, u=c_i-b_j (M,D) kernel.py:160,284 */
+  DICP_LAPK = 8,       /* out_i   = sum_j (s^2|z|^2 - D s) K         (M,)  kernel.py:164,206 */
+  DICP_GRADLAPK = 9,   /* out_i   = sum_j -z (s^3|z|^2-(D+2)s^2) K   (M,D) kernel.py:168,289 */
+  DICP_GRADKSCAL = 10, /* out_i   = sum_j -s z K d_j    b=d (N,)     (M,D) (autograd of KBase/KRedScal) */
+  DICP_GRADLAPKSCAL = 11, /* out_i = sum_j -z (s^3|z|^2-(D+2)s^2) K d_j (M,D) (autograd of LapKRed) */
+  DICP_MIN_SQDIST = 12 /* out_i   = min_j |z|^2                      (M,)  check_coverage kernel.py:324-329 */
+};
+
+/* One reduction.  x (M,D) rows, y (N,D) columns, b column weights ((N,D) or (N,) or NULL),
+ * c row weights ((M,D) or NULL), out (M,D) or (M,) as listed above.
+ * Replaces the bound aliases GK.KBase ... GK.GradKRed_rev (kernel.py:100-107). */
+int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float* y, int64_t N, int D,
+                       const float* b, const float* c, double sigma, float* out, void* ws,
+                       size_t ws_bytes, dicp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * LDDMM geodesic-shooting ODE (LDDMMModel.ODE, LDDMM.py:176-227), fused: one pass over
+ * the M x M support pairs produces every self-interaction term with one exp per pair.
+ *   v_i   = sum_j K p_j - eta grad K                                  (LDDMM.py:100-116)
+ *   mG_i  = -(GenDKRed(q,q,p,p) - eta HessKRed - eta^2 GradLapKRed)   (LDDMM.py:198-203)
+ *           (the ODE returns -Gq, so mG is exactly dp/dt)
+ *   g_i   = p_i . GradKRed(q,q)_i + eta LapKRed(q,q)_i  (per-row terms of mdivsum, LDDMM.py:133-138;
+ *           sum_i g_i = mdivsum(q,q,p))
+ *   h_i   = per-row terms of the Hamiltonian (LDDMM.py:150-155); sum_i h_i = H(q,p)
+ * g and h may be NULL (not computed).  eta = 0 (classic/hybrid) or 1/lambda (logdet).
+ * ---------------------------------------------------------------------------------- */
+int dicp_lddmm_ode_self_fwd_f32(const float* q, const float* p, int64_t M, int D, double sigma,
+                                double eta, float* v, float* mG, float* g, float* h, void* ws,
+                                size_t ws_bytes, dicp_stream_t stream);
+
+/* Vector-Jacobian product of the fused self ODE (what KeOps autodiff provides at
+ * optim.py:46).  Cotangents: gv (M,D) on v, gmG (M,D) on mG, and gdiv = cotangent of
+ * sum_i g_i, a DEVICE scalar (may be NULL = 0).  Outputs gq, gp (M,D), overwritten. */
+int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const float* gv,
+                                const float* gmG, const float* gdiv, int64_t M, int D,
+                                double sigma, double eta, float* gq, float* gp, void* ws,
+                                size_t ws_bytes, dicp_stream_t stream);
+
+/* External data points x (N,D) carried by the flow (LDDMM.py:219-227):
+ *   vx_i = v(x_i) (LDDMM.py:226), gx_i = per-row terms of mdivsum(x,q,p) (LDDMM.py:223),
+ *   summed in row (x) order; gx may be NULL. */
+int dicp_lddmm_ode_ext_fwd_f32(const float* x, int64_t N, const float* q, const float* p,
+                               int64_t M, int D, double sigma, double eta, float* vx, float* gx,
+                               void* ws, size_t ws_bytes, dicp_stream_t stream);
+
+/* VJP of the external-point terms.  Cotangents gvx (N,D) on vx and device scalar gdiv on
+ * sum_i gx_i.  Writes gxo (N,D) (gradient w.r.t. x) and ACCUMULATES into gq, gp (M,D)
+ * (gradient w.r.t. the support points / momenta), so it can follow the self backward. */
+int dicp_lddmm_ode_ext_bwd_f32(const float* x, int64_t N, const float* q, const float* p,
+                               int64_t M, int D, double sigma, double eta, const float* gvx,
+                               const float* gdiv, float* gxo, float* gq, float* gp, void* ws,
+                               size_t ws_bytes, dicp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
+ * GMM EM step reductions (GaussianMixtureUnif.EM_step_torch, GMM.py:236-325).
+ * log2-domain internally; outputs in natural log.
+ * ---------------------------------------------------------------------------------- */
+
+/* The C-sized column vectors are precomputed by the caller on the device (they are
+ * O(C) torch ops): w2_c = (w_c - LSE(w)) * log2(e), mu2_c = |mu_c|^2, lpi_c = w_c - LSE(w).
+ * Internally logits are kept in the log2 domain: t2_nc = w2_c - |x_n-mu_c|^2 log2(e)/(2 sigma^2).
+ *
+ * E-step row pass over points n (rows X (N,D)) against components (mu (C,D)):
+ *   T[n]  = LSE_c t_nc = ln2 * T2[n] - lgn,  lgn = D (log sigma + 0.5 log 2 pi)   (GMM.py:263-270)
+ *   T2[n] = log2 sum_c 2^t2_nc  (consumed by the M-step and targets passes; may be NULL)
+ * if stats != NULL also the responsibility-weighted row sums (gamma = exp(t - T)):
+ *   stats[n*(D+4) + ...] = { sum_c gamma mu_c (D), sum_c gamma |mu_c|^2,
+ *                            sum_c gamma lgamma, sum_c gamma lpi_c, sum_c gamma D2_nc }
+ *   (Y with the current mu GMM.py:303; Cfe terms :312-314; NDsigma2 with the old mu :296). */
+int dicp_gmm_estep_f32(const float* X, int64_t N, const float* mu, const float* w2,
+                       const float* mu2, int64_t C, int D, double sigma, double lgn, float* T,
+                       float* T2, float* stats, void* ws, size_t ws_bytes, dicp_stream_t stream);
+
+/* M-step column pass over components c (evaluated as a row pass, log domain, robust for
+ * empty components like softmax(lgamma, dim=0)):
+ *   colstats[c*(D+1) + ...] = { log sum_n gamma_nc          (= new w_c,  GMM.py:293),
+ *                               sum_n gamma_nc x_n / sum_n gamma_nc (D)  (= new mu_c, GMM.py:287) } */
+int dicp_gmm_mstep_f32(const float* X, const float* T2, int64_t N, const float* mu,
+                       const float* w2, int64_t C, int D, double sigma, float* colstats,
+                       void* ws, size_t ws_bytes, dicp_stream_t stream);
+
+/* Targets / free-energy row pass with OLD responsibilities and NEW parameters
+ * (GMM.py:303-314): gamma from (mu_old, w2_old, sigma_old, T2) against mu_new, lpi_new:
+ *   rows[n*(D+4) + ...] = { Y_n = sum_c gamma mu_new_c (D), sum_c gamma |mu_new_c|^2,
+ *                           sum_c gamma lpi_new_c, sum_c gamma, sum_c gamma |x_n - mu_new_c|^2 } */
+int dicp_gmm_targets_f32(const float* X, const float* T2, int64_t N, const float* mu_old,
+                         const float* w2_old, double sigma_old, const float* mu_new,
+                         const float* lpi_new, int64_t C, int D, float* rows, void* ws,
+                         size_t ws_bytes, dicp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Scratch bytes needed by entry `kind` (one of the DICP_WS_* below) at these sizes.
+ * LDDMM kinds: M = support points, N = columns (RED) or external points (EXT).
+ * GMM kinds: M = data points N, N = components C. */
+enum dicp_ws_kind {
+  DICP_WS_RED = 0, DICP_WS_ODE_SELF_FWD = 1, DICP_WS_ODE_SELF_BWD = 2, DICP_WS_ODE_EXT_FWD = 3,
+  DICP_WS_ODE_EXT_BWD = 4, DICP_WS_GMM_ESTEP = 5, DICP_WS_GMM_MSTEP = 6, DICP_WS_GMM_TARGETS = 7
+};
+size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D);
+
+const char* dicp_last_error(void);
+const char* dicp_version(void);
+/* 1 if D is compiled in. */
+int dicp_supports_dim(int D);
+/* Number of column splits the library will use for an M x N pass (diagnostics/bench). */
+int dicp_num_splits(int kind, int64_t M, int64_t N);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIFFICP_HIP_H */

@@ -1,0 +1,181 @@
+"""TEST-ONLY executable spec of the C-ABI contract (include/difficp_hip.h), backed by the
+CPU oracle.  `install(monkeypatch)` replaces the entry points of difficp_amd._lib so the
+host-side logic (shooting adjoint, EM bookkeeping, PSR driver, sharded gloo path) can be
+tested on CPU.  Never used by the product: difficp_amd raises without the HIP library.
+"""
+import math
+
+import torch
+
+from oracle import torch_ref as R
+
+LOG2E = 1.4426950408889634
+LN2 = math.log(2.0)
+
+
+def _d(t):
+    return None if t is None else t.detach().double()
+
+
+def _out(t, like):
+    return t.to(dtype=torch.float32, device=like.device).contiguous()
+
+
+def gauss_red(op, x, y, sigma, b=None, c=None):
+    from difficp_amd import _lib as L
+    X, Y, B, Cc = _d(x), _d(y), _d(b), _d(c)
+    if op == L.KBASE:
+        r = R.KBase(X, Y, sigma)
+    elif op == L.KREDSCAL:
+        r = R.KRedScal(X, Y, B, sigma)
+    elif op == L.KRED:
+        r = R.KRed(X, Y, B, sigma)
+    elif op == L.GRADK:
+        r = R.GradKRed(X, Y, sigma)
+    elif op == L.GRADK_REV:          # rows = x here (former columns), cols = (y, b)
+        r = R.GradKRed_rev(Y, X, B, sigma)
+    elif op == L.DDK:
+        r = R.DDKRed(X, Y, B, sigma)
+    elif op == L.GENDK:
+        r = R.GenDKRed(X, Y, B, Cc, sigma)
+    elif op == L.HESSK:
+        r = R.HessKRed(X, Y, B, Cc, sigma)
+    elif op == L.LAPK:
+        r = R.LapKRed(X, Y, sigma)
+    elif op == L.GRADLAPK:
+        r = R.GradLapKRed(X, Y, sigma)
+    elif op == L.GRADKSCAL:
+        r = R._rows(lambda xc: torch.sum(R.GradK(xc, Y, sigma) * B[None, :, None], 1), X)
+    elif op == L.GRADLAPKSCAL:
+        D = X.shape[1]
+
+        def f(xc):
+            D2 = torch.sum((xc[:, None, :] - Y[None, :, :]) ** 2, -1)[:, :, None]
+            return torch.sum(torch.exp(-D2 / (2 * sigma ** 2)) * (Y[None, :, :] - xc[:, None, :])
+                             * (D2 / sigma ** 6 - (D + 2) / sigma ** 4) * B[None, :, None], 1)
+        r = R._rows(f, X)
+    elif op == L.MIN_SQDIST:
+        r = R.MinSqDist(X, Y) if Y.shape[0] else torch.full((X.shape[0],), float("inf"), dtype=torch.float64)
+    else:
+        raise NotImplementedError(op)
+    return _out(r, x)
+
+
+def _self_terms(q, p, sigma, eta):
+    s = 1.0 / sigma ** 2
+    KR = R.KRed(q, q, p, sigma)
+    GK = R.GradKRed(q, q, sigma)
+    LK = R.LapKRed(q, q, sigma)
+    v = KR - eta * GK
+    G = R.GenDKRed(q, q, p, p, sigma)
+    if eta != 0:
+        G = G - eta * R.HessKRed(q, q, p, p, sigma) - eta ** 2 * R.GradLapKRed(q, q, sigma)
+    g = (p * GK).sum(-1) + eta * LK
+    h = 0.5 * (p * KR).sum(-1) - eta * (p * GK).sum(-1) - 0.5 * eta ** 2 * LK
+    return v, -G, g, h
+
+
+def ode_self_fwd(q, p, sigma, eta, want_div, want_h=False):
+    v, mG, g, h = _self_terms(_d(q), _d(p), sigma, eta)
+    return (_out(v, q), _out(mG, q), _out(g, q) if (want_div or eta != 0) else None,
+            _out(h, q) if want_h else None)
+
+
+def ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta):
+    Q = _d(q).requires_grad_(True)
+    P = _d(p).requires_grad_(True)
+    with torch.enable_grad():
+        v, mG, g, _ = _self_terms(Q, P, sigma, eta)
+        L = (v * _d(gv)).sum() + (mG * _d(gmG)).sum()
+        if gdiv is not None:
+            L = L + g.sum() * _d(gdiv).reshape(-1)[0]
+        gq, gp = torch.autograd.grad(L, (Q, P))
+    return _out(gq, q), _out(gp, q)
+
+
+def _ext_terms(x, q, p, sigma, eta):
+    s = 1.0 / sigma ** 2
+    D = x.shape[1]
+    vx = R.KRed(x, q, p, sigma) - eta * R.GradKRed(x, q, sigma)
+    z = x[:, None, :] - q[None, :, :]
+    r2 = (z ** 2).sum(-1)
+    K = torch.exp(-r2 * s / 2)
+    gx = s * (K * (z * p[None, :, :]).sum(-1)).sum(1) + eta * s * (K * (s * r2 - D)).sum(1)
+    return vx, gx
+
+
+def ode_ext_fwd(x, q, p, sigma, eta, want_div):
+    vx, gx = _ext_terms(_d(x), _d(q), _d(p), sigma, eta)
+    return _out(vx, x), (_out(gx, x) if want_div else None)
+
+
+def ode_ext_bwd(x, q, p, gvx, gdiv, sigma, eta, gq, gp):
+    X = _d(x).requires_grad_(True)
+    Q = _d(q).requires_grad_(True)
+    P = _d(p).requires_grad_(True)
+    with torch.enable_grad():
+        vx, gx = _ext_terms(X, Q, P, sigma, eta)
+        L = (vx * _d(gvx)).sum()
+        if gdiv is not None:
+            L = L + gx.sum() * _d(gdiv).reshape(-1)[0]
+        ggx, ggq, ggp = torch.autograd.grad(L, (X, Q, P))
+    gq += _out(ggq, q)
+    gp += _out(ggp, q)
+    return _out(ggx, x)
+
+
+def gmm_estep(X, mu, w2, mu2, sigma, lgn, want_stats):
+    Xd, M, W2 = _d(X), _d(mu), _d(w2)
+    D2 = ((Xd[:, None, :] - M[None, :, :]) ** 2).sum(-1)
+    t2 = W2[None, :] - D2 * LOG2E / (2 * sigma ** 2)
+    T2 = torch.logsumexp(t2 * LN2, 1) / LN2
+    T = LN2 * T2 - lgn
+    stats = None
+    if want_stats:
+        g = torch.exp(LN2 * (t2 - T2[:, None]))
+        lg = LN2 * (t2 - T2[:, None])
+        stats = torch.cat([g @ M, (g * (M ** 2).sum(-1)[None, :]).sum(1, keepdim=True),
+                           (g * lg).sum(1, keepdim=True), (g * LN2 * W2[None, :]).sum(1, keepdim=True),
+                           (g * D2).sum(1, keepdim=True)], 1)
+        stats = _out(stats, X)
+    return _out(T, X), _out(T2, X), stats
+
+
+def gmm_mstep(X, T2, mu, w2, sigma):
+    Xd, M, W2 = _d(X), _d(mu), _d(w2)
+    D2 = ((Xd[:, None, :] - M[None, :, :]) ** 2).sum(-1)
+    lg2 = W2[None, :] - D2 * LOG2E / (2 * sigma ** 2) - _d(T2)[:, None]
+    lg = lg2 * LN2
+    w_new = torch.logsumexp(lg, 0)
+    mu_new = torch.softmax(lg, 0).t() @ Xd
+    return _out(torch.cat([w_new[:, None], mu_new], 1), X)
+
+
+def gmm_targets(X, T2, mu_old, w2_old, sigma_old, mu_new, lpi_new):
+    Xd, Mo, W2, Mn, Lp = _d(X), _d(mu_old), _d(w2_old), _d(mu_new), _d(lpi_new)
+    D2 = ((Xd[:, None, :] - Mo[None, :, :]) ** 2).sum(-1)
+    g = torch.exp(LN2 * (W2[None, :] - D2 * LOG2E / (2 * sigma_old ** 2) - _d(T2)[:, None]))
+    D2n = ((Xd[:, None, :] - Mn[None, :, :]) ** 2).sum(-1)
+    rows = torch.cat([g @ Mn, (g * (Mn ** 2).sum(-1)[None, :]).sum(1, keepdim=True),
+                      (g * Lp[None, :]).sum(1, keepdim=True), g.sum(1, keepdim=True),
+                      (g * D2n).sum(1, keepdim=True)], 1)
+    return _out(rows, X)
+
+
+_ENTRIES = ("gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+            "gmm_estep", "gmm_mstep", "gmm_targets")
+
+
+def install(monkeypatch):
+    from difficp_amd import _lib
+    g = globals()
+    for name in _ENTRIES:
+        monkeypatch.setattr(_lib, name, g[name])
+
+
+def install_plain():
+    """Without pytest (subprocess workers of the gloo tests)."""
+    from difficp_amd import _lib
+    g = globals()
+    for name in _ENTRIES:
+        setattr(_lib, name, g[name])

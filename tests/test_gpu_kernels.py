@@ -1,0 +1,152 @@
+"""GPU parity of every HIP kernel against the CPU oracle (oracle/torch_ref.py, float64).
+
+Tolerance: norm-wise relative error <= max(1e-5, 4 x the oracle's own fp32-vs-fp64 error)
+(SURVEY.md 8c parity criterion), per output.
+"""
+import math
+
+import pytest
+import torch
+
+from conftest import rel_err
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from difficp_amd import _lib
+    return _lib
+
+
+def _data(M, N, D, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(M, D, generator=g, dtype=torch.float64) * scale
+    y = torch.rand(N, D, generator=g, dtype=torch.float64) * scale
+    b = torch.randn(N, D, generator=g, dtype=torch.float64)
+    c = torch.randn(M, D, generator=g, dtype=torch.float64)
+    d = torch.randn(N, generator=g, dtype=torch.float64)
+    return x, y, b, c, d
+
+
+def _tol(ref64, ref32):
+    return max(1e-5, 4 * rel_err(ref32, ref64))
+
+
+def _check(out, fn64, fn32, name):
+    r64 = fn64()
+    r32 = fn32()
+    e = rel_err(out, r64)
+    assert e <= _tol(r64, r32), f"{name}: rel err {e:.3e} (oracle32 {rel_err(r32, r64):.3e})"
+
+
+SIZES = [(1, 1), (7, 300), (300, 7), (257, 513), (1000, 1000), (64, 20000), (3000, 2000)]
+
+
+@pytest.mark.parametrize("D", [2, 3])
+@pytest.mark.parametrize("M,N", SIZES)
+def test_reductions(dev, D, M, N):
+    L = _lib()
+    sigma = 0.2
+    x, y, b, c, d = _data(M, N, D, seed=M * 31 + N)
+    f = lambda t: t.float().to(dev)
+    xs, ys, bs, cs, ds = map(f, (x, y, b, c, d))
+    x3, y3, b3, c3, d3 = (t.float() for t in (x, y, b, c, d))
+    cases = [
+        (L.KBASE, dict(), lambda a: R.KBase(*a[:2], sigma)),
+        (L.KREDSCAL, dict(b=ds), lambda a: R.KRedScal(a[0], a[1], a[4], sigma)),
+        (L.KRED, dict(b=bs), lambda a: R.KRed(a[0], a[1], a[2], sigma)),
+        (L.GRADK, dict(), lambda a: R.GradKRed(a[0], a[1], sigma)),
+        (L.DDK, dict(b=bs), lambda a: R.DDKRed(a[0], a[1], a[2], sigma)),
+        (L.GENDK, dict(b=bs, c=cs), lambda a: R.GenDKRed(a[0], a[1], a[2], a[3], sigma)),
+        (L.HESSK, dict(b=bs, c=cs), lambda a: R.HessKRed(a[0], a[1], a[2], a[3], sigma)),
+        (L.LAPK, dict(), lambda a: R.LapKRed(a[0], a[1], sigma)),
+        (L.GRADLAPK, dict(), lambda a: R.GradLapKRed(a[0], a[1], sigma)),
+    ]
+    for op, kw, ref in cases:
+        out = L.gauss_red(op, xs, ys, sigma, **kw)
+        _check(out.cpu(), lambda: ref((x, y, b, c, d)), lambda: ref((x3, y3, b3, c3, d3)), f"op{op}")
+    # GradKRed_rev: column reduction, rows = y
+    out = L.gauss_red(L.GRADK_REV, ys, xs, sigma, b=cs)
+    _check(out.cpu(), lambda: R.GradKRed_rev(x, y, c, sigma), lambda: R.GradKRed_rev(x3, y3, c3, sigma), "rev")
+    # MinSqDist
+    out = L.gauss_red(L.MIN_SQDIST, xs, ys, sigma)
+    assert rel_err(out.cpu(), R.MinSqDist(x3, y3)) < 1e-6
+
+
+def test_empty_columns(dev):
+    L = _lib()
+    x = torch.rand(10, 3, device=dev)
+    y = torch.rand(0, 3, device=dev)
+    b = torch.rand(0, 3, device=dev)
+    assert torch.all(L.gauss_red(L.KRED, x, y, 0.3, b=b) == 0)
+    assert torch.all(torch.isinf(L.gauss_red(L.MIN_SQDIST, x, y, 0.3)))
+
+
+@pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])
+@pytest.mark.parametrize("M,D", [(5, 2), (300, 2), (700, 3), (2500, 3)])
+def test_ode_self_fwd(dev, version, M, D):
+    L = _lib()
+    g = torch.Generator().manual_seed(M + D)
+    q = torch.rand(M, D, generator=g, dtype=torch.float64)
+    p = torch.randn(M, D, generator=g, dtype=torch.float64) * 0.1
+    gc = version == "logdet"
+    wl = version != "classic"
+    m = R.LDDMM(0.15, D, 50.0, gc, wl)
+    m32 = R.LDDMM(0.15, D, 50.0, gc, wl)
+    v64, mG64, c64 = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
+    v32, mG32, c32 = m32.ODE(q.float(), p.float(), torch.zeros(1))
+    H64, H32 = m.Hamiltonian(q, p), m32.Hamiltonian(q.float(), p.float())
+    v, mG, gdiv, h = L.ode_self_fwd(q.float().to(dev), p.float().to(dev), 0.15, m.eta, wl, want_h=True)
+    assert rel_err(v.cpu(), v64) <= _tol(v64, v32)
+    assert rel_err(mG.cpu(), mG64) <= _tol(mG64, mG32)
+    assert rel_err(h.sum().cpu(), H64) <= _tol(H64, H32)
+    if wl:
+        assert rel_err(gdiv.sum().cpu(), c64) <= _tol(c64, c32)
+
+
+@pytest.mark.parametrize("M,D", [(3, 2), (300, 2), (700, 3), (2100, 3)])
+@pytest.mark.parametrize("withlogdet", [False, True])
+def test_ode_self_bwd(dev, M, D, withlogdet):
+    L = _lib()
+    g = torch.Generator().manual_seed(7 * M + D)
+    q = torch.rand(M, D, generator=g, dtype=torch.float64).requires_grad_(True)
+    p = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
+    a = torch.randn(M, D, generator=g, dtype=torch.float64)
+    bm = torch.randn(M, D, generator=g, dtype=torch.float64)
+    gam = torch.randn(1, generator=g, dtype=torch.float64)
+    m = R.LDDMM(0.15, D, 50.0, False, withlogdet)
+    v, mG, c = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
+    Lf = (a * v).sum() + (bm * mG).sum() + (gam * c).sum()
+    gq64, gp64 = torch.autograd.grad(Lf, (q, p))
+    f = lambda t: t.detach().float().to(dev)
+    gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, 0.0)
+    assert rel_err(gq.cpu(), gq64) < 2e-5, rel_err(gq.cpu(), gq64)
+    assert rel_err(gp.cpu(), gp64) < 2e-5, rel_err(gp.cpu(), gp64)
+
+
+@pytest.mark.parametrize("M,N,D", [(40, 300, 2), (500, 1300, 3), (2000, 100, 3)])
+@pytest.mark.parametrize("withlogdet", [False, True])
+def test_ode_ext(dev, M, N, D, withlogdet):
+    L = _lib()
+    g = torch.Generator().manual_seed(M + N + D)
+    q = torch.rand(M, D, generator=g, dtype=torch.float64).requires_grad_(True)
+    p = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
+    x = torch.rand(N, D, generator=g, dtype=torch.float64).requires_grad_(True)
+    m = R.LDDMM(0.2, D, 50.0, False, withlogdet)
+    vq, mG, c, vx = m.ODE(q, p, torch.zeros(1, dtype=torch.float64), x)
+    f = lambda t: t.detach().float().to(dev)
+    vx_h, gx_h = L.ode_ext_fwd(f(x), f(q), f(p), 0.2, 0.0, withlogdet)
+    assert rel_err(vx_h.cpu(), vx) < 1e-5
+    if withlogdet:
+        assert rel_err(gx_h.sum().cpu(), c) < 1e-5
+    a = torch.randn(N, D, generator=g, dtype=torch.float64)
+    gam = torch.randn(1, generator=g, dtype=torch.float64)
+    Lf = (a * vx).sum() + (gam * c).sum()
+    gq64, gp64, gx64 = torch.autograd.grad(Lf, (q, p, x))
+    gq = torch.zeros(M, D, device=dev)
+    gp = torch.zeros(M, D, device=dev)
+    gx = L.ode_ext_bwd(f(x), f(q), f(p), f(a), f(gam) if withlogdet else None, 0.2, 0.0, gq, gp)
+    assert rel_err(gx.cpu(), gx64) < 2e-5
+    assert rel_err(gq.cpu(), gq64) < 2e-5
+    assert rel_err(gp.cpu(), gp64) < 2e-5

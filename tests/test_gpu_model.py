@@ -1,0 +1,139 @@
+"""GPU parity of the model-level API (LDDMMModel.Shoot / trajloss / gradients, EM_step,
+log_likelihoods, kernel autograd) against the CPU oracle (float64 restatement of the
+reference torch path)."""
+import pytest
+import torch
+
+from conftest import rel_err
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _f(t, dev):
+    return t.detach().float().to(dev)
+
+
+@pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
+@pytest.mark.parametrize("version", ["classic", "hybrid"])
+@pytest.mark.parametrize("M,D,ext", [(60, 2, 0), (400, 3, 0), (50, 2, 300), (300, 3, 900)])
+def test_shoot_and_grad(dev, scheme, version, M, D, ext):
+    from difficp_amd.core.LDDMM import LDDMMModel
+    g = torch.Generator().manual_seed(M * 3 + D + ext)
+    q0 = torch.rand(M, D, generator=g, dtype=torch.float64)
+    p0 = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
+    x0 = torch.rand(ext, D, generator=g, dtype=torch.float64) if ext else None
+    lam, sig, nt = 20.0, 0.25, 7
+    wl = version == "hybrid"
+    ref = R.LDDMM(sig, D, lam, False, wl, scheme=scheme, nt=nt)
+    shoot = ref.Shoot(q0, p0, x0)
+    tgt = torch.randn(ext if ext else M, D, generator=g, dtype=torch.float64)
+    last = shoot[-1][-1] if ext else shoot[-1][0]
+    L64 = ref.trajloss(shoot) + ((last - tgt) ** 2).sum()
+    (gp64,) = torch.autograd.grad(L64, (p0,))
+    # the same computation in fp32 on CPU: the dynamics amplify rounding, so the tolerance
+    # is set by the oracle's own fp32-vs-fp64 gap (SURVEY.md 8c parity criterion)
+    p32 = p0.detach().float().requires_grad_(True)
+    sh32 = ref.Shoot(q0.float(), p32, None if x0 is None else x0.float())
+    last32 = sh32[-1][-1] if ext else sh32[-1][0]
+    L32 = ref.trajloss(sh32) + ((last32 - tgt.float()) ** 2).sum()
+    (gp32,) = torch.autograd.grad(L32, (p32,))
+    tol = lambda a32, a64, base: max(base, 4 * rel_err(a32, a64))
+
+    LM = LDDMMModel(sigma=sig, D=D, lambd=lam, version=version, scheme=scheme, nt=nt,
+                    spec={"device": dev, "dtype": torch.float32})
+    p = _f(p0, dev).requires_grad_(True)
+    sh = LM.Shoot(_f(q0, dev), p, None if x0 is None else _f(x0, dev))
+    lastg = sh[-1][-1] if ext else sh[-1][0]
+    Lg = LM.trajloss(sh) + ((lastg - _f(tgt, dev)) ** 2).sum()
+    Lg.backward()
+    assert rel_err(lastg.cpu(), last) <= tol(last32, last, 1e-5)
+    assert rel_err(sh[-1][2].cpu(), shoot[-1][2]) <= tol(sh32[-1][2], shoot[-1][2], 1e-5)
+    assert rel_err(Lg.cpu(), L64) <= tol(L32, L64, 1e-5)
+    assert rel_err(p.grad.cpu(), gp64) <= tol(gp32, gp64, 2e-5), rel_err(p.grad.cpu(), gp64)
+
+
+@pytest.mark.parametrize("opt", [dict(mu=True, w=True, sigma=True),
+                                 dict(mu=False, w=False, sigma=True),
+                                 dict(mu=True, w=False, sigma=False),
+                                 dict(mu=False, w=True, sigma=True)])
+@pytest.mark.parametrize("N,C,D", [(500, 20, 2), (5000, 64, 3), (3000, 3000, 3)])
+@pytest.mark.parametrize("outl", [False, True])
+def test_em_step(dev, opt, N, C, D, outl):
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    g = torch.Generator().manual_seed(N + C + D)
+    X = torch.rand(N, D, generator=g, dtype=torch.float64)
+    mu = torch.rand(C, D, generator=g, dtype=torch.float64)
+    w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    sigma = 0.08
+    to_opt = dict(opt, eta0=True)
+    G = GaussianMixtureUnif(_f(mu, dev), sigma=sigma, use_outliers=outl,
+                            spec={"device": dev, "dtype": torch.float32})
+    G.w = _f(w, dev)
+    G.to_optimize = dict(to_opt)
+    outliers = {"vol0": None, "eta0": 0.0} if outl else None
+    Xg = _f(X, dev)
+    st = dict(mu=mu, w=w, sigma=sigma, outliers=outliers)
+    for it in range(3):
+        # fp32 oracle from the same state: its gap to fp64 sets the tolerance on sums
+        _, C32, F32, _ = R.em_step(X.float(), st["mu"].float(), st["w"].float(), st["sigma"], to_opt,
+                                   None if st["outliers"] is None else dict(st["outliers"]))
+        Y64, Cfe64, FE64, st = R.em_step(X, st["mu"], st["w"], st["sigma"], to_opt, st["outliers"])
+        Y, Cfe, FE = G.EM_step(Xg)
+        assert rel_err(Y.cpu(), Y64) < 2e-5, (it, rel_err(Y.cpu(), Y64))
+        tF = max(2e-5 * abs(float(FE64)), 4 * abs(float(F32) - float(FE64))) + 1e-4
+        tC = max(2e-5 * abs(float(Cfe64)), 4 * abs(float(C32) - float(Cfe64))) + 1e-4
+        assert abs(float(FE) - float(FE64)) <= tF, (float(FE), float(FE64), float(F32))
+        assert abs(float(Cfe) - float(Cfe64)) <= tC, (float(Cfe), float(Cfe64), float(C32))
+        assert abs(G.sigma - st["sigma"]) <= 1e-5 * st["sigma"]
+        assert rel_err(G.mu.cpu(), st["mu"]) < 1e-5
+        assert rel_err(G.w.cpu(), st["w"]) < 1e-5 + 1e-6
+        if outl:
+            assert abs(G.outliers["eta0"] - st["outliers"]["eta0"]) < 1e-4
+
+
+def test_em_skip_M_and_loglik(dev):
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand(4000, 3, generator=g, dtype=torch.float64)
+    mu = torch.rand(100, 3, generator=g, dtype=torch.float64)
+    G = GaussianMixtureUnif(_f(mu, dev), sigma=0.1, spec={"device": dev, "dtype": torch.float32})
+    Y, Cfe, FE = G.EM_step(_f(X, dev), skip_M=True)
+    Y64, Cfe64, FE64, _ = R.em_step(X, mu, torch.zeros(100, dtype=torch.float64), 0.1,
+                                    dict(mu=True, w=True, sigma=True), None, skip_M=True)
+    assert rel_err(Y.cpu(), Y64) < 2e-5
+    assert abs(float(FE) - float(FE64)) < 2e-5 * abs(float(FE64))
+    ll = G.log_likelihoods(_f(X, dev))
+    ll64 = R.log_likelihoods(X, mu, torch.zeros(100, dtype=torch.float64), 0.1)
+    assert rel_err(ll.cpu(), ll64) < 1e-5
+
+
+@pytest.mark.parametrize("D", [2, 3])
+def test_kernel_autograd(dev, D):
+    from difficp_amd.tools.kernel import GaussKernel
+    g = torch.Generator().manual_seed(D)
+    M, N, sig = 300, 500, 0.3
+    x = torch.rand(M, D, generator=g, dtype=torch.float64).requires_grad_(True)
+    y = torch.rand(N, D, generator=g, dtype=torch.float64).requires_grad_(True)
+    b = torch.randn(N, D, generator=g, dtype=torch.float64).requires_grad_(True)
+    d = torch.randn(N, generator=g, dtype=torch.float64).requires_grad_(True)
+    GK = GaussKernel(sig, D, spec={"device": dev, "dtype": torch.float32})
+    wv = torch.randn(M, D, generator=g, dtype=torch.float64)
+    ws = torch.randn(M, generator=g, dtype=torch.float64)
+    tests = [
+        ("KRed", lambda X, Y, B, Dd: GK.KRed(X, Y, B), lambda: R.KRed(x, y, b, sig), wv, (0, 1, 2)),
+        ("GradKRed", lambda X, Y, B, Dd: GK.GradKRed(X, Y), lambda: R.GradKRed(x, y, sig), wv, (0, 1)),
+        ("LapKRed", lambda X, Y, B, Dd: GK.LapKRed(X, Y), lambda: R.LapKRed(x, y, sig), ws, (0, 1)),
+        ("KBase", lambda X, Y, B, Dd: GK.KBase(X, Y), lambda: R.KBase(x, y, sig), ws, (0, 1)),
+        ("KRedScal", lambda X, Y, B, Dd: GK.KRedScal(X, Y, Dd), lambda: R.KRedScal(x, y, d, sig), ws, (0, 1, 3)),
+    ]
+    for name, fh, fr, wt, which in tests:
+        ins64 = (x, y, b, d)
+        out64 = fr()
+        grads64 = torch.autograd.grad((out64 * wt).sum(), [ins64[i] for i in which])
+        insg = [_f(t, dev).requires_grad_(True) for t in ins64]
+        outg = fh(*insg)
+        assert rel_err(outg.cpu(), out64) < 1e-5, name
+        gg = torch.autograd.grad((outg * _f(wt, dev)).sum(), [insg[i] for i in which])
+        for a, b_ in zip(gg, grads64):
+            assert rel_err(a.cpu(), b_) < 2e-5, (name, rel_err(a.cpu(), b_))

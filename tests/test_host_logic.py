@@ -1,0 +1,103 @@
+"""CPU tests of the host-side logic above the C-ABI (shooting adjoint, Hamiltonian,
+EM bookkeeping, PSR driver) with the kernels replaced by the oracle-backed executable spec
+(tests/fake_hip.py).  These pin the discrete-adjoint and free-energy logic independently
+of the GPU; the GPU tests pin the kernels."""
+import pytest
+import torch
+
+import fake_hip
+from conftest import rel_err
+from oracle import torch_ref as R
+
+CPU = {"device": "cpu", "dtype": torch.float32}
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    fake_hip.install(monkeypatch)
+
+
+@pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
+@pytest.mark.parametrize("version", ["classic", "hybrid"])
+@pytest.mark.parametrize("ext", [0, 40])
+def test_shoot_adjoint_matches_autograd(fake, scheme, version, ext):
+    from difficp_amd.core.LDDMM import LDDMMModel
+    g = torch.Generator().manual_seed(3 + ext)
+    M, D, lam, sig, nt = 30, 2, 20.0, 0.3, 5
+    q0 = torch.rand(M, D, generator=g, dtype=torch.float64)
+    p0 = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
+    x0 = torch.rand(ext, D, generator=g, dtype=torch.float64) if ext else None
+    ref = R.LDDMM(sig, D, lam, False, version == "hybrid", scheme=scheme, nt=nt)
+    sh = ref.Shoot(q0, p0, x0)
+    W = [torch.randn(M, D, generator=g, dtype=torch.float64) for _ in range(2)]
+    last = sh[-1][-1] if ext else sh[-1][0]
+    Wl = torch.randn(last.shape, generator=g, dtype=torch.float64)
+    # loss touching final + an intermediate state + cost (exercises every adjoint input)
+    L64 = ref.trajloss(sh) + (Wl * last).sum() + (W[0] * sh[2][0]).sum() + (W[1] * sh[3][1]).sum()
+    (gp64,) = torch.autograd.grad(L64, (p0,))
+
+    LM = LDDMMModel(sigma=sig, D=D, lambd=lam, version=version, scheme=scheme, nt=nt, spec=CPU)
+    p = p0.detach().float().requires_grad_(True)
+    s = LM.Shoot(q0.float(), p, None if x0 is None else x0.float())
+    lastg = s[-1][-1] if ext else s[-1][0]
+    Lg = LM.trajloss(s) + (Wl.float() * lastg).sum() + (W[0].float() * s[2][0]).sum() \
+        + (W[1].float() * s[3][1]).sum()
+    Lg.backward()
+    assert rel_err(lastg, last) < 1e-5
+    assert rel_err(Lg, L64) < 1e-5
+    assert rel_err(p.grad, gp64) < 1e-5
+
+
+def test_ode_api_matches_oracle(fake):
+    from difficp_amd.core.LDDMM import LDDMMModel
+    g = torch.Generator().manual_seed(1)
+    q = torch.rand(25, 3, generator=g, dtype=torch.float64)
+    p = 0.2 * torch.randn(25, 3, generator=g, dtype=torch.float64)
+    x = torch.rand(12, 3, generator=g, dtype=torch.float64)
+    for version in ("classic", "hybrid", "logdet"):
+        ref = R.LDDMM(0.3, 3, 10.0, version == "logdet", version != "classic")
+        LM = LDDMMModel(sigma=0.3, D=3, lambd=10.0, version=version, spec=CPU)
+        out = LM.ODE(q.float(), p.float(), torch.zeros(1), x.float())
+        exp = ref.ODE(q, p, torch.zeros(1, dtype=torch.float64), x)
+        for a, b in zip(out, exp):
+            assert rel_err(a, b) < 1e-6
+        assert rel_err(LM.Hamiltonian(q.float(), p.float()), ref.Hamiltonian(q, p)) < 1e-6
+        assert rel_err(LM.v(x.float(), q.float(), p.float()), ref.v(x, q, p)) < 1e-6
+        assert rel_err(LM.mdivsum(x.float(), q.float(), p.float()), ref.mdivsum(x, q, p)) < 1e-6
+
+
+@pytest.mark.parametrize("outl", [False, True])
+@pytest.mark.parametrize("opt", [dict(mu=True, w=True, sigma=True), dict(mu=False, w=False, sigma=True)])
+def test_em_host_logic(fake, outl, opt):
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    g = torch.Generator().manual_seed(11)
+    X = torch.rand(400, 2, generator=g, dtype=torch.float64)
+    mu = torch.rand(15, 2, generator=g, dtype=torch.float64)
+    G = GaussianMixtureUnif(mu.float(), sigma=0.1, use_outliers=outl, spec=CPU)
+    to = dict(opt, eta0=True)
+    G.to_optimize = dict(to)
+    st = dict(mu=mu, w=torch.zeros(15, dtype=torch.float64), sigma=0.1,
+              outliers={"vol0": None, "eta0": 0.0} if outl else None)
+    for _ in range(4):
+        Y64, C64, F64, st = R.em_step(X, st["mu"], st["w"], st["sigma"], to, st["outliers"])
+        Y, C, F = G.EM_step(X.float())
+        assert rel_err(Y, Y64) < 1e-5
+        assert abs(float(F) - float(F64)) < 1e-5 * abs(float(F64)) + 1e-4
+        assert abs(float(C) - float(C64)) < 1e-5 * abs(float(C64)) + 1e-4
+        assert abs(G.sigma - st["sigma"]) < 1e-6
+
+
+def test_check_coverage_and_rev(fake):
+    from difficp_amd.tools.kernel import GaussKernel
+    GK = GaussKernel(0.1, 2, spec=CPU)
+    X = torch.tensor([[0.0, 0.0], [1.0, 1.0]])
+    Y = torch.tensor([[0.05, 0.0]])
+    assert GK.check_coverage(X, Y, 2.0).tolist() == [False, True]
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(20, 2, generator=g)
+    y = torch.rand(30, 2, generator=g)
+    d = torch.randn(20, 2, generator=g)
+    # reversed-gradient identity of kernel.py:385-387
+    a = (d * GK.GradKRed(x, y)).sum()
+    b = GK.GradKRed_rev(x, y, d).sum()
+    assert abs(float(a) - float(b)) < 1e-4 * abs(float(a)) + 1e-5
