@@ -118,6 +118,62 @@ def _stream(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+# ---------------------------------------------------------------------------------------
+# Optional live kernel accounting (bench.py): HIP events around each launch on the launch
+# stream, algorithmic pair / flop / byte counts per launch.
+# Algorithmic cost per (row, column) pair for D = 3 (FMA = 2 flop), counted from the pair
+# operators in csrc/lddmm_ops.hpp and csrc/gmm.hip; one exp2 per pair for all of them.
+FLOPS_PER_PAIR = {
+    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 89,
+    "ode_ext_fwd": 22, "ode_ext_bwd": (36 + 49) / 2, "gmm_estep": 37, "gmm_mstep": 31,
+    "gmm_targets": 32,
+}
+
+
+class KernelProfile:
+    """Context manager collecting (name, pairs, flops, bytes, start, end) per launch."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _prof
+        _prof = self
+        return self
+
+    def __exit__(self, *exc):
+        global _prof
+        _prof = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, pairs, flops, nbytes, e0, e1 in self.records:
+            d = out.setdefault(name, {"launches": 0, "pairs": 0, "flops": 0, "bytes": 0, "ms": 0.0})
+            d["launches"] += 1
+            d["pairs"] += pairs
+            d["flops"] += flops
+            d["bytes"] += nbytes
+            d["ms"] += e0.elapsed_time(e1)
+        return out
+
+
+_prof = None
+
+
+def _launch(name, pairs, nbytes, fn):
+    if _prof is None:
+        return fn()
+    st = torch.cuda.current_stream()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    r = fn()
+    e1.record(st)
+    _prof.records.append((name, int(pairs), int(pairs * FLOPS_PER_PAIR.get(name, 0)), int(nbytes), e0, e1))
+    return r
+
+
 def _workspace(kind: int, M: int, N: int, D: int, device):
     nbytes = int(lib().dicp_workspace_bytes(kind, int(M), int(N), int(D)))
     if nbytes == 0:
@@ -145,8 +201,9 @@ def gauss_red(op: int, x, y, sigma: float, b=None, c=None):
     if M == 0:
         return out
     ws, nb = _workspace(WS_RED, M, N, D, x.device)
-    rc = lib().dicp_gauss_red_f32(int(op), _ptr(x), M, _ptr(y), N, D, _ptr(b), _ptr(c),
-                                  float(sigma), _ptr(out), _ptr(ws), nb, _stream(x.device))
+    rc = _launch("gauss_red", M * N, 4 * (2 * M * D + 2 * N * D),
+                 lambda: lib().dicp_gauss_red_f32(int(op), _ptr(x), M, _ptr(y), N, D, _ptr(b), _ptr(c),
+                                  float(sigma), _ptr(out), _ptr(ws), nb, _stream(x.device)))
     _check_rc(rc, f"gauss_red(op={op})")
     return out
 
@@ -166,9 +223,10 @@ def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = 
     if M == 0:
         return v, mG, g, h
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, dev)
-    rc = lib().dicp_lddmm_ode_self_fwd_f32(_ptr(q), _ptr(p), M, D, float(sigma), float(eta),
+    rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), M * M, 4 * M * (4 * D + 2),
+                 lambda: lib().dicp_lddmm_ode_self_fwd_f32(_ptr(q), _ptr(p), M, D, float(sigma), float(eta),
                                            _ptr(v), _ptr(mG), _ptr(g), _ptr(h), _ptr(ws), nb,
-                                           _stream(dev))
+                                           _stream(dev)))
     _check_rc(rc, "ode_self_fwd")
     return v, mG, g, h
 
@@ -186,9 +244,10 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma: float, eta: float):
     if M == 0:
         return gq, gp
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
-    rc = lib().dicp_lddmm_ode_self_bwd_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv), M,
+    rc = _launch("ode_self_bwd", M * M, 4 * M * 6 * D,
+                 lambda: lib().dicp_lddmm_ode_self_bwd_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv), M,
                                            D, float(sigma), float(eta), _ptr(gq), _ptr(gp),
-                                           _ptr(ws), nb, _stream(q.device))
+                                           _ptr(ws), nb, _stream(q.device)))
     _check_rc(rc, "ode_self_bwd")
     return gq, gp
 
@@ -204,9 +263,10 @@ def ode_ext_fwd(x, q, p, sigma: float, eta: float, want_div: bool):
     if N == 0:
         return vx, gx
     ws, nb = _workspace(WS_ODE_EXT_FWD, M, N, D, x.device)
-    rc = lib().dicp_lddmm_ode_ext_fwd_f32(_ptr(x), N, _ptr(q), _ptr(p), M, D, float(sigma),
+    rc = _launch("ode_ext_fwd", N * M, 4 * (N * (2 * D + 1) + 2 * M * D),
+                 lambda: lib().dicp_lddmm_ode_ext_fwd_f32(_ptr(x), N, _ptr(q), _ptr(p), M, D, float(sigma),
                                           float(eta), _ptr(vx), _ptr(gx), _ptr(ws), nb,
-                                          _stream(x.device))
+                                          _stream(x.device)))
     _check_rc(rc, "ode_ext_fwd")
     return vx, gx
 
@@ -226,9 +286,10 @@ def ode_ext_bwd(x, q, p, gvx, gdiv, sigma: float, eta: float, gq, gp):
     if N == 0:
         return gx
     ws, nb = _workspace(WS_ODE_EXT_BWD, M, N, D, x.device)
-    rc = lib().dicp_lddmm_ode_ext_bwd_f32(_ptr(x), N, _ptr(q), _ptr(p), M, D, float(sigma),
+    rc = _launch("ode_ext_bwd", 2 * N * M, 4 * (3 * N * D + 6 * M * D),
+                 lambda: lib().dicp_lddmm_ode_ext_bwd_f32(_ptr(x), N, _ptr(q), _ptr(p), M, D, float(sigma),
                                           float(eta), _ptr(gvx), _ptr(gdiv), _ptr(gx), _ptr(gq),
-                                          _ptr(gp), _ptr(ws), nb, _stream(x.device))
+                                          _ptr(gp), _ptr(ws), nb, _stream(x.device)))
     _check_rc(rc, "ode_ext_bwd")
     return gx
 
@@ -250,9 +311,10 @@ def gmm_estep(X, mu, w2, mu2, sigma: float, lgn: float, want_stats: bool):
     if N == 0:
         return T, T2, stats
     ws, nb = _workspace(WS_GMM_ESTEP, N, C, D, dev)
-    rc = lib().dicp_gmm_estep_f32(_ptr(X), N, _ptr(mu), _ptr(w2), _ptr(mu2), C, D, float(sigma),
+    rc = _launch("gmm_estep", N * C, 4 * (N * (2 * D + 6) + C * (D + 2)),
+                 lambda: lib().dicp_gmm_estep_f32(_ptr(X), N, _ptr(mu), _ptr(w2), _ptr(mu2), C, D, float(sigma),
                                   float(lgn), _ptr(T), _ptr(T2), _ptr(stats), _ptr(ws), nb,
-                                  _stream(dev))
+                                  _stream(dev)))
     _check_rc(rc, "gmm_estep")
     return T, T2, stats
 
@@ -266,8 +328,9 @@ def gmm_mstep(X, T2, mu, w2, sigma: float):
     C = mu.shape[0]
     colstats = torch.empty((C, D + 1), device=X.device, dtype=torch.float32)
     ws, nb = _workspace(WS_GMM_MSTEP, N, C, D, X.device)
-    rc = lib().dicp_gmm_mstep_f32(_ptr(X), _ptr(T2), N, _ptr(mu), _ptr(w2), C, D, float(sigma),
-                                  _ptr(colstats), _ptr(ws), nb, _stream(X.device))
+    rc = _launch("gmm_mstep", N * C, 4 * (N * (D + 1) + 2 * C * (D + 1)),
+                 lambda: lib().dicp_gmm_mstep_f32(_ptr(X), _ptr(T2), N, _ptr(mu), _ptr(w2), C, D, float(sigma),
+                                  _ptr(colstats), _ptr(ws), nb, _stream(X.device)))
     _check_rc(rc, "gmm_mstep")
     return colstats
 
@@ -285,8 +348,9 @@ def gmm_targets(X, T2, mu_old, w2_old, sigma_old: float, mu_new, lpi_new):
     if N == 0:
         return rows
     ws, nb = _workspace(WS_GMM_TARGETS, N, C, D, X.device)
-    rc = lib().dicp_gmm_targets_f32(_ptr(X), _ptr(T2), N, _ptr(mu_old), _ptr(w2_old),
+    rc = _launch("gmm_targets", N * C, 4 * (N * (2 * D + 5) + C * (2 * D + 3)),
+                 lambda: lib().dicp_gmm_targets_f32(_ptr(X), _ptr(T2), N, _ptr(mu_old), _ptr(w2_old),
                                     float(sigma_old), _ptr(mu_new), _ptr(lpi_new), C, D,
-                                    _ptr(rows), _ptr(ws), nb, _stream(X.device))
+                                    _ptr(rows), _ptr(ws), nb, _stream(X.device)))
     _check_rc(rc, "gmm_targets")
     return rows

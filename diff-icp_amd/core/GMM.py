@@ -217,9 +217,12 @@ class GaussianMixtureUnif(torch.nn.Module):
         if changed or keops_sem:
             lpi_new, _, _ = self._columns(self.mu, self.w)
             rows = _lib.gmm_targets(X, T2, mu_old, w2_old, sigma_old, self.mu.contiguous(), lpi_new)
-            Y = rows[:, :D]
-            P_row = rows[:, D + 1]
-            D2new_row = rows[:, D + 3]
+            # renormalise by sum_c gamma (= 1 exactly; removes the bias that the fp32
+            # rounding of the stored log-normaliser T2 would put on every weighted sum)
+            inv = 1.0 / rows[:, D + 2]
+            Y = rows[:, :D] * inv[:, None]
+            P_row = rows[:, D + 1] * inv
+            D2new_row = rows[:, D + 3] * inv
         else:
             Y = stats[:, :D]
             P_row = stats[:, D + 2]

@@ -1,0 +1,78 @@
+// Peak-rate probes for the roofline of the pair kernels (diagnostic library, not the product):
+// v_exp_f32 throughput, v_fma_f32 / v_pk_fma_f32 throughput.  Each thread runs ITER
+// iterations of UNROLL independent chains so issue (not latency) bounds the loop.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kChains = 8;
+
+__global__ __launch_bounds__(256) void exp_probe(float* out, int iters, float seed) {
+  float a[kChains];
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) a[k] = seed * (threadIdx.x + k) * 1e-7f;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k) a[k] = __builtin_amdgcn_exp2f(a[k]) - 1.0f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) s += a[k];
+  if (s == 12345.f) out[threadIdx.x] = s;  // keep live
+}
+
+__global__ __launch_bounds__(256) void fma_probe(float* out, int iters, float seed) {
+  float a[kChains], b[kChains];
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) {
+    a[k] = seed * (threadIdx.x + k);
+    b[k] = seed * 0.5f + k;
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k) a[k] = fmaf(a[k], b[k], 0.999f);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) s += a[k];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256) void pkfma_probe(float* out, int iters, float seed) {
+  float2v a[kChains], b[kChains], c;
+  c.x = 0.999f;
+  c.y = 0.998f;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) {
+    a[k].x = seed * (threadIdx.x + k);
+    a[k].y = seed * (threadIdx.x + 2 * k);
+    b[k].x = seed * 0.5f + k;
+    b[k].y = seed * 0.25f + k;
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k) a[k] = __builtin_elementwise_fma(a[k], b[k], c);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) s += a[k].x + a[k].y;
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
+}  // namespace
+
+// kind: 0 = exp2, 1 = fma, 2 = pk_fma.  Returns 0 on success.  ops per launch:
+// blocks*256*iters*kChains (x2 lanes for pk_fma).
+extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 g(blocks), b(256);
+  if (kind == 0) exp_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 1) fma_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  else pkfma_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+extern "C" int dicp_mb_chains(void) { return kChains; }
