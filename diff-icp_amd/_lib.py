@@ -47,6 +47,7 @@ _SIGNATURES = {
     "dicp_version": [],
     "dicp_supports_dim": [_INT],
     "dicp_num_splits": [_INT, _I64, _I64],
+    "dicp_set_option": [ctypes.c_char_p, _INT],
 }
 _RESTYPES = {"dicp_workspace_bytes": _SZ, "dicp_last_error": ctypes.c_char_p,
              "dicp_version": ctypes.c_char_p}
@@ -85,6 +86,11 @@ def version() -> str:
 
 def supports_dim(D: int) -> bool:
     return bool(lib().dicp_supports_dim(int(D)))
+
+
+def set_option(name: str, value: int):
+    """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
+    _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")
 
 
 def num_splits(kind: int, M: int, N: int) -> int:

@@ -48,6 +48,9 @@ struct Args {
   const float* c1;
   const float* c2;
   const float* c3;
+  // coordinate pre-scale alpha = sqrt(log2(e) / (2 sigma^2)) for ops that work in scaled
+  // coordinates (K = exp2(-|alpha z|^2) needs no per-pair multiply); 0 when unused
+  float scale;
 };
 
 // Output descriptor: up to 4 output arrays, each (rows, width) row-major.
@@ -82,7 +85,9 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
   constexpr int CW4 = Op::CW4;
   constexpr int NACC = Op::NACC;
   constexpr bool MIN = Op::kMin;
-  __shared__ float4 lds[kTile * CW4];
+  // double-buffered column tiles: the global loads of tile t+1 are in flight while tile t
+  // is consumed from LDS; one barrier per tile.
+  __shared__ float4 lds[2][kTile * CW4];
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];  // device-resident scalar (no host sync)
 
   const int tid = threadIdx.x;
@@ -106,22 +111,33 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
   int64_t j1 = j0 + chunk;
   if (j1 > N) j1 = N;
 
+  float pre[CW4 * 4];
+  int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
+  if (cnt > 0 && tid < cnt) {
+    Op::load_col(args, j0 + tid, pre);
+#pragma unroll
+    for (int k = 0; k < CW4; ++k)
+      lds[0][tid * CW4 + k] = make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+  }
+  __syncthreads();
+  int buf = 0;
   for (int64_t jt = j0; jt < j1; jt += kTile) {
-    const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
-    if (tid < cnt) Op::load_col(args, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
-    __syncthreads();
+    const int64_t jn = jt + kTile;
+    const int cntn = jn < j1 ? (int)((j1 - jn) < kTile ? (j1 - jn) : kTile) : 0;
+    if (tid < cntn) Op::load_col(args, jn + tid, pre);  // prefetch next tile (registers)
+
     float acc[R][NACC];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int k = 0; k < NACC; ++k) acc[r][k] = MIN ? __builtin_huge_valf() : 0.f;
-
+    const float4* tile = lds[buf];
 #pragma unroll 2
     for (int t = 0; t < cnt; ++t) {
       float rec[CW4 * 4];
 #pragma unroll
       for (int k = 0; k < CW4; ++k) {
-        const float4 q = lds[t * CW4 + k];
+        const float4 q = tile[t * CW4 + k];
         rec[4 * k + 0] = q.x;
         rec[4 * k + 1] = q.y;
         rec[4 * k + 2] = q.z;
@@ -135,7 +151,15 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
 #pragma unroll
       for (int k = 0; k < NACC; ++k)
         tot[r][k] = MIN ? fminf(tot[r][k], acc[r][k]) : tot[r][k] + acc[r][k];
+    if (tid < cntn) {
+#pragma unroll
+      for (int k = 0; k < CW4; ++k)
+        lds[buf ^ 1][tid * CW4 + k] =
+            make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+    }
     __syncthreads();
+    buf ^= 1;
+    cnt = cntn;
   }
 
   const bool split = gridDim.y > 1;

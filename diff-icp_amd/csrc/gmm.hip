@@ -274,8 +274,15 @@ struct OpGmmTargets {
 };
 
 template <class Op, int R>
+int lse_splits(int64_t M, int64_t N) {
+  static int64_t cap = -1;
+  if (cap < 0) cap = (int64_t)device_cus() * blocks_per_cu(lse_rowred_kernel<Op, R>);
+  return num_splits_cap(M, N, R, cap);
+}
+
+template <class Op, int R>
 size_t lse_ws_bytes(int64_t M, int64_t N) {
-  const int S = num_splits(M, N, R);
+  const int S = lse_splits<Op, R>(M, N);
   return (size_t)S * (size_t)M * (size_t)(2 + Op::NACC) * sizeof(float);
 }
 
@@ -283,7 +290,7 @@ template <class Op, int R>
 int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
   if (M <= 0) return DICP_OK;
-  const int S = num_splits(M, N, R);
+  const int S = lse_splits<Op, R>(M, N);
   const int64_t chunk = N > 0 ? chunk_of(N, S) : 0;
   const size_t need = lse_ws_bytes<Op, R>(M, N);
   if (ws == nullptr || ws_bytes < need) {
@@ -377,8 +384,11 @@ size_t dicp_gmm_ws(int kind, int64_t M, int64_t N, int D) {
   // M = rows of the data (N points), N = components (C) for the GMM kinds
   if (D != 2 && D != 3) return 0;
   switch (kind) {
-    case DICP_WS_GMM_ESTEP:
-      return D == 2 ? lse_ws_bytes<OpGmmE<2, true>, kRG>(M, N) : lse_ws_bytes<OpGmmE<3, true>, kRG>(M, N);
+    case DICP_WS_GMM_ESTEP: {  // both variants (their occupancies, hence splits, differ)
+      size_t a = D == 2 ? lse_ws_bytes<OpGmmE<2, true>, kRG>(M, N) : lse_ws_bytes<OpGmmE<3, true>, kRG>(M, N);
+      size_t b = D == 2 ? lse_ws_bytes<OpGmmE<2, false>, kRG>(M, N) : lse_ws_bytes<OpGmmE<3, false>, kRG>(M, N);
+      return a > b ? a : b;
+    }
     case DICP_WS_GMM_MSTEP:
       return D == 2 ? lse_ws_bytes<OpGmmM<2>, kRG>(N, M) : lse_ws_bytes<OpGmmM<3>, kRG>(N, M);
     case DICP_WS_GMM_TARGETS:

@@ -13,29 +13,97 @@ namespace dicp {
 
 void set_error(const char* fmt, ...);
 
-// Workgroups we aim for per pass: 256 CUs x ~8 resident workgroups, so that the tail of
-// an unevenly-clocked chip (8 XCDs) stays short.
-constexpr int64_t kTargetBlocks = 2048;
-constexpr int64_t kMinChunk = 2 * kTile;
+constexpr int64_t kMinChunk = 256;  // smallest column chunk of a split
 
-// Number of column chunks (gridDim.y) for an M-row, N-column pass with R rows per thread.
-inline int num_splits(int64_t M, int64_t N, int R) {
-  if (M <= 0 || N <= 0) return 1;
-  const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
-  int64_t S = (kTargetBlocks + bx - 1) / bx;
-  const int64_t smax = (N + kMinChunk - 1) / kMinChunk;
-  if (S > smax) S = smax;
-  if (S < 1) S = 1;
-  // chunk rounded up to whole tiles; recompute S so no chunk is empty
-  int64_t chunk = (N + S - 1) / S;
-  chunk = (chunk + kTile - 1) / kTile * kTile;
-  S = (N + chunk - 1) / chunk;
-  return (int)S;
+// Resident-workgroup capacity of the device for a kernel: CUs x blocks per CU (occupancy
+// query, cached per kernel by the caller).  Falls back to 256 x 4 without a device.
+inline int device_cus() {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      cus = n;
+    else
+      cus = 256;
+  }
+  return cus;
 }
 
-inline int64_t chunk_of(int64_t N, int S) {
+// Resident 256-thread workgroups per CU from the kernel's resources (MI355X_MICROARCH.md
+// "Register files": waves/SIMD = min(8, 512 / alloc(VGPR+AGPR, granule 8)); one wave of a
+// 4-wave workgroup per SIMD; LDS 160 KiB per CU).  hipOccupancyMaxActiveBlocksPerMultiprocessor
+// under-reports on gfx950 (it assumes a smaller LDS), which made the split model leave
+// CUs idle.
+template <class K>
+int blocks_per_cu(K kernel) {
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(kernel)) != hipSuccess) {
+    (void)hipGetLastError();
+    return 4;
+  }
+  const int vg = at.numRegs > 0 ? ((at.numRegs + 7) / 8) * 8 : 64;
+  int waves = 512 / vg;
+  if (waves > 8) waves = 8;
+  if (waves < 1) waves = 1;
+  int b = waves;  // blocks per CU limited by waves per SIMD (1 wave / SIMD / block)
+  const size_t lds = at.sharedSizeBytes;
+  if (lds > 0) {
+    const int bl = (int)((160 * 1024) / lds);
+    if (bl < b) b = bl;
+  }
+  return b < 1 ? 1 : b;
+}
+
+// Column split of an M-row x N-column pass, R rows per thread, `cap` resident workgroups.
+// The pair loops are latency-bound per wave (long dependent chains through the exp), so the
+// chip needs all its wave slots filled: aim at ~g_split_rounds x cap workgroups (chunk
+// granularity kChunkGran columns).  Deterministic for given (M, N, R, cap, knob).
+constexpr int64_t kChunkGran = 64;
+// 0 = automatic: rounds = clamp(M / 16000, 1, 8) (measured on MI355X: 20k rows -> 1,
+// 50k -> 3-4, 200k -> 8; tools/ab_tune.py); > 0 forces a value (dicp_set_option).
+inline int& split_rounds() {
+  static int r = 0;
+  return r;
+}
+inline int64_t rounds_for(int64_t M) {
+  if (split_rounds() > 0) return split_rounds();
+  int64_t r = M / 16000;
+  return r < 1 ? 1 : (r > 8 ? 8 : r);
+}
+
+inline int64_t round_chunk(int64_t N, int64_t S) {
   int64_t chunk = (N + S - 1) / S;
-  return (chunk + kTile - 1) / kTile * kTile;
+  return (chunk + kChunkGran - 1) / kChunkGran * kChunkGran;
+}
+
+inline int num_splits_cap(int64_t M, int64_t N, int R, int64_t cap) {
+  if (M <= 0 || N <= 0) return 1;
+  const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
+  int64_t S = (rounds_for(M) * cap + bx - 1) / bx;
+  int64_t smax = (N + kMinChunk - 1) / kMinChunk;
+  if (smax < 1) smax = 1;
+  if (S > smax) S = smax;
+  if (S < 1) S = 1;
+  const int64_t chunk = round_chunk(N, S);
+  return (int)((N + chunk - 1) / chunk);
+}
+
+inline int64_t chunk_of(int64_t N, int S) { return round_chunk(N, S); }
+
+template <class Op, int R>
+__global__ __launch_bounds__(kBlock) void rowred_kernel(Args, Scal, int64_t, int64_t, int64_t, Outs);
+
+template <class Op, int R>
+int64_t rowred_capacity() {
+  static int64_t cap = -1;
+  if (cap < 0) cap = (int64_t)device_cus() * blocks_per_cu(rowred_kernel<Op, R>);
+  return cap;
+}
+
+template <class Op, int R>
+int rowred_splits(int64_t M, int64_t N) {
+  return num_splits_cap(M, N, R, rowred_capacity<Op, R>());
 }
 
 inline int check_launch(const char* what) {
@@ -54,7 +122,7 @@ constexpr int total_out_width() {
 
 template <class Op, int R>
 size_t rowred_ws_bytes(int64_t M, int64_t N) {
-  const int S = num_splits(M, N, R);
+  const int S = rowred_splits<Op, R>(M, N);
   if (S <= 1) return 0;
   return (size_t)S * (size_t)M * (size_t)total_out_width<Op>() * sizeof(float);
 }
@@ -65,7 +133,7 @@ template <class Op, int R>
 int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                   const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
   if (M <= 0) return DICP_OK;
-  const int S = num_splits(M, N, R);
+  const int S = rowred_splits<Op, R>(M, N);
   const int64_t chunk = N > 0 ? chunk_of(N, S) : 0;
   const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
   if (bx > 0x7fffffff) {

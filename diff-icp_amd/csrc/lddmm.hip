@@ -3,12 +3,46 @@
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
 
+#include <stdlib.h>
+
+#include <cmath>
+
 using namespace dicp;
 
 namespace {
 
-constexpr int kR = 2;       // rows per thread for the light reductions / fused forward
-constexpr int kRBwd = 1;    // rows per thread for the (register-heavy) fused backward
+constexpr int kR = 2;       // rows per thread for the light reductions
+
+// Rows per thread of the fused ODE passes (tuning knobs, env DICP_R_FWD / DICP_R_BWD in
+// {1, 2, 4}; read once).  Defaults chosen from measurements on MI355X.
+int env_r(const char* name, int def) {
+  const char* v = getenv(name);
+  if (!v) return def;
+  const int r = atoi(v);
+  return (r == 1 || r == 2 || r == 4) ? r : def;
+}
+int g_r_fwd = -1, g_r_bwd = -1;
+int r_fwd() { if (g_r_fwd < 0) g_r_fwd = env_r("DICP_R_FWD", 2); return g_r_fwd; }
+int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 2); return g_r_bwd; }
+
+template <class Op>
+int launch_r(int R, const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
+             const Outs& o, void* ws, size_t wsb, hipStream_t st) {
+  switch (R) {
+    case 1: return launch_rowred<Op, 1>(name, a, sc, M, N, o, ws, wsb, st);
+    case 4: return launch_rowred<Op, 4>(name, a, sc, M, N, o, ws, wsb, st);
+    default: return launch_rowred<Op, 2>(name, a, sc, M, N, o, ws, wsb, st);
+  }
+}
+
+template <class Op>
+size_t ws_r(int R, int64_t M, int64_t N) {
+  switch (R) {
+    case 1: return rowred_ws_bytes<Op, 1>(M, N);
+    case 4: return rowred_ws_bytes<Op, 4>(M, N);
+    default: return rowred_ws_bytes<Op, 2>(M, N);
+  }
+}
 
 template <template <int> class OpT>
 int red_dispatch(const char* name, int D, const Args& a, const Scal& sc, int64_t M, int64_t N,
@@ -32,9 +66,31 @@ size_t red_ws(int D, int64_t M, int64_t N) {
 
 bool supported_dim(int D) { return D == 2 || D == 3; }
 
+// Scaled-coordinate ops (OpOdeSelfFwd / OpOdeSelfBwd): alpha = sqrt(log2 e / (2 sigma^2)),
+// aux1 = s / alpha.
+void scale_coords(Args& a, Scal& sc, double sigma) {
+  const double alpha = std::sqrt(1.4426950408889634 / (2.0 * sigma * sigma));
+  a.scale = (float)alpha;
+  sc.aux1 = (float)(1.0 / (sigma * sigma) / alpha);
+}
+
 }  // namespace
 
 extern "C" int dicp_supports_dim(int D) { return supported_dim(D) ? 1 : 0; }
+
+// Tuning knobs (A/B measurements in one process): "r_fwd", "r_bwd" in {1, 2, 4}.
+extern "C" int dicp_set_option(const char* name, int value) {
+  if (!strcmp(name, "split_rounds")) {
+    if (value < 0 || value > 64) return DICP_ERR_INVALID;  // 0 = automatic
+    split_rounds() = value;
+    return DICP_OK;
+  }
+  if (value != 1 && value != 2 && value != 4) return DICP_ERR_INVALID;
+  if (!strcmp(name, "r_fwd")) { g_r_fwd = value; return DICP_OK; }
+  if (!strcmp(name, "r_bwd")) { g_r_bwd = value; return DICP_OK; }
+  set_error("dicp_set_option: unknown option %s", name);
+  return DICP_ERR_INVALID;
+}
 
 extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float* y, int64_t N,
                                   int D, const float* b, const float* c, double sigma, float* out,
@@ -80,32 +136,37 @@ namespace {
 template <int D>
 int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, double eta, float* v,
                    float* mG, float* g, float* h, void* ws, size_t wsb, hipStream_t st) {
-  const Args a = {q, p, nullptr, nullptr, q, p, nullptr, nullptr};
-  const Scal sc = make_scal(sigma, eta);
+  Args a = {q, p, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
+  Scal sc = make_scal(sigma, eta);
+  scale_coords(a, sc, sigma);
   const Outs o = make_outs(v, mG, g, h);
   if (eta != 0.0)
-    return launch_rowred<OpOdeSelfFwd<D, true, true>, kR>("ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
+    return launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
   if (g != nullptr)
-    return launch_rowred<OpOdeSelfFwd<D, false, true>, kR>("ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
-  return launch_rowred<OpOdeSelfFwd<D, false, false>, kR>("ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
+    return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
+  return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
 }
 
 template <int D>
 size_t ode_self_fwd_ws(int64_t M) {
-  size_t a = rowred_ws_bytes<OpOdeSelfFwd<D, true, true>, kR>(M, M);
-  size_t b = rowred_ws_bytes<OpOdeSelfFwd<D, false, true>, kR>(M, M);
-  return a > b ? a : b;
+  // every variant that ode_self_fwd_d may launch (their occupancies, hence splits, differ)
+  size_t a = ws_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), M, M);
+  size_t b = ws_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), M, M);
+  size_t c = ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), M, M);
+  a = a > b ? a : b;
+  return a > c ? a : c;
 }
 
 template <int D>
 int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float* gmG,
                    const float* gdiv, int64_t M, double sigma, float* gq, float* gp, void* ws,
                    size_t wsb, hipStream_t st) {
-  const Args a = {q, p, gv, gmG, q, p, gv, gmG};
+  Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
   Scal sc = make_scal(sigma, 0.0);
+  scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
   const Outs o = make_outs(gq, gp);
-  return launch_rowred<OpOdeSelfBwd<D>, kRBwd>("ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
+  return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
 }
 
 template <int D>
@@ -125,9 +186,13 @@ int ode_ext_fwd_d(const float* x, int64_t N, const float* q, const float* p, int
 
 template <int D>
 size_t ode_ext_fwd_ws(int64_t N, int64_t M) {
-  size_t a = rowred_ws_bytes<OpOdeExtFwd<D, true, true>, kR>(N, M);
-  size_t b = rowred_ws_bytes<OpOdeExtFwd<D, false, true>, kR>(N, M);
-  return a > b ? a : b;
+  size_t m = 0;
+  for (size_t v : {rowred_ws_bytes<OpOdeExtFwd<D, true, true>, kR>(N, M),
+                   rowred_ws_bytes<OpOdeExtFwd<D, true, false>, kR>(N, M),
+                   rowred_ws_bytes<OpOdeExtFwd<D, false, true>, kR>(N, M),
+                   rowred_ws_bytes<OpOdeExtFwd<D, false, false>, kR>(N, M)})
+    m = v > m ? v : m;
+  return m;
 }
 
 template <int D>
@@ -253,8 +318,7 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
     }
     case DICP_WS_ODE_SELF_FWD: return D == 2 ? ode_self_fwd_ws<2>(M) : ode_self_fwd_ws<3>(M);
     case DICP_WS_ODE_SELF_BWD:
-      return D == 2 ? rowred_ws_bytes<OpOdeSelfBwd<2>, kRBwd>(M, M)
-                    : rowred_ws_bytes<OpOdeSelfBwd<3>, kRBwd>(M, M);
+      return D == 2 ? ws_r<OpOdeSelfBwd<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd<3>>(r_bwd(), M, M);
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);
     case DICP_WS_ODE_EXT_BWD: return D == 2 ? ode_ext_bwd_ws<2>(N, M) : ode_ext_bwd_ws<3>(N, M);
     default: return 0;
@@ -263,8 +327,14 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
 
 int dicp_lddmm_splits(int kind, int64_t M, int64_t N) {
   switch (kind) {
-    case DICP_WS_ODE_SELF_BWD: return num_splits(M, M, kRBwd);
-    case DICP_WS_ODE_SELF_FWD: return num_splits(M, M, kR);
-    default: return num_splits(M, N, kR);
+    case DICP_WS_ODE_SELF_BWD:
+      return r_bwd() == 1 ? rowred_splits<OpOdeSelfBwd<3>, 1>(M, M)
+           : r_bwd() == 2 ? rowred_splits<OpOdeSelfBwd<3>, 2>(M, M)
+                          : rowred_splits<OpOdeSelfBwd<3>, 4>(M, M);
+    case DICP_WS_ODE_SELF_FWD:
+      return r_fwd() == 1 ? rowred_splits<OpOdeSelfFwd<3, false, true>, 1>(M, M)
+           : r_fwd() == 2 ? rowred_splits<OpOdeSelfFwd<3, false, true>, 2>(M, M)
+                          : rowred_splits<OpOdeSelfFwd<3, false, true>, 4>(M, M);
+    default: return rowred_splits<OpKRed<3>, kR>(M, N);
   }
 }

@@ -324,18 +324,30 @@ struct OpMinSqDist {
 // Fused LDDMM ODE right-hand side on the support points (LDDMMModel.ODE, LDDMM.py:176-227).
 // Rows and columns are both (q, p).  One exp per pair feeds every term.
 //
+// Scaled coordinates: q' = alpha q, alpha = sqrt(log2(e)/(2 sigma^2)) (Args::scale), so
+// z' = alpha z and K = exp2(-|z'|^2) with no per-pair multiply; s2 = s / alpha^2 = 2 ln 2.
 // ETA=false (classic / hybrid, eta = 0):
-//   V = sum K p_j,  Z = sum K z,  Gs = sum K z (p_i.p_j)
-//   v = V ; mG = -GenDKRed = s Gs ; g = p_i . GradKRed_i = -s p_i.Z ; h = 1/2 p_i.V
+//   V = sum K p_j,  Z' = sum K z',  Gs' = sum K z' (p_i.p_j)
+//   v = V ; mG = -GenDKRed = (s/alpha) Gs' ; g = p_i.GradKRed_i = -(s/alpha) p_i.Z' ;
+//   h = 1/2 p_i.V
 // ETA=true (logdet, eta = 1/lambda), additionally with u = p_i - p_j:
-//   Hs = sum K [s (z.u) z - u]   (HessKRed = s Hs),   GL = sum K z (s r2 - (D+2))
-//   (GradLapKRed = -s^2 GL),  L = sum K (s r2 - D)  (LapKRed = s L)
-//   v  = V + eta s Z                                             (LDDMM.py:114)
-//   mG = s Gs + eta s Hs - eta^2 s^2 GL                          (LDDMM.py:201-203)
-//   g  = -s p_i.Z + eta s L                                      (LDDMM.py:135)
-//   h  = 1/2 p_i.V + eta s p_i.Z - 1/2 eta^2 s L                 (LDDMM.py:151-153)
-// 3D cost (ETA=false, DIV=true): ~36 flop + 1 T per pair.
+//   Hs = sum K [s2 (z'.u) z' - u]        (HessKRed = s Hs),
+//   GL' = sum K z' (s2 r2' - (D+2))       (GradLapKRed = -(s^2/alpha) GL'),
+//   L = sum K (s2 r2' - D)                (LapKRed = s L)
+//   v  = V + eta (s/alpha) Z'                                     (LDDMM.py:114)
+//   mG = (s/alpha) Gs' + eta s Hs - eta^2 (s^2/alpha) GL'         (LDDMM.py:201-203)
+//   g  = -(s/alpha) p_i.Z' + eta s L                              (LDDMM.py:135)
+//   h  = 1/2 p_i.V + eta (s/alpha) p_i.Z' - 1/2 eta^2 s L         (LDDMM.py:151-153)
+// 3D cost (ETA=false, DIV=true): 33 flop + 1 T per pair.
 // -------------------------------------------------------------------------------------
+constexpr float kS2 = 1.3862943611198906f;  // s / alpha^2 = 2 ln 2
+
+template <int D>
+__device__ __forceinline__ void ld_scaled(const float* __restrict__ p, int64_t i, float a, float* dst) {
+#pragma unroll
+  for (int d = 0; d < D; ++d) dst[d] = a * p[i * D + d];
+}
+
 template <int D, bool ETA, bool DIV>
 struct OpOdeSelfFwd {
   static constexpr int CW4 = cw4(2 * D);
@@ -345,66 +357,66 @@ struct OpOdeSelfFwd {
   static constexpr bool kMin = false;
   struct Row { float q[D]; float p[D]; };
   __device__ static void load_row(const Args& a, int64_t i, Row& r) {
-    ld<D>(a.r0, i, r.q);
+    ld_scaled<D>(a.r0, i, a.scale, r.q);
     ld<D>(a.r1, i, r.p);
   }
   __device__ static void load_col(const Args& a, int64_t j, float* rec) {
-    ld<D>(a.c0, j, rec);
+    ld_scaled<D>(a.c0, j, a.scale, rec);
     ld<D>(a.c1, j, rec + D);
   }
   __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
     float z[D];
     const float r2 = diff_sq<D>(r.q, rec, z);
-    const float K = fast_exp2(sc.nc * r2);
+    const float K = fast_exp2(-r2);
     const float* pj = rec + D;
     const float Kpp = K * dot<D>(r.p, pj);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       acc[d] = fmaf(K, pj[d], acc[d]);           // V
-      acc[D + d] = fmaf(Kpp, z[d], acc[D + d]);  // Gs
+      acc[D + d] = fmaf(Kpp, z[d], acc[D + d]);  // Gs'
     }
     if (ETA || DIV) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) acc[2 * D + d] = fmaf(K, z[d], acc[2 * D + d]);  // Z
+      for (int d = 0; d < D; ++d) acc[2 * D + d] = fmaf(K, z[d], acc[2 * D + d]);  // Z'
     }
     if (ETA) {
       float u[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) u[d] = r.p[d] - pj[d];
-      const float szu = sc.s * dot<D>(z, u);
-      const float sr2 = sc.s * r2;
+      const float szu = kS2 * dot<D>(z, u);
+      const float sr2 = kS2 * r2;
       const float KGL = K * (sr2 - (float)(D + 2));
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         acc[3 * D + d] = fmaf(K, fmaf(szu, z[d], -u[d]), acc[3 * D + d]);  // Hs
-        acc[4 * D + d] = fmaf(KGL, z[d], acc[4 * D + d]);                   // GL
+        acc[4 * D + d] = fmaf(KGL, z[d], acc[4 * D + d]);                   // GL'
       }
       acc[5 * D] = fmaf(K, sr2 - (float)D, acc[5 * D]);  // L
     }
   }
   __device__ static void store(const Scal& sc, const Row& r, const float* t, float* v) {
-    const float s = sc.s, eta = sc.eta;
+    const float s = sc.s, eta = sc.eta, sa = sc.aux1;  // aux1 = s / alpha
     const float* V = t;
     const float* Gs = t + D;
     const float* Z = t + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       if (ETA) {
-        v[d] = fmaf(eta * s, Z[d], V[d]);
-        v[D + d] = s * Gs[d] + eta * s * t[3 * D + d] - eta * eta * s * s * t[4 * D + d];
+        v[d] = fmaf(eta * sa, Z[d], V[d]);
+        v[D + d] = sa * Gs[d] + eta * s * t[3 * D + d] - eta * eta * s * sa * t[4 * D + d];
       } else {
         v[d] = V[d];
-        v[D + d] = s * Gs[d];
+        v[D + d] = sa * Gs[d];
       }
     }
     const float pV = dot<D>(r.p, V);
     if (ETA) {
       const float pZ = dot<D>(r.p, Z);
       const float L = t[5 * D];
-      v[2 * D] = -s * pZ + eta * s * L;
-      v[2 * D + 1] = 0.5f * pV + eta * s * pZ - 0.5f * eta * eta * s * L;
+      v[2 * D] = -sa * pZ + eta * s * L;
+      v[2 * D + 1] = 0.5f * pV + eta * sa * pZ - 0.5f * eta * eta * s * L;
     } else {
-      v[2 * D] = DIV ? -s * dot<D>(r.p, Z) : 0.f;
+      v[2 * D] = DIV ? -sa * dot<D>(r.p, Z) : 0.f;
       v[2 * D + 1] = 0.5f * pV;
     }
   }
@@ -412,12 +424,15 @@ struct OpOdeSelfFwd {
 
 // -------------------------------------------------------------------------------------
 // VJP of OpOdeSelfFwd (eta = 0): cotangents a = dL/dv, bm = dL/dmG, gam = dL/d(sum g).
-// Row m, column j, z = q_m - q_j (derivation in DESIGN.md, verified against torch
-// autograd of the reference formulas in tests/test_ode_grad.py):
+// Row m, column j, z = q_m - q_j (derivation in DESIGN.md; checked against torch autograd
+// of the oracle in tests/test_gpu_kernels.py::test_ode_self_bwd):
 //   gp_m = sum_j K [ a_j + s ((bm_m - bm_j).z) p_j - s gam z ]
 //   gq_m = s sum_j K [ (p_m.p_j)(bm_m - bm_j) - gam (p_m - p_j)
 //                      + z ( s (gam (p_m-p_j).z - (p_m.p_j)(bm_m-bm_j).z) - (a_m.p_j + a_j.p_m) ) ]
-// 3D cost ~80 flop + 1 T per pair.
+// In scaled coordinates (z' = alpha z, s1 = s/alpha, s2 = s/alpha^2, ia = 1/alpha):
+//   gp_m = sum_j K [ a_j + s1 (db.z') p_j - s1 gam z' ]
+//   gq_m = s sum_j K [ pp db - gam dp + z' (s2 (gam dp.z' - pp db.z') - ia ap) ]
+// 3D cost: 89 flop + 1 T per pair.
 // -------------------------------------------------------------------------------------
 template <int D>
 struct OpOdeSelfBwd {
@@ -426,23 +441,27 @@ struct OpOdeSelfBwd {
   static constexpr int kNOut = 2;
   static constexpr int kOutW[4] = {D, D, 0, 0};
   static constexpr bool kMin = false;
-  struct Row { float q[D]; float p[D]; float a[D]; float b[D]; };
+  // ap is evaluated with the row's a, p pre-multiplied by 1/alpha (ia_a, ia_p)
+  struct Row { float q[D]; float p[D]; float b[D]; float ia_a[D]; float ia_p[D]; };
   __device__ static void load_row(const Args& a, int64_t i, Row& r) {
-    ld<D>(a.r0, i, r.q);
+    ld_scaled<D>(a.r0, i, a.scale, r.q);
     ld<D>(a.r1, i, r.p);
-    ld<D>(a.r2, i, r.a);
     ld<D>(a.r3, i, r.b);
+    const float ia = 1.0f / a.scale;
+    ld_scaled<D>(a.r2, i, ia, r.ia_a);
+#pragma unroll
+    for (int d = 0; d < D; ++d) r.ia_p[d] = ia * r.p[d];
   }
   __device__ static void load_col(const Args& a, int64_t j, float* rec) {
-    ld<D>(a.c0, j, rec);
+    ld_scaled<D>(a.c0, j, a.scale, rec);
     ld<D>(a.c1, j, rec + D);
     ld<D>(a.c2, j, rec + 2 * D);
     ld<D>(a.c3, j, rec + 3 * D);
   }
   __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
-    const float s = sc.s, gam = sc.aux0;
+    const float s1 = sc.aux1, gam = sc.aux0;
     float z[D], db[D], dp[D];
-    const float K = fast_exp2(sc.nc * diff_sq<D>(r.q, rec, z));
+    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
     const float* bj = rec + 3 * D;
@@ -452,12 +471,13 @@ struct OpOdeSelfBwd {
       dp[d] = r.p[d] - pj[d];
     }
     const float pp = dot<D>(r.p, pj);
-    const float ap = dot<D>(r.a, pj) + dot<D>(aj, r.p);
+    const float iap = dot<D>(r.ia_a, pj) + dot<D>(aj, r.ia_p);
     const float zb = dot<D>(z, db);
     const float zp = dot<D>(z, dp);
-    const float t1 = K * s * zb;
-    const float t2 = K * s * gam;
-    const float w = s * (gam * zp - pp * zb) - ap;
+    const float Ks1 = K * s1;
+    const float t1 = Ks1 * zb;
+    const float t2 = Ks1 * gam;
+    const float w = fmaf(kS2, fmaf(-pp, zb, gam * zp), -iap);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       acc[d] = fmaf(K, aj[d], fmaf(t1, pj[d], fmaf(-t2, z[d], acc[d])));            // gp

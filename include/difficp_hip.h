@@ -161,6 +161,9 @@ const char* dicp_last_error(void);
 const char* dicp_version(void);
 /* 1 if D is compiled in. */
 int dicp_supports_dim(int D);
+/* Tuning knobs for measurements: "r_fwd" / "r_bwd" = rows per thread {1,2,4} of the fused
+ * ODE forward / backward passes (defaults from env DICP_R_FWD / DICP_R_BWD or built-in). */
+int dicp_set_option(const char* name, int value);
 /* Number of column splits the library will use for an M x N pass (diagnostics/bench). */
 int dicp_num_splits(int kind, int64_t M, int64_t N);
 

@@ -1,0 +1,69 @@
+"""Interleaved A/B timing of tuning variants in ONE process (cdna_hip_programming.md 5.4
+rule 24): rows-per-thread of the fused ODE forward / backward.
+
+    python tools/ab_tune.py [--M 50000] [--rounds 5]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from difficp_amd import _lib  # noqa: E402
+
+
+def t_once(fn, reps=3):
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        fn()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=50000)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    M, D = a.M, 3
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    q = torch.rand(M, D, device=dev)
+    p = 0.01 * torch.randn(M, D, device=dev)
+    ga = torch.randn(M, D, device=dev)
+    gb = torch.randn(M, D, device=dev)
+    gd = torch.ones(1, device=dev)
+    variants = []
+    fwd = lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True)
+    bwd = lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0)
+    for sr in (1, 2, 4, 8):
+        for r in (1, 2):
+            variants.append((f"fwd_r{r}_s{sr}", {"r_fwd": r, "split_rounds": sr}, fwd))
+            variants.append((f"bwd_r{r}_s{sr}", {"r_bwd": r, "split_rounds": sr}, bwd))
+    res = {v[0]: [] for v in variants}
+
+    def setopts(o):
+        for k, v in o.items():
+            _lib.set_option(k, v)
+
+    for name, o, fn in variants:  # warm every variant once
+        setopts(o)
+        fn()
+    torch.cuda.synchronize()
+    for _ in range(a.rounds):
+        for name, o, fn in variants:
+            setopts(o)
+            res[name].append(t_once(fn))
+    out = {k: {"median_ms": statistics.median(v), "min_ms": min(v),
+               "Gpairs_per_s": M * M / (min(v) * 1e-3) / 1e9} for k, v in res.items()}
+    print(json.dumps({"M": M, "ab": out}))
+
+
+if __name__ == "__main__":
+    main()
