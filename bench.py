@@ -96,6 +96,17 @@ def load_traffic(kernel_name):
 
 
 def main():
+    # the driver parses ONE JSON line from stdout: everything else (e.g. the reference's
+    # "GMM optimization - reached maximum number of iterations" message) goes to stderr
+    real_stdout = sys.stdout
+    sys.stdout = sys.stderr
+    try:
+        _main(real_stdout)
+    finally:
+        sys.stdout = real_stdout
+
+
+def _main(out):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -210,7 +221,7 @@ def main():
             "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                             "Gpairs": round(v["pairs"] / 1e9, 3)} for k, v in summ.items()},
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

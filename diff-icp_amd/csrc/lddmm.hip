@@ -159,9 +159,15 @@ size_t ode_self_fwd_ws(int64_t M) {
 
 template <int D>
 int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float* gmG,
-                   const float* gdiv, int64_t M, double sigma, float* gq, float* gp, void* ws,
-                   size_t wsb, hipStream_t st) {
+                   const float* gdiv, int64_t M, double sigma, double eta, float* gq, float* gp,
+                   void* ws, size_t wsb, hipStream_t st) {
   Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
+  if (eta != 0.0) {
+    Scal sc = make_scal(sigma, eta);
+    sc.dev0 = gdiv;
+    const Outs o = make_outs(gq, gp);
+    return launch_r<OpOdeSelfBwdEta<D>>(r_bwd(), "ode_self_bwd_eta", a, sc, M, M, o, ws, wsb, st);
+  }
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
@@ -197,15 +203,17 @@ size_t ode_ext_fwd_ws(int64_t N, int64_t M) {
 
 template <int D>
 int ode_ext_bwd_d(const float* x, int64_t N, const float* q, const float* p, int64_t M,
-                  double sigma, const float* gvx, const float* gdiv, float* gxo, float* gq,
-                  float* gp, void* ws, size_t wsb, hipStream_t st) {
-  Scal sc = make_scal(sigma, 0.0);
+                  double sigma, double eta, const float* gvx, const float* gdiv, float* gxo,
+                  float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
+  Scal sc = make_scal(sigma, eta);
   sc.dev0 = gdiv;
   // rows x: gradient w.r.t. the carried points
   {
     const Args a = {x, gvx, nullptr, nullptr, q, p, nullptr, nullptr};
     const Outs o = make_outs(gxo);
-    int rc = launch_rowred<OpOdeExtBwdX<D>, kR>("ode_ext_bwd_x", a, sc, N, M, o, ws, wsb, st);
+    int rc = eta != 0.0
+        ? launch_rowred<OpOdeExtBwdXEta<D>, kR>("ode_ext_bwd_x", a, sc, N, M, o, ws, wsb, st)
+        : launch_rowred<OpOdeExtBwdX<D>, kR>("ode_ext_bwd_x", a, sc, N, M, o, ws, wsb, st);
     if (rc) return rc;
   }
   // rows q: gradient w.r.t. support points and momenta (accumulated)
@@ -213,15 +221,20 @@ int ode_ext_bwd_d(const float* x, int64_t N, const float* q, const float* p, int
     const Args a = {q, p, nullptr, nullptr, x, gvx, nullptr, nullptr};
     Outs o = make_outs(gq, gp);
     o.accumulate[0] = o.accumulate[1] = 1;
-    return launch_rowred<OpOdeExtBwdQ<D>, kR>("ode_ext_bwd_q", a, sc, M, N, o, ws, wsb, st);
+    return eta != 0.0
+        ? launch_rowred<OpOdeExtBwdQEta<D>, kR>("ode_ext_bwd_q", a, sc, M, N, o, ws, wsb, st)
+        : launch_rowred<OpOdeExtBwdQ<D>, kR>("ode_ext_bwd_q", a, sc, M, N, o, ws, wsb, st);
   }
 }
 
 template <int D>
 size_t ode_ext_bwd_ws(int64_t N, int64_t M) {
-  size_t a = rowred_ws_bytes<OpOdeExtBwdX<D>, kR>(N, M);
-  size_t b = rowred_ws_bytes<OpOdeExtBwdQ<D>, kR>(M, N);
-  return a > b ? a : b;
+  size_t m = 0;
+  for (size_t v : {rowred_ws_bytes<OpOdeExtBwdX<D>, kR>(N, M), rowred_ws_bytes<OpOdeExtBwdQ<D>, kR>(M, N),
+                   rowred_ws_bytes<OpOdeExtBwdXEta<D>, kR>(N, M),
+                   rowred_ws_bytes<OpOdeExtBwdQEta<D>, kR>(M, N)})
+    m = v > m ? v : m;
+  return m;
 }
 
 }  // namespace
@@ -252,13 +265,9 @@ extern "C" int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const
     set_error("dicp_lddmm_ode_self_bwd_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }
-  if (eta != 0.0) {
-    set_error("ode_self_bwd: eta != 0 (gradcomponent=True) backward not compiled in yet");
-    return DICP_ERR_UNSUPPORTED;
-  }
   switch (D) {
-    case 2: return ode_self_bwd_d<2>(q, p, gv, gmG, gdiv, M, sigma, gq, gp, ws, ws_bytes, st);
-    case 3: return ode_self_bwd_d<3>(q, p, gv, gmG, gdiv, M, sigma, gq, gp, ws, ws_bytes, st);
+    case 2: return ode_self_bwd_d<2>(q, p, gv, gmG, gdiv, M, sigma, eta, gq, gp, ws, ws_bytes, st);
+    case 3: return ode_self_bwd_d<3>(q, p, gv, gmG, gdiv, M, sigma, eta, gq, gp, ws, ws_bytes, st);
     default: set_error("ode_self_bwd: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
@@ -290,13 +299,9 @@ extern "C" int dicp_lddmm_ode_ext_bwd_f32(const float* x, int64_t N, const float
     set_error("dicp_lddmm_ode_ext_bwd_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }
-  if (eta != 0.0) {
-    set_error("ode_ext_bwd: eta != 0 (gradcomponent=True) backward not compiled in yet");
-    return DICP_ERR_UNSUPPORTED;
-  }
   switch (D) {
-    case 2: return ode_ext_bwd_d<2>(x, N, q, p, M, sigma, gvx, gdiv, gxo, gq, gp, ws, ws_bytes, st);
-    case 3: return ode_ext_bwd_d<3>(x, N, q, p, M, sigma, gvx, gdiv, gxo, gq, gp, ws, ws_bytes, st);
+    case 2: return ode_ext_bwd_d<2>(x, N, q, p, M, sigma, eta, gvx, gdiv, gxo, gq, gp, ws, ws_bytes, st);
+    case 3: return ode_ext_bwd_d<3>(x, N, q, p, M, sigma, eta, gvx, gdiv, gxo, gq, gp, ws, ws_bytes, st);
     default: set_error("ode_ext_bwd: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
@@ -318,7 +323,11 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
     }
     case DICP_WS_ODE_SELF_FWD: return D == 2 ? ode_self_fwd_ws<2>(M) : ode_self_fwd_ws<3>(M);
     case DICP_WS_ODE_SELF_BWD:
-      return D == 2 ? ws_r<OpOdeSelfBwd<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd<3>>(r_bwd(), M, M);
+    {
+      size_t a = D == 2 ? ws_r<OpOdeSelfBwd<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd<3>>(r_bwd(), M, M);
+      size_t b = D == 2 ? ws_r<OpOdeSelfBwdEta<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwdEta<3>>(r_bwd(), M, M);
+      return a > b ? a : b;
+    }
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);
     case DICP_WS_ODE_EXT_BWD: return D == 2 ? ode_ext_bwd_ws<2>(N, M) : ode_ext_bwd_ws<3>(N, M);
     default: return 0;

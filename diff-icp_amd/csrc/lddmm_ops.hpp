@@ -614,4 +614,159 @@ struct OpOdeExtBwdQ {
   }
 };
 
+// -------------------------------------------------------------------------------------
+// VJP of the fused self ODE with gradcomponent (eta = 1/lambda != 0, "logdet" model,
+// LDDMM.py:198-203 + :133-135).  Row m, column j, z = q_m - q_j, d* = *_m - *_j:
+//   gp_m = sum_j K [ a_j + s zb p_j + eta s (s zb z - db) - gam s z ]
+//   gq_m = sum_j K [ eta s da + s pp db + eta s^2 (zb dp + zp db)
+//                    - eta^2 s^2 ((s r2 - D - 2) db + 2 s zb z) - gam s dp + 4 gam eta s^2 z
+//                    - s Phi z ]
+//   Phi = ap + eta s za + s pp zb + eta s (s zp zb - db.dp) - eta^2 s^2 zb (s r2 - D - 2)
+//         - gam s zp + 2 gam eta s (s r2 - D)
+// with zb = db.z, zp = dp.z, za = da.z, pp = p_m.p_j, ap = a_m.p_j + a_j.p_m
+// (checked against torch autograd of the oracle, tests/test_gpu_kernels.py).
+// -------------------------------------------------------------------------------------
+template <int D>
+struct OpOdeSelfBwdEta {
+  static constexpr int CW4 = cw4(4 * D);
+  static constexpr int NACC = 2 * D;
+  static constexpr int kNOut = 2;
+  static constexpr int kOutW[4] = {D, D, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float q[D]; float p[D]; float a[D]; float b[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.q);
+    ld<D>(a.r1, i, r.p);
+    ld<D>(a.r2, i, r.a);
+    ld<D>(a.r3, i, r.b);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+    ld<D>(a.c2, j, rec + 2 * D);
+    ld<D>(a.c3, j, rec + 3 * D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    const float s = sc.s, eta = sc.eta, gam = sc.aux0;
+    float z[D], da[D], db[D], dp[D];
+    const float r2 = diff_sq<D>(r.q, rec, z);
+    const float K = fast_exp2(sc.nc * r2);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      da[d] = r.a[d] - aj[d];
+      db[d] = r.b[d] - bj[d];
+      dp[d] = r.p[d] - pj[d];
+    }
+    const float pp = dot<D>(r.p, pj);
+    const float ap = dot<D>(r.a, pj) + dot<D>(aj, r.p);
+    const float zb = dot<D>(z, db), zp = dot<D>(z, dp), za = dot<D>(z, da), bp = dot<D>(db, dp);
+    const float es = eta * s, es2 = es * s, e2s2 = eta * es2, gs = gam * s;
+    const float sr2 = s * r2;
+    const float Phi = ap + es * za + s * pp * zb + es * (s * zp * zb - bp) -
+                      e2s2 * zb * (sr2 - (float)(D + 2)) - gs * zp + 2.f * gam * es * (sr2 - (float)D);
+    const float cz_p = s * zb * es - gs;                      // gp: coefficient of z
+    const float cz_q = -2.f * e2s2 * s * zb + 4.f * gam * es2 - s * Phi;  // gq: coefficient of z
+    const float cdb = s * pp + es2 * zp - e2s2 * (sr2 - (float)(D + 2));
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, aj[d] + s * zb * pj[d] - es * db[d] + cz_p * z[d], acc[d]);           // gp
+      acc[D + d] = fmaf(K, es * da[d] + cdb * db[d] + es2 * zb * dp[d] - gs * dp[d] + cz_q * z[d],
+                        acc[D + d]);                                                        // gq
+    }
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      v[d] = t[D + d];  // gq
+      v[D + d] = t[d];  // gp
+    }
+  }
+};
+
+// VJP of the external-point ODE terms with gradcomponent (eta != 0), rows x_i (+ a_i):
+//   dF/dz = K [ eta s a_i + gam s p_j + 2 gam eta s^2 z - s Phi z ],
+//   Phi = a_i.p_j + eta s (a_i.z) + gam s (z.p_j) + gam eta s (s r2 - D);   gx_i = sum_j dF/dz
+template <int D>
+struct OpOdeExtBwdXEta {
+  static constexpr int CW4 = cw4(2 * D);
+  static constexpr int NACC = D;
+  static constexpr int kNOut = 1;
+  static constexpr int kOutW[4] = {D, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; float a[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.x);
+    ld<D>(a.r1, i, r.a);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    const float s = sc.s, eta = sc.eta, gam = sc.aux0;
+    float z[D];
+    const float r2 = diff_sq<D>(r.x, rec, z);
+    const float K = fast_exp2(sc.nc * r2);
+    const float* pj = rec + D;
+    const float es = eta * s, gs = gam * s;
+    const float Phi = dot<D>(r.a, pj) + es * dot<D>(r.a, z) + gs * dot<D>(z, pj) +
+                      gam * es * (s * r2 - (float)D);
+    const float cz = 2.f * gam * es * s - s * Phi;
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, es * r.a[d] + gs * pj[d] + cz * z[d], acc[d]);
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = t[d];
+  }
+};
+
+// ... and w.r.t. (q_j, p_j) as a row reduction over supports (z' = q_j - x_i = -z):
+//   gq_j = -sum_i K [ eta s a_i + gam s p_j - 2 gam eta s^2 z' + s Phi' z' ],
+//   Phi' = a_i.p_j - eta s (a_i.z') - gam s (z'.p_j) + gam eta s (s r2 - D);
+//   gp_j = sum_i K [ a_i - gam s z' ]
+template <int D>
+struct OpOdeExtBwdQEta {
+  static constexpr int CW4 = cw4(2 * D);
+  static constexpr int NACC = 2 * D;
+  static constexpr int kNOut = 2;
+  static constexpr int kOutW[4] = {D, D, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float q[D]; float p[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.q);
+    ld<D>(a.r1, i, r.p);
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    ld<D>(a.c1, j, rec + D);
+  }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    const float s = sc.s, eta = sc.eta, gam = sc.aux0;
+    float z[D];
+    const float r2 = diff_sq<D>(r.q, rec, z);
+    const float K = fast_exp2(sc.nc * r2);
+    const float* ai = rec + D;
+    const float es = eta * s, gs = gam * s;
+    const float Phi = dot<D>(ai, r.p) - es * dot<D>(ai, z) - gs * dot<D>(z, r.p) +
+                      gam * es * (s * r2 - (float)D);
+    const float cz = -2.f * gam * es * s + s * Phi;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, fmaf(-gs, z[d], ai[d]), acc[d]);                             // gp
+      acc[D + d] = fmaf(K, es * ai[d] + gs * r.p[d] + cz * z[d], acc[D + d]);      // -gq
+    }
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      v[d] = -t[D + d];  // gq
+      v[D + d] = t[d];   // gp
+    }
+  }
+};
+
 }  // namespace dicp

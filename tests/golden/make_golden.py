@@ -1,0 +1,228 @@
+"""Generate the golden fixtures of tests/golden/*.npz by IMPORTING THE REFERENCE ITSELF
+(AdrienWohrer/diff-icp at /root/reference, torch path) -- build container only; the GPU
+box never runs this (the reference does not exist there).  No reference source is copied:
+the script imports the package and records inputs/outputs of its public functions.
+
+pykeops is absent, and diffICP/tools/point_sets.py:8 imports it unconditionally, so a stub
+module is placed in sys.modules AFTER importing kernel/LDDMM (which guard their import), and
+GMM.use_keops is forced False: every computversion then resolves to the reference's own
+torch implementation.
+
+    python tests/golden/make_golden.py
+"""
+import importlib.machinery
+import os
+import sys
+import types
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+
+
+def import_reference():
+    import matplotlib
+    matplotlib.use("Agg")
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    import diffICP.tools.kernel as K  # noqa: F401  (guarded keops import -> torch path)
+    import diffICP.core.LDDMM as L  # noqa: F401
+    pk = types.ModuleType("pykeops")
+    pk.__spec__ = importlib.machinery.ModuleSpec("pykeops", None)
+    pkt = types.ModuleType("pykeops.torch")
+    pkt.__spec__ = importlib.machinery.ModuleSpec("pykeops.torch", None)
+
+    def _nope(*a, **k):
+        raise RuntimeError("keops unavailable")
+    pkt.LazyTensor = pkt.Vi = pkt.Vj = pkt.Pm = _nope
+    pk.torch = pkt
+    sys.modules["pykeops"] = pk
+    sys.modules["pykeops.torch"] = pkt
+    import diffICP.core.GMM as G
+    G.use_keops = False
+    import diffICP.core.PSR as P
+
+    # kernel.py:328's torch branch compares a (values, indices) namedtuple with a float and
+    # raises; patch in the intended boolean for non-dense supports.
+    def check_coverage(self, X, Y, Rthreshold):
+        return ((X[:, None, :] - Y[None, :, :]) ** 2).sum(-1).min(dim=1).values > (Rthreshold * self.sigma) ** 2
+    K.GaussKernel.check_coverage = check_coverage
+    return K, L, G, P
+
+
+def main():
+    import torch
+    K, L, G, P = import_reference()
+    torch.manual_seed(20261015)
+    f64 = torch.float64
+
+    # ---------------- 1. the ten reductions (kernel.py:177-292) ----------------
+    red = {}
+    for (M, N, D, sig) in [(64, 96, 2, 0.05), (64, 96, 3, 0.2), (64, 96, 2, 1.0), (300, 300, 3, 0.2)]:
+        key = f"M{M}_N{N}_D{D}_s{sig}"
+        g = torch.Generator().manual_seed(M * 7 + N + D)
+        x = torch.rand(M, D, generator=g, dtype=f64)
+        y = torch.rand(N, D, generator=g, dtype=f64)
+        b = torch.randn(N, D, generator=g, dtype=f64)
+        c = torch.randn(M, D, generator=g, dtype=f64)
+        d = torch.randn(N, generator=g, dtype=f64)
+        dm = torch.randn(M, D, generator=g, dtype=f64)
+        GK = K.GaussKernel(sig, D, computversion="torch", spec={"device": "cpu", "dtype": f64})
+        for nm, t in dict(x=x, y=y, b=b, c=c, d=d, dm=dm).items():
+            red[f"{key}/in_{nm}"] = t.numpy()
+        red[f"{key}/sigma"] = np.array(sig)
+        red[f"{key}/KBase"] = GK.KBase(x, y).numpy()
+        red[f"{key}/KRedScal"] = GK.KRedScal(x, y, d).numpy()
+        red[f"{key}/KRed"] = GK.KRed(x, y, b).numpy()
+        red[f"{key}/GradKRed"] = GK.GradKRed(x, y).numpy()
+        red[f"{key}/GradKRed_rev"] = GK.GradKRed_rev(x, y, dm).numpy()
+        red[f"{key}/DDKRed"] = GK.DDKRed(x, y, b).numpy()
+        red[f"{key}/GenDKRed"] = GK.GenDKRed(x, y, b, c).numpy()
+        red[f"{key}/HessKRed"] = GK.HessKRed(x, y, b, c).numpy()
+        red[f"{key}/LapKRed"] = GK.LapKRed(x, y).numpy()
+        red[f"{key}/GradLapKRed"] = GK.GradLapKRed(x, y).numpy()
+    np.savez_compressed(os.path.join(HERE, "reductions.npz"), **red)
+
+    # ---------------- 2. LDDMM shooting + gradients (LDDMM.py:100-334) ----------------
+    sh = {}
+    for version in ("classic", "hybrid", "logdet"):
+        for scheme in ("Euler", "Ralston"):
+            for ext in (0, 30):
+                for D in (2, 3):
+                    key = f"{version}_{scheme}_x{ext}_D{D}"
+                    g = torch.Generator().manual_seed(zlib.crc32(key.encode()))
+                    M, lam, sig, nt = 40, 50.0, 0.3, 6
+                    q0 = torch.rand(M, D, generator=g, dtype=f64)
+                    p0 = 0.05 * torch.randn(M, D, generator=g, dtype=f64)
+                    x0 = torch.rand(ext, D, generator=g, dtype=f64) if ext else None
+                    tgt = torch.randn(ext if ext else M, D, generator=g, dtype=f64)
+                    LM = L.LDDMMModel(sigma=sig, D=D, lambd=lam, version=version, scheme=scheme, nt=nt,
+                                      computversion="torch", spec={"device": "cpu", "dtype": f64})
+                    pr = p0.clone().requires_grad_(True)
+                    s = LM.Shoot(q0, pr, x0)
+                    last = s[-1][-1] if ext else s[-1][0]
+                    traj = LM.trajloss(s)
+                    Lt = traj + ((last - tgt) ** 2).sum()
+                    (gp,) = torch.autograd.grad(Lt, (pr,))
+                    sh[f"{key}/q0"] = q0.numpy()
+                    sh[f"{key}/p0"] = p0.numpy()
+                    if ext:
+                        sh[f"{key}/x0"] = x0.numpy()
+                    sh[f"{key}/tgt"] = tgt.numpy()
+                    sh[f"{key}/params"] = np.array([sig, lam, nt])
+                    sh[f"{key}/q1"] = s[-1][0].detach().numpy()
+                    sh[f"{key}/p1"] = s[-1][1].detach().numpy()
+                    sh[f"{key}/cost1"] = s[-1][2].detach().numpy()
+                    if ext:
+                        sh[f"{key}/x1"] = s[-1][3].detach().numpy()
+                    sh[f"{key}/trajloss"] = np.array(traj.item())
+                    sh[f"{key}/loss"] = np.array(Lt.item())
+                    sh[f"{key}/grad_p0"] = gp.numpy()
+                    sh[f"{key}/H0"] = np.array(LM.Hamiltonian(q0, p0).item())
+    np.savez_compressed(os.path.join(HERE, "shoot.npz"), **sh)
+
+    # ---------------- 3. EM step (GMM.py:236-325) + log-likelihoods (:714-721) ----------------
+    em = {}
+    opts = {"all": dict(mu=True, w=True, sigma=True, eta0=True),
+            "sigma": dict(mu=False, w=False, sigma=True, eta0=True),
+            "mu": dict(mu=True, w=False, sigma=False, eta0=False),
+            "mu_w": dict(mu=True, w=True, sigma=False, eta0=True)}
+    for D in (2, 3):
+        for outl in (False, True):
+            for oname, opt in opts.items():
+                key = f"D{D}_out{int(outl)}_{oname}"
+                g = torch.Generator().manual_seed(zlib.crc32(key.encode()))
+                N, C = 200, 12
+                X = torch.rand(N, D, generator=g, dtype=f64)
+                mu = torch.rand(C, D, generator=g, dtype=f64)
+                w = 0.3 * torch.randn(C, generator=g, dtype=f64)
+                GM = G.GaussianMixtureUnif(mu, sigma=0.15, use_outliers=outl, computversion="torch",
+                                           spec={"device": "cpu", "dtype": f64})
+                GM.w = w.clone()
+                GM.to_optimize = dict(opt)
+                em[f"{key}/X"] = X.numpy()
+                em[f"{key}/mu0"] = mu.numpy()
+                em[f"{key}/w0"] = w.numpy()
+                em[f"{key}/sigma0"] = np.array(0.15)
+                for it in range(2):
+                    Y, Cfe, FE = GM.EM_step(X)
+                    em[f"{key}/it{it}/Y"] = Y.numpy()
+                    em[f"{key}/it{it}/Cfe"] = np.array(float(Cfe))
+                    em[f"{key}/it{it}/FE"] = np.array(float(FE))
+                    em[f"{key}/it{it}/mu"] = GM.mu.numpy()
+                    em[f"{key}/it{it}/w"] = GM.w.numpy()
+                    em[f"{key}/it{it}/sigma"] = np.array(GM.sigma)
+                    if outl:
+                        em[f"{key}/it{it}/eta0"] = np.array(GM.outliers["eta0"])
+                        em[f"{key}/it{it}/vol0"] = np.array(GM.outliers["vol0"])
+                em[f"{key}/loglik"] = GM.log_likelihoods(X).numpy()
+                Ys, Cs, Fs = GM.EM_step(X, skip_M=True)
+                em[f"{key}/skipM/Y"] = Ys.numpy()
+                em[f"{key}/skipM/FE"] = np.array(float(Fs))
+    np.savez_compressed(os.path.join(HERE, "em.npz"), **em)
+
+    # ---------------- 4. PSR traces (PSR.py:242-569) ----------------
+    tr = {}
+    # (a) two-set style, 3D, hybrid dense, GMM on y fixed mu/w, sigma optimised
+    #     (ICP_two_set.py:179-187 GMM; LDDMM hybrid as ICP_atlas's default model)
+    g = torch.Generator().manual_seed(7)
+    N = 150
+    xB = torch.rand(N, 3, generator=g, dtype=f64)
+    xA = xB + 0.03 * torch.sin(2 * np.pi * xB[:, [1, 2, 0]]) + 0.005 * torch.randn(N, 3, generator=g, dtype=f64)
+    spec64 = {"device": "cpu", "dtype": f64}
+    GMMi = G.GaussianMixtureUnif(xB, sigma=0.05, computversion="torch", spec=spec64)
+    GMMi.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LMi = L.LDDMMModel(sigma=0.1, D=3, lambd=1e3, version="hybrid", scheme="Euler", nt=10,
+                       computversion="torch", spec=spec64)
+    PS = P.DiffPSR([[xA]], GMMi, LMi, dataspec=spec64, compspec=spec64)
+    PS.printstuff = False
+    tr["twoset/xA"] = xA.numpy()
+    tr["twoset/xB"] = xB.numpy()
+    tr["twoset/FE_init"] = np.array(float(PS.FE))
+    for it in range(3):
+        PS.GMM_opt(max_iterations=10, tol=1e-3)
+        tr[f"twoset/it{it}/FE_gmm"] = np.array(float(PS.FE))
+        tr[f"twoset/it{it}/sigma"] = np.array(PS.GMMi[0].sigma)
+        PS.Reg_opt(tol=1e-3, nmax=1)
+        tr[f"twoset/it{it}/FE_reg"] = np.array(float(PS.FE))
+        tr[f"twoset/it{it}/x1"] = PS.x1[0, 0].numpy()
+        tr[f"twoset/it{it}/a0"] = PS.a0[0].numpy()
+    # (b) atlas style, 2D, 3 frames, GMM fully optimised (ICP_atlas.py:170-298), classic,
+    #     grid support (2D only, PSR.py:472-482)
+    frames = []
+    for k in range(3):
+        gk = torch.Generator().manual_seed(100 + k)
+        base = torch.rand(60, 2, generator=gk, dtype=f64)
+        frames.append([base + 0.02 * torch.sin(2 * np.pi * base[:, [1, 0]]) * (1 + k)])
+    GMMa = G.GaussianMixtureUnif(torch.zeros(8, 2, dtype=f64), computversion="torch", spec=spec64)
+    LMa = L.LDDMMModel(sigma=0.2, D=2, lambd=500.0, version="classic", scheme="Euler", nt=10,
+                       computversion="torch", spec=spec64)
+    PA = P.DiffPSR(frames, GMMa, LMa, dataspec=spec64, compspec=spec64)
+    PA.printstuff = False
+    torch.manual_seed(3)
+    PA.reinitialize_GMM()
+    PA.set_support_scheme("grid", rho=np.sqrt(2))
+    for k in range(3):
+        tr[f"atlas/x0_{k}"] = frames[k][0].numpy()
+    tr["atlas/mu_init"] = PA.GMMi[0].mu.numpy()
+    tr["atlas/sigma_init"] = np.array(PA.GMMi[0].sigma)
+    tr["atlas/q0"] = PA.q0[0].numpy()
+    tr["atlas/FE_init"] = np.array(float(PA.FE))
+    for it in range(2):
+        PA.GMM_opt(max_iterations=10, tol=1e-3)
+        tr[f"atlas/it{it}/FE_gmm"] = np.array(float(PA.FE))
+        tr[f"atlas/it{it}/mu"] = PA.GMMi[0].mu.numpy()
+        tr[f"atlas/it{it}/sigma"] = np.array(PA.GMMi[0].sigma)
+        PA.Reg_opt(tol=1e-3, nmax=1)
+        tr[f"atlas/it{it}/FE_reg"] = np.array(float(PA.FE))
+        for k in range(3):
+            tr[f"atlas/it{it}/x1_{k}"] = PA.x1[k, 0].numpy()
+    np.savez_compressed(os.path.join(HERE, "psr_traces.npz"), **tr)
+    for fn in ("reductions", "shoot", "em", "psr_traces"):
+        print(fn, os.path.getsize(os.path.join(HERE, fn + ".npz")), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,164 @@
+"""GPU parity of the product (HIP path through the C-ABI) against the golden vectors produced
+by the reference itself (tests/golden/make_golden.py; fp64 reference runs).
+
+fp32 tolerances: kernel sums 1e-5 norm-wise; shooting / gradients 2e-5;
+multi-iteration PSR traces (L-BFGS with strong-Wolfe line search amplifies rounding,
+SURVEY.md 7(c)) 2e-3 relative on the free energy."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"))
+
+
+def G(z, k, dev):
+    return torch.from_numpy(np.asarray(z[k])).float().to(dev)
+
+
+def keys(z, suffix):
+    return sorted({k.split("/")[0] for k in z.files if k.endswith(suffix)})
+
+
+def spec(dev):
+    return {"device": dev, "dtype": torch.float32}
+
+
+def test_reductions_golden(dev):
+    from difficp_amd.tools.kernel import GaussKernel
+    z = load("reductions")
+    for key in keys(z, "/KRed"):
+        x, y, b, c, d, dm = (G(z, f"{key}/in_{n}", dev) for n in ("x", "y", "b", "c", "d", "dm"))
+        s = float(z[f"{key}/sigma"])
+        GK = GaussKernel(s, x.shape[1], spec=spec(dev))
+        out = {"KBase": GK.KBase(x, y), "KRedScal": GK.KRedScal(x, y, d), "KRed": GK.KRed(x, y, b),
+               "GradKRed": GK.GradKRed(x, y), "GradKRed_rev": GK.GradKRed_rev(x, y, dm),
+               "DDKRed": GK.DDKRed(x, y, b), "GenDKRed": GK.GenDKRed(x, y, b, c),
+               "HessKRed": GK.HessKRed(x, y, b, c), "LapKRed": GK.LapKRed(x, y),
+               "GradLapKRed": GK.GradLapKRed(x, y)}
+        for name, v in out.items():
+            ref = torch.from_numpy(z[f"{key}/{name}"])
+            assert rel_err(v.cpu(), ref) < 1e-5, (key, name, rel_err(v.cpu(), ref))
+
+
+def test_shoot_golden(dev):
+    from difficp_amd.core.LDDMM import LDDMMModel
+    z = load("shoot")
+    for key in keys(z, "/q1"):
+        version, scheme, xs, Ds = key.split("_")
+        ext, D = int(xs[1:]), int(Ds[1:])
+        sig, lam, nt = z[f"{key}/params"]
+        LM = LDDMMModel(sigma=float(sig), D=D, lambd=float(lam), version=version, scheme=scheme,
+                        nt=int(nt), spec=spec(dev))
+        q0, tgt = G(z, f"{key}/q0", dev), G(z, f"{key}/tgt", dev)
+        p0 = G(z, f"{key}/p0", dev).requires_grad_(True)
+        x0 = G(z, f"{key}/x0", dev) if ext else None
+        sh = LM.Shoot(q0, p0, x0)
+        last = sh[-1][-1] if ext else sh[-1][0]
+        traj = LM.trajloss(sh)
+        L = traj + ((last - tgt) ** 2).sum()
+        ref = lambda n: torch.from_numpy(z[f"{key}/{n}"])
+        assert rel_err(sh[-1][0].detach().cpu(), ref("q1")) < 1e-5, key
+        assert rel_err(sh[-1][1].detach().cpu(), ref("p1")) < 2e-5, key
+        assert rel_err(sh[-1][2].detach().cpu(), ref("cost1")) < 2e-5, key
+        if ext:
+            assert rel_err(sh[-1][3].detach().cpu(), ref("x1")) < 1e-5, key
+        assert abs(float(traj) - float(ref("trajloss"))) < 2e-5 * abs(float(ref("trajloss"))) + 1e-6, key
+        L.backward()
+        assert rel_err(p0.grad.cpu(), ref("grad_p0")) < 2e-5, (key, rel_err(p0.grad.cpu(), ref("grad_p0")))
+
+
+def test_em_golden(dev):
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    z = load("em")
+    opts = {"all": dict(mu=True, w=True, sigma=True, eta0=True),
+            "sigma": dict(mu=False, w=False, sigma=True, eta0=True),
+            "mu": dict(mu=True, w=False, sigma=False, eta0=False),
+            "mu_w": dict(mu=True, w=True, sigma=False, eta0=True)}
+    for key in keys(z, "/X"):
+        Ds, outs, oname = key.split("_", 2)
+        outl = outs == "out1"
+        X = G(z, f"{key}/X", dev)
+        GM = GaussianMixtureUnif(G(z, f"{key}/mu0", dev), sigma=float(z[f"{key}/sigma0"]),
+                                 use_outliers=outl, spec=spec(dev))
+        GM.w = G(z, f"{key}/w0", dev)
+        GM.to_optimize = dict(opts[oname])
+        for it in range(2):
+            Y, Cfe, FE = GM.EM_step(X)
+            r = lambda n: z[f"{key}/it{it}/{n}"]
+            assert rel_err(Y.cpu(), torch.from_numpy(r("Y"))) < 2e-5, (key, it)
+            assert abs(float(FE) - float(r("FE"))) < 2e-5 * abs(float(r("FE"))) + 2e-4, (key, it, float(FE), float(r("FE")))
+            assert abs(float(Cfe) - float(r("Cfe"))) < 2e-5 * abs(float(r("Cfe"))) + 2e-4, (key, it)
+            assert rel_err(GM.mu.cpu(), torch.from_numpy(r("mu"))) < 1e-5
+            assert rel_err(GM.w.cpu(), torch.from_numpy(r("w"))) < 1e-5
+            assert abs(GM.sigma - float(r("sigma"))) < 1e-5 * float(r("sigma"))
+            if outl:
+                assert abs(GM.outliers["eta0"] - float(r("eta0"))) < 1e-4
+        ll = GM.log_likelihoods(X)
+        assert rel_err(ll.cpu(), torch.from_numpy(z[f"{key}/loglik"])) < 1e-5, key
+        Ys, _, Fs = GM.EM_step(X, skip_M=True)
+        assert rel_err(Ys.cpu(), torch.from_numpy(z[f"{key}/skipM/Y"])) < 2e-5
+        assert abs(float(Fs) - float(z[f"{key}/skipM/FE"])) < 2e-5 * abs(float(Fs)) + 2e-4
+
+
+def test_psr_twoset_trace_golden(dev):
+    """3 diff-ICP iterations (GMM_opt + Reg_opt) of a 150-point 3D two-set problem."""
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    z = load("psr_traces")
+    xA, xB = G(z, "twoset/xA", dev), G(z, "twoset/xB", dev)
+    GM = GaussianMixtureUnif(xB, sigma=0.05, spec=spec(dev))
+    GM.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LM = LDDMMModel(sigma=0.1, D=3, lambd=1e3, version="hybrid", scheme="Euler", nt=10, spec=spec(dev))
+    PS = DiffPSR(xA, GM, LM, dataspec=spec(dev), compspec=spec(dev))
+    PS.printstuff = False
+    assert abs(PS.FE - float(z["twoset/FE_init"])) < 1e-4 * abs(float(z["twoset/FE_init"]))
+    for it in range(3):
+        PS.GMM_opt(max_iterations=10, tol=1e-3)
+        fe = float(z[f"twoset/it{it}/FE_gmm"])
+        assert abs(PS.FE - fe) < 2e-3 * abs(fe), (it, PS.FE, fe)
+        assert abs(PS.GMMi[0].sigma - float(z[f"twoset/it{it}/sigma"])) < 2e-3 * float(z[f"twoset/it{it}/sigma"])
+        PS.Reg_opt(tol=1e-3, nmax=1)
+        fe = float(z[f"twoset/it{it}/FE_reg"])
+        assert abs(PS.FE - fe) < 2e-3 * abs(fe), (it, PS.FE, fe)
+        x1 = torch.from_numpy(z[f"twoset/it{it}/x1"])
+        assert rel_err(PS.x1[0, 0].cpu(), x1) < 1e-3
+
+
+def test_psr_atlas_trace_golden(dev):
+    """2 iterations of a 3-frame 2D atlas (GMM mu/sigma/w optimised, classic LDDMM, grid support)."""
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    z = load("psr_traces")
+    frames = [[G(z, f"atlas/x0_{k}", dev)] for k in range(3)]
+    GM = GaussianMixtureUnif(torch.zeros(8, 2), spec=spec(dev))
+    LM = LDDMMModel(sigma=0.2, D=2, lambd=500.0, version="classic", scheme="Euler", nt=10, spec=spec(dev))
+    PA = DiffPSR(frames, GM, LM, dataspec=spec(dev), compspec=spec(dev))
+    PA.printstuff = False
+    # reinitialize_GMM draws randn: use the reference's drawn values
+    PA.GMMi[0].mu = G(z, "atlas/mu_init", dev)
+    PA.GMMi[0].sigma = float(z["atlas/sigma_init"])
+    PA.update_GMM_targets()
+    PA.set_support_scheme("grid", rho=np.sqrt(2))
+    assert rel_err(PA.q0[0].cpu(), torch.from_numpy(z["atlas/q0"])) < 1e-6
+    assert abs(PA.FE - float(z["atlas/FE_init"])) < 1e-4 * abs(float(z["atlas/FE_init"]))
+    for it in range(2):
+        PA.GMM_opt(max_iterations=10, tol=1e-3)
+        fe = float(z[f"atlas/it{it}/FE_gmm"])
+        assert abs(PA.FE - fe) < 2e-3 * abs(fe), (it, PA.FE, fe)
+        PA.Reg_opt(tol=1e-3, nmax=1)
+        fe = float(z[f"atlas/it{it}/FE_reg"])
+        assert abs(PA.FE - fe) < 2e-3 * abs(fe), (it, PA.FE, fe)
+        for k in range(3):
+            x1 = torch.from_numpy(z[f"atlas/it{it}/x1_{k}"])
+            assert rel_err(PA.x1[k, 0].cpu(), x1) < 2e-3, (it, k)

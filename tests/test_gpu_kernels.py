@@ -106,8 +106,8 @@ def test_ode_self_fwd(dev, version, M, D):
 
 
 @pytest.mark.parametrize("M,D", [(3, 2), (300, 2), (700, 3), (2100, 3)])
-@pytest.mark.parametrize("withlogdet", [False, True])
-def test_ode_self_bwd(dev, M, D, withlogdet):
+@pytest.mark.parametrize("withlogdet,gradcomp", [(False, False), (True, False), (True, True), (False, True)])
+def test_ode_self_bwd(dev, M, D, withlogdet, gradcomp):
     L = _lib()
     g = torch.Generator().manual_seed(7 * M + D)
     q = torch.rand(M, D, generator=g, dtype=torch.float64).requires_grad_(True)
@@ -115,28 +115,28 @@ def test_ode_self_bwd(dev, M, D, withlogdet):
     a = torch.randn(M, D, generator=g, dtype=torch.float64)
     bm = torch.randn(M, D, generator=g, dtype=torch.float64)
     gam = torch.randn(1, generator=g, dtype=torch.float64)
-    m = R.LDDMM(0.15, D, 50.0, False, withlogdet)
+    m = R.LDDMM(0.15, D, 50.0, gradcomp, withlogdet)
     v, mG, c = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
     Lf = (a * v).sum() + (bm * mG).sum() + (gam * c).sum()
     gq64, gp64 = torch.autograd.grad(Lf, (q, p))
     f = lambda t: t.detach().float().to(dev)
-    gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, 0.0)
+    gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, m.eta)
     assert rel_err(gq.cpu(), gq64) < 2e-5, rel_err(gq.cpu(), gq64)
     assert rel_err(gp.cpu(), gp64) < 2e-5, rel_err(gp.cpu(), gp64)
 
 
 @pytest.mark.parametrize("M,N,D", [(40, 300, 2), (500, 1300, 3), (2000, 100, 3)])
-@pytest.mark.parametrize("withlogdet", [False, True])
-def test_ode_ext(dev, M, N, D, withlogdet):
+@pytest.mark.parametrize("withlogdet,gradcomp", [(False, False), (True, False), (True, True)])
+def test_ode_ext(dev, M, N, D, withlogdet, gradcomp):
     L = _lib()
     g = torch.Generator().manual_seed(M + N + D)
     q = torch.rand(M, D, generator=g, dtype=torch.float64).requires_grad_(True)
     p = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
     x = torch.rand(N, D, generator=g, dtype=torch.float64).requires_grad_(True)
-    m = R.LDDMM(0.2, D, 50.0, False, withlogdet)
+    m = R.LDDMM(0.2, D, 50.0, gradcomp, withlogdet)
     vq, mG, c, vx = m.ODE(q, p, torch.zeros(1, dtype=torch.float64), x)
     f = lambda t: t.detach().float().to(dev)
-    vx_h, gx_h = L.ode_ext_fwd(f(x), f(q), f(p), 0.2, 0.0, withlogdet)
+    vx_h, gx_h = L.ode_ext_fwd(f(x), f(q), f(p), 0.2, m.eta, withlogdet)
     assert rel_err(vx_h.cpu(), vx) < 1e-5
     if withlogdet:
         assert rel_err(gx_h.sum().cpu(), c) < 1e-5
@@ -146,7 +146,7 @@ def test_ode_ext(dev, M, N, D, withlogdet):
     gq64, gp64, gx64 = torch.autograd.grad(Lf, (q, p, x))
     gq = torch.zeros(M, D, device=dev)
     gp = torch.zeros(M, D, device=dev)
-    gx = L.ode_ext_bwd(f(x), f(q), f(p), f(a), f(gam) if withlogdet else None, 0.2, 0.0, gq, gp)
+    gx = L.ode_ext_bwd(f(x), f(q), f(p), f(a), f(gam) if withlogdet else None, 0.2, m.eta, gq, gp)
     assert rel_err(gx.cpu(), gx64) < 2e-5
     assert rel_err(gq.cpu(), gq64) < 2e-5
     assert rel_err(gp.cpu(), gp64) < 2e-5

@@ -15,7 +15,7 @@ def _f(t, dev):
 
 
 @pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
-@pytest.mark.parametrize("version", ["classic", "hybrid"])
+@pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])
 @pytest.mark.parametrize("M,D,ext", [(60, 2, 0), (400, 3, 0), (50, 2, 300), (300, 3, 900)])
 def test_shoot_and_grad(dev, scheme, version, M, D, ext):
     from difficp_amd.core.LDDMM import LDDMMModel
@@ -24,8 +24,8 @@ def test_shoot_and_grad(dev, scheme, version, M, D, ext):
     p0 = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
     x0 = torch.rand(ext, D, generator=g, dtype=torch.float64) if ext else None
     lam, sig, nt = 20.0, 0.25, 7
-    wl = version == "hybrid"
-    ref = R.LDDMM(sig, D, lam, False, wl, scheme=scheme, nt=nt)
+    wl = version != "classic"
+    ref = R.LDDMM(sig, D, lam, version == "logdet", wl, scheme=scheme, nt=nt)
     shoot = ref.Shoot(q0, p0, x0)
     tgt = torch.randn(ext if ext else M, D, generator=g, dtype=torch.float64)
     last = shoot[-1][-1] if ext else shoot[-1][0]

@@ -18,7 +18,7 @@ def fake(monkeypatch):
 
 
 @pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
-@pytest.mark.parametrize("version", ["classic", "hybrid"])
+@pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])
 @pytest.mark.parametrize("ext", [0, 40])
 def test_shoot_adjoint_matches_autograd(fake, scheme, version, ext):
     from difficp_amd.core.LDDMM import LDDMMModel
@@ -27,7 +27,7 @@ def test_shoot_adjoint_matches_autograd(fake, scheme, version, ext):
     q0 = torch.rand(M, D, generator=g, dtype=torch.float64)
     p0 = (0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)).requires_grad_(True)
     x0 = torch.rand(ext, D, generator=g, dtype=torch.float64) if ext else None
-    ref = R.LDDMM(sig, D, lam, False, version == "hybrid", scheme=scheme, nt=nt)
+    ref = R.LDDMM(sig, D, lam, version == "logdet", version != "classic", scheme=scheme, nt=nt)
     sh = ref.Shoot(q0, p0, x0)
     W = [torch.randn(M, D, generator=g, dtype=torch.float64) for _ in range(2)]
     last = sh[-1][-1] if ext else sh[-1][0]
