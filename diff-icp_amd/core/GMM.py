@@ -53,12 +53,20 @@ def _gather_rows(t, comm):
     return torch.stack(out, 0)
 
 
+def _comm_device():
+    """Device the collectives run on: the current GPU for RCCL ("nccl"), else the CPU."""
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def _sum_ranks(x, comm):
     """Deterministic cross-rank sum (gather + rank-ordered sum, float64)."""
-    t = torch.as_tensor(x, dtype=torch.float64,
-                        device=x.device if isinstance(x, torch.Tensor) else None).reshape(1)
     if not _comm_active(comm):
-        return t[0]
+        return torch.as_tensor(x, dtype=torch.float64).reshape(1)[0]
+    dev = x.device if isinstance(x, torch.Tensor) else _comm_device()
+    t = torch.as_tensor(x, dtype=torch.float64).reshape(1).to(dev)
     return _gather_rows(t, comm).sum(0)[0]
 
 

@@ -1,0 +1,58 @@
+"""The C-ABI library loads and exports every symbol include/difficp_hip.h declares (CPU,
+no compute calls); the Python binding binds exactly those symbols."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "difficp_hip.h")
+LIB = os.path.join(ROOT, "diff-icp_amd", "libdifficp_hip.so")
+
+
+def declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dicp_\w+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} not built (run __graft_entry__.build())")
+    return ctypes.CDLL(LIB)
+
+
+def test_header_symbols_exported(lib):
+    names = declared()
+    assert len(names) >= 12
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_binding_matches_header():
+    from difficp_amd import _lib
+    assert set(_lib.EXPORTED_SYMBOLS) == set(declared())
+
+
+def test_host_only_entry_points(lib):
+    lib.dicp_version.restype = ctypes.c_char_p
+    assert b"gfx950" in lib.dicp_version()
+    assert lib.dicp_supports_dim(3) == 1 and lib.dicp_supports_dim(2) == 1
+    assert lib.dicp_supports_dim(7) == 0
+    lib.dicp_last_error.restype = ctypes.c_char_p
+    # invalid arguments are rejected before any device work, with a message
+    rc = lib.dicp_gauss_red_f32(2, None, ctypes.c_int64(5), None, ctypes.c_int64(5), 3, None, None,
+                                ctypes.c_double(1.0), None, None, ctypes.c_size_t(0), None)
+    assert rc == 1
+    assert b"invalid" in lib.dicp_last_error()
+
+
+def test_no_cpu_fallback():
+    """The product refuses host tensors instead of computing on the CPU."""
+    import torch
+    from difficp_amd import _lib
+    x = torch.rand(4, 3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.gauss_red(_lib.KRED, x, x, 0.5, b=x)
