@@ -202,10 +202,14 @@ def _main(out):
                     "traffic": traffic, "kernel": dom, "launches": d["launches"],
                     "avg_launch_ms": round(d["ms"] / d["launches"], 4),
                     "pairs_per_launch": d["pairs"] / d["launches"],
+                    "alg_bytes_per_launch": d["bytes"] / d["launches"],
                     "alg_hbm_GBps": round(d["bytes"] / d["launches"] / avg_s / 1e9, 3),
                     "share_of_step_time": round(d["ms"] * 1e-3 / elapsed, 3),
                     "note": "pair kernels are fp32 VALU/exp-bound (O(N) bytes, O(N^2) work): "
-                            "compute roofline, HBM bytes reported as alg_hbm_GBps/traffic"}
+                            "compute roofline, HBM bytes reported as alg_hbm_GBps/traffic; traffic "
+                            "(rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, profiles/pmc_traffic.json) is "
+                            "dominated by the per-column-split partial slabs (S x M x outputs x 4 B) "
+                            "that the deterministic merge reads back"}
         base = None
         if not args.no_cpu_baseline and world == 1 and pair_counts:
             try:

@@ -1,0 +1,35 @@
+"""Launch each hot kernel a few times at the bench's sizes (C2: 50k support points, 50k x 50k
+E-step) for rocprofv3 PMC passes, e.g.
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o fetch --output-format csv -- python tools/pmc_probe.py
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc -o write --output-format csv -- python tools/pmc_probe.py
+    python tools/pmc_traffic.py gpurun_out/pmc > profiles/pmc_traffic.json
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from difficp_amd import _lib  # noqa: E402
+
+
+def main():
+    M = int(os.environ.get("PMC_M", "50000"))
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    q = torch.rand(M, 3, device=dev)
+    p = 0.01 * torch.randn(M, 3, device=dev)
+    a = torch.randn(M, 3, device=dev)
+    gd = torch.ones(1, device=dev)
+    mu2 = (q * q).sum(-1)
+    w2 = torch.zeros(M, device=dev)
+    for _ in range(3):
+        _lib.ode_self_fwd(q, p, 0.1, 0.0, True)
+        _lib.ode_self_bwd(q, p, a, a, gd, 0.1, 0.0)
+        _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

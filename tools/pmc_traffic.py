@@ -1,0 +1,52 @@
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes per kernel.
+
+gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE = TCC_EA0_RDREQ x 64 B reads
+exactly 1/2 of the bytes of a wide (16 B/lane) coalesced streaming read; for other access
+widths it is uncalibrated.  Our pair kernels read their inputs with 4-B and 16-B loads, so
+we report both the raw value and the x2-corrected upper estimate, and use the raw
+FETCH_SIZE + WRITE_SIZE (KB x 1024) as `hbm_bytes_per_launch` (a lower bound).
+
+    python tools/pmc_traffic.py <dir with *_counter_collection.csv>
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+NAMES = {"OpOdeSelfBwd": "ode_self_bwd", "OpOdeSelfFwd": "ode_self_fwd", "OpGmmE": "gmm_estep",
+         "OpGmmM": "gmm_mstep", "OpGmmTargets": "gmm_targets", "merge_slabs": "merge_slabs",
+         "lse_finalize": "lse_finalize"}
+
+
+def short(kname):
+    for k, v in NAMES.items():
+        if k in kname:
+            return v
+    return None
+
+
+def main():
+    d = sys.argv[1]
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            s = short(r["Kernel_Name"])
+            if s is None:
+                continue
+            acc[s][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, c in acc.items():
+        fetch = sum(c.get("FETCH_SIZE", [0])) / max(1, len(c.get("FETCH_SIZE", [1])))
+        write = sum(c.get("WRITE_SIZE", [0])) / max(1, len(c.get("WRITE_SIZE", [1])))
+        out[k] = {"fetch_kb_per_launch": fetch, "write_kb_per_launch": write,
+                  "hbm_bytes_per_launch": (fetch + write) * 1024,
+                  "hbm_bytes_per_launch_fetch_x2": (2 * fetch + write) * 1024,
+                  "launches": len(c.get("FETCH_SIZE", c.get("WRITE_SIZE", [])))}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
