@@ -26,13 +26,18 @@ class Shoot(list):
     (LDDMM.py:286-299).  The states are views into stacked trajectory tensors Q, P, C[, X]
     that stay resident on the device."""
 
-    def __init__(self, Q, P, C, X=None):
+    def __init__(self, Q, P, C, X=None, H0=None):
         nt1 = Q.shape[0]
         if X is None:
             super().__init__((Q[t], P[t], C[t]) for t in range(nt1))
         else:
             super().__init__((Q[t], P[t], C[t], X[t]) for t in range(nt1))
         self.Q, self.P, self.C, self.X = Q, P, C, X
+        self.H0 = H0   # H(q0, p0) from the first ODE evaluation (differentiable), or None
+
+    def detach(self):
+        d = lambda t: None if t is None else t.detach()
+        return Shoot(d(self.Q), d(self.P), d(self.C), d(self.X), d(self.H0))
 
 
 class LDDMMModel:
@@ -170,6 +175,9 @@ class LDDMMModel:
         outs = ShootFn.apply(q0.contiguous(), p0.contiguous(),
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
                              float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet))
+        if x0 is None:
+            Q, P, C, H0 = outs
+            return Shoot(Q, P, C, None, H0)
         return Shoot(*outs)
 
     def BasicQuadLossFunctor(self, y, cmul=1):
@@ -187,7 +195,10 @@ class LDDMMModel:
         if not is_x and self.withlogdet and self.gradcomponent and self.try_trajcost_optim:
             return cost
         q0, p0 = shoot[0][:2]
-        return self.lam * self.Hamiltonian(q0, p0) + cost
+        H0 = getattr(shoot, "H0", None)
+        if H0 is None:
+            H0 = self.Hamiltonian(q0, p0)
+        return self.lam * H0 + cost
 
     def Optimize(self, dataloss, q0, p0, x0=None, nmax=10, tol=1e-3, errthresh=1e8):
         """min_p0 trajloss + dataloss(q1 or x1) with L-BFGS (LDDMM.py:338-398).
@@ -198,16 +209,24 @@ class LDDMMModel:
         if is_x:
             x0 = x0.detach()
 
+        last_eval = {}
+
         def lossfunc(p0):
             shoot = self.Shoot(q0, p0, x0)
             last = shoot[-1][-1] if is_x else shoot[-1][0]
+            last_eval["p0"], last_eval["shoot"] = p0.detach().clone(), shoot.detach()
             return self.trajloss(shoot) + dataloss(last)
 
         p0, _, nsteps, change = LBFGS_optimization([p0], lossfunc, nmax=nmax, tol=tol,
                                                    errthresh=errthresh)
         p0 = p0[0]
         with torch.no_grad():
-            shoot = self.Shoot(q0, p0, x0)
+            # final shoot (LDDMM.py:390): the kernels are deterministic, so when L-BFGS's
+            # last closure evaluation was at the returned p0 its trajectory is reused
+            if "p0" in last_eval and torch.equal(last_eval["p0"], p0):
+                shoot = last_eval["shoot"]
+            else:
+                shoot = self.Shoot(q0, p0, x0)
             trajl = self.trajloss(shoot).item()
             datal = dataloss(shoot[-1][-1] if is_x else shoot[-1][0]).item()
         return p0, shoot, trajl, datal, nsteps, change

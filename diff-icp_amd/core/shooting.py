@@ -19,19 +19,19 @@ import torch
 from .. import _lib
 
 
-def _f_self(q, p, sigma, eta, want_div):
-    """ODE right-hand side at the support points: (v, mG, div[1])."""
-    v, mG, g, _ = _lib.ode_self_fwd(q, p, sigma, eta, want_div)
+def _f_self(q, p, sigma, eta, want_div, want_h=False):
+    """ODE right-hand side at the support points: (v, mG, div[1]) [+ per-row h]."""
+    v, mG, g, h = _lib.ode_self_fwd(q, p, sigma, eta, want_div, want_h=want_h)
     div = g.sum().reshape(1) if want_div else None
-    return v, mG, div
+    return (v, mG, div, h) if want_h else (v, mG, div)
 
 
-def _f_ext(q, p, x, sigma, eta, want_div):
-    """ODE with external points: (vq, mGq, div over x [1], vx)."""
-    v, mG, _, _ = _lib.ode_self_fwd(q, p, sigma, eta, False)
+def _f_ext(q, p, x, sigma, eta, want_div, want_h=False):
+    """ODE with external points: (vq, mGq, div over x [1], vx) [+ per-row h]."""
+    v, mG, _, h = _lib.ode_self_fwd(q, p, sigma, eta, False, want_h=want_h)
     vx, gx = _lib.ode_ext_fwd(x, q, p, sigma, eta, want_div)
     div = gx.sum().reshape(1) if want_div else None
-    return v, mG, div, vx
+    return (v, mG, div, vx, h) if want_h else (v, mG, div, vx)
 
 
 def _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div):
@@ -46,10 +46,13 @@ def _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div):
 
 
 class ShootFn(torch.autograd.Function):
-    """(q0, p0[, x0]) -> stacked trajectory Q, P (nt+1, M, D), C (nt+1, 1)[, X (nt+1, N, D)].
+    """(q0, p0[, x0]) -> stacked trajectory Q, P (nt+1, M, D), C (nt+1, 1)[, X (nt+1, N, D)],
+    H0 = H(q0, p0).
 
     scheme: "Euler" (x += dt f(x)) or "Ralston" (k1 = f(x), k2 = f(x + 2dt/3 k1),
-    x += dt/4 (k1 + 3 k2)), as integrators.py:20-51.
+    x += dt/4 (k1 + 3 k2)), as integrators.py:20-51.  The Hamiltonian at the start point,
+    which trajloss needs (LDDMM.py:318-334), comes for free from the first ODE evaluation
+    (same fused pass, one extra per-row store): dH0/dp0 = v(q0, p0), dH0/dq0 = -mG(q0, p0).
     """
 
     @staticmethod
@@ -67,14 +70,20 @@ class ShootFn(torch.autograd.Function):
         if has_x:
             X[0].copy_(x0)
         mids = []  # Ralston intermediate states (needed by the adjoint)
+        H0 = v0 = mG0 = None
         for t in range(nt):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
+            first = t == 0
             if has_x:
-                v, mG, div, vx = _f_ext(q, p, x, sigma, eta, want_div)
+                out = _f_ext(q, p, x, sigma, eta, want_div, want_h=first)
+                v, mG, div, vx = out[:4]
             else:
-                v, mG, div = _f_self(q, p, sigma, eta, want_div)
+                out = _f_self(q, p, sigma, eta, want_div, want_h=first)
+                v, mG, div = out[:3]
                 vx = None
+            if first:
+                H0, v0, mG0 = out[-1].sum(), v, mG
             if scheme == "Euler":
                 torch.add(q, v, alpha=dt, out=Q[t + 1])
                 torch.add(p, mG, alpha=dt, out=P[t + 1])
@@ -105,21 +114,25 @@ class ShootFn(torch.autograd.Function):
                 mids.append((qi, pi, xi))
         ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x = \
             sigma, eta, nt, scheme, want_div, has_x
-        saved = [Q, P] + ([X] if has_x else [])
+        if H0 is None:  # nt == 0
+            v0, mG0, _, h = _lib.ode_self_fwd(q0, p0, sigma, eta, False, want_h=True)
+            H0 = h.sum()
+        saved = [Q, P, v0, mG0] + ([X] if has_x else [])
         for (qi, pi, xi) in mids:
             saved += [qi, pi] + ([xi] if has_x else [])
         ctx.save_for_backward(*saved)
-        outs = (Q, P, C, X) if has_x else (Q, P, C)
+        outs = (Q, P, C, X, H0) if has_x else (Q, P, C, H0)
         return outs
 
     @staticmethod
-    def backward(ctx, gQ, gP, gC, gX=None):
+    def backward(ctx, gQ, gP, gC, *rest):
+        gX, gH = rest if len(rest) == 2 else (None, rest[0])
         sigma, eta, nt, scheme, want_div, has_x = \
             ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x
         saved = ctx.saved_tensors
-        Q, P = saved[0], saved[1]
-        X = saved[2] if has_x else None
-        k = 3 if has_x else 2
+        Q, P, v0, mG0 = saved[:4]
+        X = saved[4] if has_x else None
+        k = 5 if has_x else 4
         mids = []
         if scheme != "Euler":
             step = 3 if has_x else 2
@@ -175,6 +188,9 @@ class ShootFn(torch.autograd.Function):
                 lc = lc + gC[t]
             if has_x and gX is not None:
                 lx = lx + gX[t]
+        if gH is not None:
+            lq = lq - gH * mG0
+            lp = lp + gH * v0
         return lq, lp, (lx if has_x else None), None, None, None, None, None
 
 

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace dicp {
 
 constexpr int kBlock = 256;       // threads per workgroup (4 waves)
@@ -62,6 +64,30 @@ struct Outs {
   int accumulate[4];
 };
 
+// Ops may define load_row_s / load_col_s, which also see the launch scalars (e.g. to stage
+// a scalar-premultiplied copy of a column field in LDS once per column instead of
+// multiplying once per pair).
+template <class T, class = void>
+struct has_row_s : std::false_type {};
+template <class T>
+struct has_row_s<T, std::void_t<decltype(&T::load_row_s)>> : std::true_type {};
+template <class T, class = void>
+struct has_col_s : std::false_type {};
+template <class T>
+struct has_col_s<T, std::void_t<decltype(&T::load_col_s)>> : std::true_type {};
+
+template <class Op>
+__device__ __forceinline__ void op_load_row(const Args& a, const Scal& sc, int64_t i,
+                                            typename Op::Row& r) {
+  if constexpr (has_row_s<Op>::value) Op::load_row_s(a, sc, i, r);
+  else Op::load_row(a, i, r);
+}
+template <class Op>
+__device__ __forceinline__ void op_load_col(const Args& a, const Scal& sc, int64_t j, float* rec) {
+  if constexpr (has_col_s<Op>::value) Op::load_col_s(a, sc, j, rec);
+  else Op::load_col(a, j, rec);
+}
+
 template <int W>
 struct Vec {
   float v[W];
@@ -98,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
   for (int r = 0; r < R; ++r) {
     int64_t i = ibase + (int64_t)r * kBlock;
     if (i >= M) i = M - 1;
-    Op::load_row(args, i, row[r]);
+    op_load_row<Op>(args, sc, i, row[r]);
   }
 
   float tot[R][NACC];
@@ -114,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
   float pre[CW4 * 4];
   int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
   if (cnt > 0 && tid < cnt) {
-    Op::load_col(args, j0 + tid, pre);
+    op_load_col<Op>(args, sc, j0 + tid, pre);
 #pragma unroll
     for (int k = 0; k < CW4; ++k)
       lds[0][tid * CW4 + k] = make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
@@ -124,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int64_t jn = jt + kTile;
     const int cntn = jn < j1 ? (int)((j1 - jn) < kTile ? (j1 - jn) : kTile) : 0;
-    if (tid < cntn) Op::load_col(args, jn + tid, pre);  // prefetch next tile (registers)
+    if (tid < cntn) op_load_col<Op>(args, sc, jn + tid, pre);  // prefetch next tile (registers)
 
     float acc[R][NACC];
 #pragma unroll

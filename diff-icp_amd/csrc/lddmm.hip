@@ -24,6 +24,8 @@ int env_r(const char* name, int def) {
 int g_r_fwd = -1, g_r_bwd = -1;
 int r_fwd() { if (g_r_fwd < 0) g_r_fwd = env_r("DICP_R_FWD", 2); return g_r_fwd; }
 int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 2); return g_r_bwd; }
+// eta = 0 VJP pair algebra: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48)
+int g_bwd_alg = 1;
 
 template <class Op>
 int launch_r(int R, const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
@@ -83,6 +85,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
   if (!strcmp(name, "split_rounds")) {
     if (value < 0 || value > 64) return DICP_ERR_INVALID;  // 0 = automatic
     split_rounds() = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "bwd_alg")) {
+    if (value != 0 && value != 1) return DICP_ERR_INVALID;
+    g_bwd_alg = value;
     return DICP_OK;
   }
   if (value != 1 && value != 2 && value != 4) return DICP_ERR_INVALID;
@@ -172,6 +179,8 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
   const Outs o = make_outs(gq, gp);
+  if (g_bwd_alg == 1)
+    return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
 }
 
@@ -326,7 +335,9 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
     {
       size_t a = D == 2 ? ws_r<OpOdeSelfBwd<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd<3>>(r_bwd(), M, M);
       size_t b = D == 2 ? ws_r<OpOdeSelfBwdEta<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwdEta<3>>(r_bwd(), M, M);
-      return a > b ? a : b;
+      size_t c = D == 2 ? ws_r<OpOdeSelfBwd2<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd2<3>>(r_bwd(), M, M);
+      a = a > b ? a : b;
+      return a > c ? a : c;
     }
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);
     case DICP_WS_ODE_EXT_BWD: return D == 2 ? ode_ext_bwd_ws<2>(N, M) : ode_ext_bwd_ws<3>(N, M);
@@ -337,6 +348,10 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
 int dicp_lddmm_splits(int kind, int64_t M, int64_t N) {
   switch (kind) {
     case DICP_WS_ODE_SELF_BWD:
+      if (g_bwd_alg == 1)
+        return r_bwd() == 1 ? rowred_splits<OpOdeSelfBwd2<3>, 1>(M, M)
+             : r_bwd() == 2 ? rowred_splits<OpOdeSelfBwd2<3>, 2>(M, M)
+                            : rowred_splits<OpOdeSelfBwd2<3>, 4>(M, M);
       return r_bwd() == 1 ? rowred_splits<OpOdeSelfBwd<3>, 1>(M, M)
            : r_bwd() == 2 ? rowred_splits<OpOdeSelfBwd<3>, 2>(M, M)
                           : rowred_splits<OpOdeSelfBwd<3>, 4>(M, M);

@@ -120,9 +120,14 @@ def test_ode_self_bwd(dev, M, D, withlogdet, gradcomp):
     Lf = (a * v).sum() + (bm * mG).sum() + (gam * c).sum()
     gq64, gp64 = torch.autograd.grad(Lf, (q, p))
     f = lambda t: t.detach().float().to(dev)
-    gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, m.eta)
-    assert rel_err(gq.cpu(), gq64) < 2e-5, rel_err(gq.cpu(), gq64)
-    assert rel_err(gp.cpu(), gp64) < 2e-5, rel_err(gp.cpu(), gp64)
+    for alg in (0, 1):  # both eta = 0 pair-algebra variants (lddmm_ops.hpp)
+        L.set_option("bwd_alg", alg)
+        try:
+            gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, m.eta)
+        finally:
+            L.set_option("bwd_alg", 1)
+        assert rel_err(gq.cpu(), gq64) < 2e-5, (alg, rel_err(gq.cpu(), gq64))
+        assert rel_err(gp.cpu(), gp64) < 2e-5, (alg, rel_err(gp.cpu(), gp64))
 
 
 @pytest.mark.parametrize("M,N,D", [(40, 300, 2), (500, 1300, 3), (2000, 100, 3)])

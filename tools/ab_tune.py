@@ -1,5 +1,6 @@
 """Interleaved A/B timing of tuning variants in ONE process (cdna_hip_programming.md 5.4
-rule 24): rows-per-thread of the fused ODE forward / backward.
+rule 24): rows-per-thread of the fused ODE forward / backward (--mode rsplit) and the
+backward's pair-algebra variants (--mode alg).
 
     python tools/ab_tune.py [--M 50000] [--rounds 5]
 """
@@ -30,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg"])
     a = ap.parse_args()
     M, D = a.M, 3
     dev = torch.device("cuda:0")
@@ -42,10 +44,16 @@ def main():
     variants = []
     fwd = lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True)
     bwd = lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0)
-    for sr in (1, 2, 4, 8):
-        for r in (1, 2):
-            variants.append((f"fwd_r{r}_s{sr}", {"r_fwd": r, "split_rounds": sr}, fwd))
-            variants.append((f"bwd_r{r}_s{sr}", {"r_bwd": r, "split_rounds": sr}, bwd))
+    if a.mode == "rsplit":
+        for sr in (1, 2, 4, 8):
+            for r in (1, 2):
+                variants.append((f"fwd_r{r}_s{sr}", {"r_fwd": r, "split_rounds": sr}, fwd))
+                variants.append((f"bwd_r{r}_s{sr}", {"r_bwd": r, "split_rounds": sr}, bwd))
+    else:  # pair-algebra variants of the backward, automatic splits
+        for alg in (0, 1):
+            for r in (1, 2, 4):
+                variants.append((f"bwd_alg{alg}_r{r}", {"bwd_alg": alg, "r_bwd": r, "split_rounds": 0}, bwd))
+        variants.append(("fwd_r2", {"r_fwd": 2, "split_rounds": 0}, fwd))
     res = {v[0]: [] for v in variants}
 
     def setopts(o):
