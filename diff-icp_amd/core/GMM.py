@@ -260,7 +260,7 @@ class GaussianMixtureUnif(torch.nn.Module):
             Cfe = Cfe_n_comp.sum()
             q = quad_n.sum()
             if dist_on:
-                Cfe = _sum_ranks(Cfe, comm).to(torch.float32)
+                Cfe = _sum_ranks(Cfe, comm).to(X.dtype)
                 q = _sum_ranks(q, comm)
             FE = Cfe + q.item() / sig2x2
         else:

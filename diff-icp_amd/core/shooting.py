@@ -61,10 +61,10 @@ class ShootFn(torch.autograd.Function):
         M, D = q0.shape
         dev = q0.device
         dt = 1.0 / nt
-        Q = torch.empty((nt + 1, M, D), device=dev, dtype=torch.float32)
+        Q = torch.empty((nt + 1, M, D), device=dev, dtype=q0.dtype)
         P = torch.empty_like(Q)
-        C = torch.zeros((nt + 1, 1), device=dev, dtype=torch.float32)
-        X = torch.empty((nt + 1,) + tuple(x0.shape), device=dev, dtype=torch.float32) if has_x else None
+        C = torch.zeros((nt + 1, 1), device=dev, dtype=q0.dtype)
+        X = torch.empty((nt + 1,) + tuple(x0.shape), device=dev, dtype=q0.dtype) if has_x else None
         Q[0].copy_(q0)
         P[0].copy_(p0)
         if has_x:
@@ -145,7 +145,7 @@ class ShootFn(torch.autograd.Function):
 
         def g_or_zero(G, t, shape):
             if G is None:
-                return torch.zeros(shape, device=dev, dtype=torch.float32)
+                return torch.zeros(shape, device=dev, dtype=Q.dtype)
             return G[t]
 
         lq = g_or_zero(gQ, nt, (M, D)).clone()
@@ -218,7 +218,7 @@ class OdeFn(torch.autograd.Function):
     def forward(ctx, q, p, sigma, eta, want_div):
         v, mG, div = _f_self(q, p, sigma, eta, want_div)
         if div is None:
-            div = torch.zeros(1, device=q.device, dtype=torch.float32)
+            div = torch.zeros(1, device=q.device, dtype=q.dtype)
         ctx.save_for_backward(q, p)
         ctx.sigma, ctx.eta, ctx.want_div = sigma, eta, want_div
         return v, mG, div
@@ -239,7 +239,7 @@ class OdeExtFn(torch.autograd.Function):
     def forward(ctx, q, p, x, sigma, eta, want_div):
         v, mG, div, vx = _f_ext(q, p, x, sigma, eta, want_div)
         if div is None:
-            div = torch.zeros(1, device=q.device, dtype=torch.float32)
+            div = torch.zeros(1, device=q.device, dtype=q.dtype)
         ctx.save_for_backward(q, p, x)
         ctx.sigma, ctx.eta, ctx.want_div = sigma, eta, want_div
         return v, mG, div, vx

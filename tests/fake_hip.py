@@ -18,7 +18,7 @@ def _d(t):
 
 
 def _out(t, like):
-    return t.to(dtype=torch.float32, device=like.device).contiguous()
+    return t.to(dtype=like.dtype, device=like.device).contiguous()
 
 
 def gauss_red(op, x, y, sigma, b=None, c=None):

@@ -8,7 +8,7 @@ module is placed in sys.modules AFTER importing kernel/LDDMM (which guard their 
 GMM.use_keops is forced False: every computversion then resolves to the reference's own
 torch implementation.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--only c1]
 """
 import importlib.machinery
 import os
@@ -224,5 +224,51 @@ def main():
         print(fn, os.path.getsize(os.path.join(HERE, fn + ".npz")), "bytes")
 
 
+def c1_trace():
+    """BASELINE configs[0] (diffICP/examples/diffICP_basic.py): one 2D spiral point set of
+    500 points (generate_spiral_point_sets, seed 1234 set by that module at import) registered
+    to the FIXED generating GMM (mu, w frozen, sigma optimised from 0.1), classic LDDMM
+    sigma 0.2 lambda 500 Euler, grid support rho = sqrt(2) (diffICP_basic.py:58-93);
+    iteration = GMM_opt() + Reg_opt(tol=1e-5) with the reference defaults
+    (diffICP_basic.py:116-119).  The inputs are generated in the reference's float32, the
+    trace is recorded in float64."""
+    import torch
+    K, L, G, P = import_reference()
+    from diffICP.examples.generate_spiral_point_sets import generate_spiral_point_sets
+    torch.manual_seed(1234)
+    x0, GMMg, _ = generate_spiral_point_sets(K=1, Nkbounds=(500, 501), sigma_GMM=0.025,
+                                             sigma_LDDMM=0.1, lambda_LDDMM=1e2)
+    f64 = torch.float64
+    spec64 = {"device": "cpu", "dtype": f64}
+    x = x0[0].to(f64)
+    tr = {"x0": x.numpy(), "mu": GMMg.mu.to(f64).numpy(), "w": GMMg.w.to(f64).numpy()}
+    GM = G.GaussianMixtureUnif(GMMg.mu.to(f64), computversion="torch", spec=spec64)
+    GM.w = GMMg.w.to(f64)
+    GM.sigma = 0.1
+    GM.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LM = L.LDDMMModel(sigma=0.2, D=2, lambd=5e2, version="classic", computversion="torch",
+                      scheme="Euler", spec=spec64)
+    PS = P.DiffPSR([[x]], GM, LM, dataspec=spec64, compspec=spec64)
+    PS.printstuff = False
+    PS.set_support_scheme("grid", rho=np.sqrt(2))
+    tr["q0"] = PS.q0[0].numpy()
+    tr["FE_init"] = np.array(float(PS.FE))
+    for it in range(3):
+        PS.GMM_opt()
+        tr[f"it{it}/FE_gmm"] = np.array(float(PS.FE))
+        tr[f"it{it}/sigma"] = np.array(PS.GMMi[0].sigma)
+        PS.Reg_opt(tol=1e-5)
+        tr[f"it{it}/FE_reg"] = np.array(float(PS.FE))
+        tr[f"it{it}/x1"] = PS.x1[0, 0].numpy()
+        tr[f"it{it}/a0"] = PS.a0[0].numpy()
+        print("C1 it", it, float(PS.FE), PS.GMMi[0].sigma)
+    np.savez_compressed(os.path.join(HERE, "c1_trace.npz"), **tr)
+    print("c1_trace", os.path.getsize(os.path.join(HERE, "c1_trace.npz")), "bytes")
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--only", "c1"]:
+        c1_trace()
+    else:
+        main()
+        c1_trace()

@@ -162,3 +162,23 @@ def test_psr_atlas_trace_golden(dev):
         for k in range(3):
             x1 = torch.from_numpy(z[f"atlas/it{it}/x1_{k}"])
             assert rel_err(PA.x1[k, 0].cpu(), x1) < 2e-3, (it, k)
+
+
+def test_c1_trace_golden(dev):
+    """BASELINE configs[0] (diffICP_basic.py, 2D spiral 500 points, fixed GMM, classic,
+    grid support) for 3 iterations on the HIP path; fp32 vs the reference's fp64 trace
+    (the reference's own fp32 run gives -146.042 / -411.006 / -498.336)."""
+    import c1_case
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            assert rel_err(PS.q0[0].cpu(), torch.from_numpy(z["q0"])) < 1e-6
+            assert abs(PS.FE - float(z["FE_init"])) < 1e-4 * abs(float(z["FE_init"]))
+            return
+        fe = float(z[f"it{it}/FE_{stage}"])
+        assert abs(PS.FE - fe) < 2e-3 * abs(fe), (stage, it, PS.FE, fe)
+        if stage == "gmm":
+            assert abs(PS.GMMi[0].sigma - float(z[f"it{it}/sigma"])) < 2e-3 * float(z[f"it{it}/sigma"])
+        else:
+            assert rel_err(PS.x1[0, 0].cpu(), torch.from_numpy(z[f"it{it}/x1"])) < 2e-3
+    c1_case.run_c1(spec(dev), iters=3, check=check)

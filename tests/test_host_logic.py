@@ -101,3 +101,23 @@ def test_check_coverage_and_rev(fake):
     a = (d * GK.GradKRed(x, y)).sum()
     b = GK.GradKRed_rev(x, y, d).sum()
     assert abs(float(a) - float(b)) < 1e-4 * abs(float(a)) + 1e-5
+
+
+def test_c1_trace_host_logic_fp64(fake):
+    """BASELINE configs[0] end to end on CPU (fp64, oracle-backed kernels): grid support,
+    classic model, fixed GMM with sigma optimisation, default GMM_opt / Reg_opt(tol=1e-5)."""
+    import c1_case
+    spec = {"device": "cpu", "dtype": torch.float64}
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            assert rel_err(PS.q0[0], torch.from_numpy(z["q0"])) < 1e-12
+            assert abs(PS.FE - float(z["FE_init"])) < 1e-9 * abs(float(z["FE_init"]))
+            return
+        fe = float(z[f"it{it}/FE_{stage}"])
+        assert abs(PS.FE - fe) < 1e-6 * abs(fe), (stage, it, PS.FE, fe)
+        if stage == "gmm":
+            assert abs(PS.GMMi[0].sigma - float(z[f"it{it}/sigma"])) < 1e-6 * float(z[f"it{it}/sigma"])
+        else:
+            assert rel_err(PS.x1[0, 0], torch.from_numpy(z[f"it{it}/x1"])) < 1e-6
+    c1_case.run_c1(spec, iters=2, check=check)
