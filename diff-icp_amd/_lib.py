@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(_HERE, "libdifficp_hip.so")
 
 # enum dicp_red_op (include/difficp_hip.h)
 KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRADKSCAL, \
-    GRADLAPKSCAL, MIN_SQDIST = range(13)
+    GRADLAPKSCAL, MIN_SQDIST, MIN_SQDIST_OTHER = range(14)
 # enum dicp_ws_kind
 WS_RED, WS_ODE_SELF_FWD, WS_ODE_SELF_BWD, WS_ODE_EXT_FWD, WS_ODE_EXT_BWD, WS_GMM_ESTEP, \
     WS_GMM_MSTEP, WS_GMM_TARGETS = range(8)
@@ -34,6 +34,7 @@ _SZ = ctypes.c_size_t
 
 _SIGNATURES = {
     "dicp_gauss_red_f32": [_INT, _P, _I64, _P, _I64, _INT, _P, _P, _DBL, _P, _P, _SZ, _P],
+    "dicp_radius_count_f32": [_P, _I64, _P, _I64, _INT, _DBL, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_fwd_f32": [_P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_bwd_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_ext_fwd_f32": [_P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _SZ, _P],
@@ -211,6 +212,26 @@ def gauss_red(op: int, x, y, sigma: float, b=None, c=None):
                  lambda: lib().dicp_gauss_red_f32(int(op), _ptr(x), M, _ptr(y), N, D, _ptr(b), _ptr(c),
                                   float(sigma), _ptr(out), _ptr(ws), nb, _stream(x.device)))
     _check_rc(rc, f"gauss_red(op={op})")
+    return out
+
+
+def radius_count(x, y, R: float):
+    """counts_i = #{j : |x_i - y_j|^2 <= R^2} (float32, exact integers), torch-exact distances
+    (dicp_radius_count_f32)."""
+    x = _dev(x, "x")
+    y = _dev(y, "y")
+    M, D = x.shape
+    N = y.shape[0]
+    if y.shape[1] != D:
+        raise ValueError("x and y must have the same dimension")
+    out = torch.empty((M,), device=x.device, dtype=torch.float32)
+    if M == 0:
+        return out
+    ws, nb = _workspace(WS_RED, M, N, D, x.device)
+    rc = _launch("radius_count", M * N, 4 * (M * D + N * D + M),
+                 lambda: lib().dicp_radius_count_f32(_ptr(x), M, _ptr(y), N, D, float(R), _ptr(out),
+                                                     _ptr(ws), nb, _stream(x.device)))
+    _check_rc(rc, "radius_count")
     return out
 
 

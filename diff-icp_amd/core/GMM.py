@@ -27,6 +27,7 @@ import torch
 from torch.nn.functional import log_softmax, softmax
 
 from .. import _lib
+from ..tools.point_sets import intrinsic_scale
 from ..tools.spec import defspec
 
 _LOG2E = 1.4426950408889634
@@ -167,9 +168,6 @@ class GaussianMixtureUnif(torch.nn.Module):
     # ------------------------------------------------------------------------------------
     def EM_step_hip(self, X, skip_M=False):
         """One E + M step (GMM.py:236-325).  Returns (Y (N,D), Cfe, FE) like EM_step_torch."""
-        if self.ensure_continuum:
-            raise NotImplementedError("ensure_continuum (intrinsic_scale, KeOps Kmin) is not "
-                                      "provided by the HIP backend")
         X = X.detach().contiguous()
         N, D = X.shape
         comm = self.comm
@@ -243,8 +241,8 @@ class GaussianMixtureUnif(torch.nn.Module):
                 nds = _sum_ranks(nds, comm)
                 Ntot = int(_sum_ranks(float(N), comm).item())
             self.sigma = torch.sqrt(nds / (self.D * Ntot)).item()
-            if self.ensure_continuum:
-                raise NotImplementedError
+            if self.ensure_continuum:      # (experimental) GMM.py:298-299 / :457-458
+                self.sigma = max(self.sigma, intrinsic_scale(self.mu))
 
         # ---- targets and free energy (GMM.py:303-323) ----
         Y = Y.contiguous()

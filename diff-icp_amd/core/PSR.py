@@ -25,6 +25,7 @@ from .GMM import GaussianMixtureUnif, _comm_active, _gather_rows, _sum_ranks
 from .LDDMM import LDDMMModel
 from .registrations import LDDMMRegistration
 from ..tools.in_out import read_point_sets
+from ..tools.point_sets import decimate
 from ..tools.spec import defspec
 
 
@@ -219,8 +220,9 @@ class DiffPSR(MultiPSR):
             self.a0[k] = self.LMi.v2p(self.q0[k], v0, **v2p_args)
 
     def set_support_scheme(self, scheme="decim", rho=1.0, xticks=None, yticks=None, q0=None):
-        """Support points: "grid" (2D, PSR.py:472-482) or "custom" (:484-487).
-        "decim" (greedy O(N^2) host decimation, point_sets.py:102-133) is a next-row item."""
+        """Support points (PSR.py:430-493): "decim" (greedy covering decimation of each
+        structure, point_sets.py:102-133, device kernels), "grid" (2D, :472-482) or
+        "custom" (:484-487)."""
         self.rho = rho
         Rcover = rho * self.LMi.Kernel.sigma
         self.support_scheme = scheme
@@ -247,7 +249,18 @@ class DiffPSR(MultiPSR):
             assert q0 is not None, "For a custom support scheme, please specify argument q0"
             self.q0 = [q0.clone().detach().to(**self.compspec).contiguous()] * self.K
         elif scheme == "decim":
-            raise NotImplementedError("support scheme 'decim' is not provided yet (use 'grid' or 'custom')")
+            # greedy covering decimation of every structure (PSR.py:458-470), on the device
+            self.supp_ids = np.array([[None] * self.S] * self.K, dtype=object)
+            self.q0 = [None] * self.K
+            for k in range(self.K):
+                for s in range(self.S):
+                    self.supp_ids[k, s], _ = decimate(self.x0[k, s].to(**self.compspec), Rcover)
+                Ndecim = sum(len(self.supp_ids[k, s]) for s in range(self.S))
+                if self.printstuff:
+                    Pdecim = Ndecim / sum(int(self.N[k, s]) for s in range(self.S))
+                    print(f"Decimation, frame {k} : {Ndecim} support points ({Pdecim:.0%} of original sets)")
+                self.q0[k] = torch.cat(tuple(self.x0[k, s][self.supp_ids[k, s]] for s in range(self.S)),
+                                       dim=0).to(**self.compspec).contiguous()
         else:
             raise ValueError(f"Unknown value of support point scheme : {scheme}.")
         self.update_a0(q0_prev, rcond=1e-1)

@@ -131,8 +131,28 @@ extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float
     case DICP_GRADKSCAL: return red_dispatch<OpGradKScal>("GradKScal", D, a, sc, M, N, out, ws, ws_bytes, st);
     case DICP_GRADLAPKSCAL: return red_dispatch<OpGradLapKScal>("GradLapKScal", D, a, sc, M, N, out, ws, ws_bytes, st);
     case DICP_MIN_SQDIST: return red_dispatch<OpMinSqDist>("MinSqDist", D, a, sc, M, N, out, ws, ws_bytes, st);
+    case DICP_MIN_SQDIST_OTHER:
+      if (N != M || x != y || M > INT32_MAX) {
+        set_error("dicp_gauss_red_f32: MIN_SQDIST_OTHER needs y == x (same buffer, M == N < 2^31)");
+        return DICP_ERR_INVALID;
+      }
+      return red_dispatch<OpMinSqDistOther>("MinSqDistOther", D, a, sc, M, N, out, ws, ws_bytes, st);
     default: set_error("dicp_gauss_red_f32: unknown op %d", op); return DICP_ERR_UNSUPPORTED;
   }
+}
+
+extern "C" int dicp_radius_count_f32(const float* x, int64_t M, const float* y, int64_t N, int D,
+                                     double R, float* counts, void* ws, size_t ws_bytes,
+                                     dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || N < 0 || (M > 0 && (!x || !counts)) || (N > 0 && !y) || !(R >= 0)) {
+    set_error("dicp_radius_count_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  const Args a = {x, nullptr, nullptr, nullptr, y, nullptr, nullptr, nullptr};
+  Scal sc = make_scal(1.0, 0.0);
+  sc.aux0 = (float)(R * R);  // torch compares the float32 distances with (float)(R**2)
+  return red_dispatch<OpRadiusCount>("RadiusCount", D, a, sc, M, N, counts, ws, ws_bytes, st);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -326,7 +346,8 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
                     red_ws<OpGradLapKPlain>(D, M, N), red_ws<OpGradKScal>(D, M, N),
                     red_ws<OpMinSqDist>(D, M, N), red_ws<OpZDotB>(D, M, N),
                     red_ws<OpDDK>(D, M, N), red_ws<OpKRedScal>(D, M, N),
-                    red_ws<OpGradLapKScal>(D, M, N)};
+                    red_ws<OpGradLapKScal>(D, M, N), red_ws<OpMinSqDistOther>(D, M, N),
+                    red_ws<OpRadiusCount>(D, M, N)};
       for (size_t v : c) m = v > m ? v : m;
       return m;
     }

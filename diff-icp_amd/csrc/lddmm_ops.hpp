@@ -304,7 +304,25 @@ struct OpGradLapK {
   }
 };
 
-// min_j |x_i - y_j|^2  (GaussKernel.check_coverage, kernel.py:324-329)
+// Squared distance with the exact arithmetic of the reference's torch expression
+// ((x_i - x_j)**2).sum(-1) on the CPU: products rounded, summed left to right, no FMA
+// contraction (so comparisons against a radius give bit-identical decisions).  The empty
+// asm makes each rounded product opaque: -ffp-contract=fast would otherwise fuse it into
+// the following add in the backend (a source-level contract pragma does not prevent that).
+template <int D>
+__device__ __forceinline__ float exact_sq(const float* __restrict__ x, const float* __restrict__ y) {
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float z = x[d] - y[d];
+    float zz = z * z;
+    asm("" : "+v"(zz));
+    s = (d == 0) ? zz : s + zz;
+  }
+  return s;
+}
+
+// out_i = min_j |x_i - y_j|^2   (check_coverage, kernel.py:324-329)
 template <int D>
 struct OpMinSqDist {
   static constexpr int CW4 = cw4(D), NACC = 1, kNOut = 1;
@@ -314,8 +332,47 @@ struct OpMinSqDist {
   __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
   __device__ static void load_col(const Args& a, int64_t j, float* rec) { ld<D>(a.c0, j, rec); }
   __device__ static void pair(const Scal&, const Row& r, const float* rec, float* acc) {
-    float z[D];
-    acc[0] = fminf(acc[0], diff_sq<D>(r.x, rec, z));
+    acc[0] = fminf(acc[0], exact_sq<D>(r.x, rec));
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) { v[0] = t[0]; }
+};
+
+// out_i = min_{j != i} |x_i - x_j|^2 over the same point set (rows = columns): the second
+// smallest entry of row i of the distance matrix, D_ij.Kmin(2)[:, 1] of intrinsic_scale
+// (point_sets.py:13-26).  Indices travel as raw int bits in a float slot.
+template <int D>
+struct OpMinSqDistOther {
+  static constexpr int CW4 = cw4(D + 1), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = true;
+  struct Row { float x[D]; int i; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+    ld<D>(a.r0, i, r.x);
+    r.i = (int)i;
+  }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+    ld<D>(a.c0, j, rec);
+    rec[D] = __int_as_float((int)j);
+  }
+  __device__ static void pair(const Scal&, const Row& r, const float* rec, float* acc) {
+    const float d2 = exact_sq<D>(r.x, rec);
+    acc[0] = (__float_as_int(rec[D]) != r.i) ? fminf(acc[0], d2) : acc[0];
+  }
+  __device__ static void store(const Scal&, const Row&, const float* t, float* v) { v[0] = t[0]; }
+};
+
+// out_i = #{j : |x_i - y_j|^2 <= R2}  (float-valued, exact below 2^24)   decimate,
+// point_sets.py:114-116 (D <= R**2 with the torch arithmetic of exact_sq); R2 in sc.aux0.
+template <int D>
+struct OpRadiusCount {
+  static constexpr int CW4 = cw4(D), NACC = 1, kNOut = 1;
+  static constexpr int kOutW[4] = {1, 0, 0, 0};
+  static constexpr bool kMin = false;
+  struct Row { float x[D]; };
+  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static void load_col(const Args& a, int64_t j, float* rec) { ld<D>(a.c0, j, rec); }
+  __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
+    acc[0] += (exact_sq<D>(r.x, rec) <= sc.aux0) ? 1.f : 0.f;
   }
   __device__ static void store(const Scal&, const Row&, const float* t, float* v) { v[0] = t[0]; }
 };

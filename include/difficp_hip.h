@@ -62,8 +62,13 @@ enum dicp_red_op {
   DICP_GRADLAPK = 9,   /* out_i   = sum_j -z (s^3|z|^2-(D+2)s^2) K   (M,D) kernel.py:168,289 */
   DICP_GRADKSCAL = 10, /* out_i   = sum_j -s z K d_j    b=d (N,)     (M,D) (autograd of KBase/KRedScal) */
   DICP_GRADLAPKSCAL = 11, /* out_i = sum_j -z (s^3|z|^2-(D+2)s^2) K d_j (M,D) (autograd of LapKRed) */
-  DICP_MIN_SQDIST = 12 /* out_i   = min_j |z|^2                      (M,)  check_coverage kernel.py:324-329 */
+  DICP_MIN_SQDIST = 12, /* out_i  = min_j |z|^2                      (M,)  check_coverage kernel.py:324-329 */
+  DICP_MIN_SQDIST_OTHER = 13 /* out_i = min_{j != i} |z|^2, x == y, M == N (M,)  intrinsic_scale
+                          point_sets.py:13-26 (Kmin(2)[:,1]); sigma unused */
 };
+/* MIN_SQDIST, MIN_SQDIST_OTHER and dicp_radius_count_f32 compute |z|^2 with the torch CPU
+ * arithmetic of ((x_i - y_j)**2).sum(-1) (no FMA contraction), so threshold decisions are
+ * bit-identical to the reference's. */
 
 /* One reduction.  x (M,D) rows, y (N,D) columns, b column weights ((N,D) or (N,) or NULL),
  * c row weights ((M,D) or NULL), out (M,D) or (M,) as listed above.
@@ -71,6 +76,12 @@ enum dicp_red_op {
 int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float* y, int64_t N, int D,
                        const float* b, const float* c, double sigma, float* out, void* ws,
                        size_t ws_bytes, dicp_stream_t stream);
+
+/* counts_i = #{j < N : |x_i - y_j|^2 <= (float)(R*R)}, x (M,D), y (N,D), counts (M,) float
+ * (exact integers below 2^24).  The O(N^2) part of the greedy support decimation
+ * decimate(x, R) (point_sets.py:102-133); workspace kind DICP_WS_RED. */
+int dicp_radius_count_f32(const float* x, int64_t M, const float* y, int64_t N, int D, double R,
+                          float* counts, void* ws, size_t ws_bytes, dicp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
  * LDDMM geodesic-shooting ODE (LDDMMModel.ODE, LDDMM.py:176-227), fused: one pass over

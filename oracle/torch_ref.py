@@ -107,6 +107,35 @@ def MinSqDist(x, y):                                  # kernel.py:324-329 (inten
     return _rows(lambda xc: ((xc[:, None, :] - y[None, :, :]) ** 2).sum(-1).min(dim=1).values, x)
 
 
+def SqDistF32(x, y):                                  # point_sets.py:114-116 (float32 arithmetic)
+    x, y = x.float(), y.float()
+    return ((x[:, None, :] - y[None, :, :]) ** 2).sum(-1)
+
+
+def MinSqDistOther(x):                                # point_sets.py:22-23, Kmin(2)[:, 1]
+    d = SqDistF32(x, x)
+    return d.sort(dim=1).values[:, 1] if x.shape[0] > 1 else torch.full((x.shape[0],), float("inf"))
+
+
+def intrinsic_scale(x):                               # point_sets.py:13-26
+    return MinSqDistOther(x).mean().sqrt().item()
+
+
+def decimate(x, R):                                   # point_sets.py:102-133, restated as written
+    """Greedy covering decimation: O(N^2) per kept point, small N only."""
+    import numpy as np
+    M = (SqDistF32(x, x) <= R ** 2).numpy()
+    N = x.shape[0]
+    notcovered = np.arange(N)
+    kept = []
+    while len(notcovered) > 0:
+        i = notcovered[M[np.ix_(notcovered, notcovered)].sum(axis=0).argmax()]
+        kept.append(int(i))
+        notcovered = notcovered[~M[i, notcovered]]
+    kept_set = set(kept)
+    return kept, [i for i in range(N) if i not in kept_set]
+
+
 # ---------------------------------------------------------------------------------------
 # LDDMM (diffICP/core/LDDMM.py:100-227, 286-334)
 # ---------------------------------------------------------------------------------------

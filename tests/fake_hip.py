@@ -54,6 +54,8 @@ def gauss_red(op, x, y, sigma, b=None, c=None):
             return torch.sum(torch.exp(-D2 / (2 * sigma ** 2)) * (Y[None, :, :] - xc[:, None, :])
                              * (D2 / sigma ** 6 - (D + 2) / sigma ** 4) * B[None, :, None], 1)
         r = R._rows(f, X)
+    elif op == L.MIN_SQDIST_OTHER:
+        return _out(R.MinSqDistOther(x.detach()), x)
     elif op == L.MIN_SQDIST:
         r = R.MinSqDist(X, Y) if Y.shape[0] else torch.full((X.shape[0],), float("inf"), dtype=torch.float64)
     else:
@@ -162,7 +164,12 @@ def gmm_targets(X, T2, mu_old, w2_old, sigma_old, mu_new, lpi_new):
     return _out(rows, X)
 
 
-_ENTRIES = ("gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+def radius_count(x, y, radius):
+    d = R.SqDistF32(x.detach(), y.detach())
+    return _out((d <= radius ** 2).sum(1).to(torch.float64), x)
+
+
+_ENTRIES = ("radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 

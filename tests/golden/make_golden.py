@@ -8,7 +8,7 @@ module is placed in sys.modules AFTER importing kernel/LDDMM (which guard their 
 GMM.use_keops is forced False: every computversion then resolves to the reference's own
 torch implementation.
 
-    python tests/golden/make_golden.py [--only c1]
+    python tests/golden/make_golden.py [--only c1|decim]
 """
 import importlib.machinery
 import os
@@ -266,9 +266,58 @@ def c1_trace():
     print("c1_trace", os.path.getsize(os.path.join(HERE, "c1_trace.npz")), "bytes")
 
 
+def decim_cases():
+    """decimate (point_sets.py:102-133) on random 2D/3D sets and on a regular grid (many ties
+    and near-threshold distances), plus a 2-iteration 3D PSR trace with the "decim" support
+    scheme (PSR.py:458-470; custom support -> external-point shooting)."""
+    import torch
+    K, L, G, P = import_reference()
+    import diffICP.tools.point_sets as PS_
+    out = {}
+    g = torch.Generator().manual_seed(11)
+    cases = {"rand2d": (torch.rand(400, 2, generator=g), 0.1),
+             "rand3d": (torch.rand(600, 3, generator=g), 0.15),
+             "grid2d": (torch.stack(torch.meshgrid(torch.arange(20) * 0.05, torch.arange(20) * 0.05,
+                                                   indexing="ij"), -1).reshape(-1, 2).float(), 0.05),
+             "dup3d": (torch.rand(50, 3, generator=g).repeat(3, 1), 0.2)}
+    for name, (x, R) in cases.items():
+        kept, rej = PS_.decimate(x, R)
+        out[f"{name}/x"] = x.numpy()
+        out[f"{name}/R"] = np.array(R)
+        out[f"{name}/kept"] = np.array(kept, dtype=np.int64)
+        print("decim", name, len(kept))
+    f64 = torch.float64
+    spec64 = {"device": "cpu", "dtype": f64}
+    gx = torch.Generator().manual_seed(12)
+    xB = torch.rand(200, 3, generator=gx, dtype=f64)
+    xA = xB + 0.03 * torch.sin(2 * np.pi * xB[:, [2, 0, 1]]) + 0.005 * torch.randn(200, 3, generator=gx, dtype=f64)
+    GM = G.GaussianMixtureUnif(xB, sigma=0.05, computversion="torch", spec=spec64)
+    GM.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LM = L.LDDMMModel(sigma=0.15, D=3, lambd=1e3, version="hybrid", scheme="Euler", nt=10,
+                      computversion="torch", spec=spec64)
+    PSR = P.DiffPSR([[xA]], GM, LM, dataspec=spec64, compspec=spec64)
+    PSR.printstuff = False
+    PSR.set_support_scheme("decim", rho=1.0)
+    out["psr/xA"] = xA.numpy()
+    out["psr/xB"] = xB.numpy()
+    out["psr/q0"] = PSR.q0[0].numpy()
+    out["psr/FE_init"] = np.array(float(PSR.FE))
+    for it in range(2):
+        PSR.GMM_opt(max_iterations=10, tol=1e-3)
+        out[f"psr/it{it}/FE_gmm"] = np.array(float(PSR.FE))
+        PSR.Reg_opt(tol=1e-3, nmax=1)
+        out[f"psr/it{it}/FE_reg"] = np.array(float(PSR.FE))
+        out[f"psr/it{it}/x1"] = PSR.x1[0, 0].numpy()
+        print("decim psr it", it, float(PSR.FE), PSR.q0[0].shape)
+    np.savez_compressed(os.path.join(HERE, "decim.npz"), **out)
+    print("decim", os.path.getsize(os.path.join(HERE, "decim.npz")), "bytes")
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["--only", "c1"]:
-        c1_trace()
-    else:
+    only = sys.argv[2] if sys.argv[1:2] == ["--only"] else None
+    if only is None:
         main()
+    if only in (None, "c1"):
         c1_trace()
+    if only in (None, "decim"):
+        decim_cases()

@@ -182,3 +182,63 @@ def test_c1_trace_golden(dev):
         else:
             assert rel_err(PS.x1[0, 0].cpu(), torch.from_numpy(z[f"it{it}/x1"])) < 2e-3
     c1_case.run_c1(spec(dev), iters=3, check=check)
+
+
+def test_decimate_golden(dev):
+    """Device decimation returns exactly the reference's kept indices (bit-exact distances
+    and tie-breaking), incl. a regular grid with R equal to the spacing."""
+    from difficp_amd.tools.point_sets import decimate
+    z = load("decim")
+    for name in ("rand2d", "rand3d", "grid2d", "dup3d"):
+        x = torch.from_numpy(z[f"{name}/x"]).to(dev)
+        kept, rej = decimate(x, float(z[f"{name}/R"]))
+        assert kept == z[f"{name}/kept"].tolist(), name
+        assert len(kept) + len(rej) == x.shape[0]
+
+
+def test_decimate_and_scale_vs_oracle(dev):
+    """Larger sets against the oracle's restatement of the reference loop; intrinsic_scale
+    (KeOps Kmin in the reference: parity vs the oracle only) and check_coverage distances
+    bit-exact to torch's float32 arithmetic."""
+    from oracle import torch_ref as R
+    from difficp_amd import _lib
+    from difficp_amd.tools.point_sets import decimate, intrinsic_scale
+    g = torch.Generator().manual_seed(31)
+    for N, D, Rad in ((2000, 2, 0.04), (1500, 3, 0.12)):
+        x = torch.rand(N, D, generator=g)
+        kept, _ = decimate(x.to(dev), Rad)
+        assert kept == R.decimate(x, Rad)[0]
+        assert abs(intrinsic_scale(x.to(dev)) - R.intrinsic_scale(x)) <= 1e-6 * R.intrinsic_scale(x)
+        y = torch.rand(700, D, generator=g)
+        d2 = _lib.gauss_red(_lib.MIN_SQDIST, x.to(dev), y.to(dev), 1.0).cpu()
+        assert torch.equal(d2, R.SqDistF32(x, y).min(dim=1).values)
+        cnt = _lib.radius_count(x.to(dev), y.to(dev), Rad).cpu()
+        assert torch.equal(cnt, (R.SqDistF32(x, y) <= Rad ** 2).sum(1).float())
+
+
+def test_decim_psr_trace_golden(dev):
+    """2 iterations with the "decim" support scheme (3D hybrid, external-point shooting)."""
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    z = load("decim")
+    xA, xB = G(z, "psr/xA", dev), G(z, "psr/xB", dev)
+    GM = GaussianMixtureUnif(xB, sigma=0.05, spec=spec(dev))
+    GM.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LM = LDDMMModel(sigma=0.15, D=3, lambd=1e3, version="hybrid", scheme="Euler", nt=10, spec=spec(dev))
+    PS = DiffPSR(xA, GM, LM, dataspec=spec(dev), compspec=spec(dev))
+    PS.printstuff = False
+    PS.set_support_scheme("decim", rho=1.0)
+    # the fp64 reference decimated the fp64 points; fp32 rounding may flip a borderline
+    # neighbour, so the support set is checked for size and near-equality
+    q0 = torch.from_numpy(z["psr/q0"])
+    assert PS.q0[0].shape == q0.shape
+    assert rel_err(PS.q0[0].cpu(), q0) < 1e-6
+    for it in range(2):
+        PS.GMM_opt(max_iterations=10, tol=1e-3)
+        fe = float(z[f"psr/it{it}/FE_gmm"])
+        assert abs(PS.FE - fe) < 2e-3 * abs(fe), (it, PS.FE, fe)
+        PS.Reg_opt(tol=1e-3, nmax=1)
+        fe = float(z[f"psr/it{it}/FE_reg"])
+        assert abs(PS.FE - fe) < 2e-3 * abs(fe), (it, PS.FE, fe)
+        assert rel_err(PS.x1[0, 0].cpu(), torch.from_numpy(z[f"psr/it{it}/x1"])) < 2e-3

@@ -121,3 +121,47 @@ def test_c1_trace_host_logic_fp64(fake):
         else:
             assert rel_err(PS.x1[0, 0], torch.from_numpy(z[f"it{it}/x1"])) < 1e-6
     c1_case.run_c1(spec, iters=2, check=check)
+
+
+def test_decimate_host_logic(fake):
+    """Device decimation algorithm (incremental neighbour counts) == the reference's greedy
+    loop, on the reference's own outputs (tests/golden/decim.npz), incl. ties on a grid."""
+    import numpy as np
+    import os
+    from difficp_amd.tools.point_sets import decimate, intrinsic_scale
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "decim.npz"))
+    for name in ("rand2d", "rand3d", "grid2d", "dup3d"):
+        x = torch.from_numpy(z[f"{name}/x"])
+        kept, rej = decimate(x, float(z[f"{name}/R"]))
+        assert kept == z[f"{name}/kept"].tolist(), name
+        assert len(kept) + len(rej) == x.shape[0]
+        assert abs(intrinsic_scale(x) - R.intrinsic_scale(x)) <= 1e-7 * max(1.0, R.intrinsic_scale(x))
+
+
+def test_decim_psr_trace_host_logic_fp64(fake):
+    """"decim" support scheme (PSR.py:458-470) + external-point shooting, 2 iterations,
+    fp64 with oracle-backed kernels vs the reference's fp64 trace."""
+    import numpy as np
+    import os
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "decim.npz"))
+    spec = {"device": "cpu", "dtype": torch.float64}
+    xA, xB = torch.from_numpy(z["psr/xA"]), torch.from_numpy(z["psr/xB"])
+    GM = GaussianMixtureUnif(xB, sigma=0.05, spec=spec)
+    GM.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LM = LDDMMModel(sigma=0.15, D=3, lambd=1e3, version="hybrid", scheme="Euler", nt=10, spec=spec)
+    PS = DiffPSR([[xA]], GM, LM, dataspec=spec, compspec=spec)
+    PS.printstuff = False
+    PS.set_support_scheme("decim", rho=1.0)
+    assert torch.equal(PS.q0[0], torch.from_numpy(z["psr/q0"]))
+    assert abs(PS.FE - float(z["psr/FE_init"])) < 1e-9 * abs(float(z["psr/FE_init"]))
+    for it in range(2):
+        PS.GMM_opt(max_iterations=10, tol=1e-3)
+        fe = float(z[f"psr/it{it}/FE_gmm"])
+        assert abs(PS.FE - fe) < 1e-6 * abs(fe), (it, PS.FE, fe)
+        PS.Reg_opt(tol=1e-3, nmax=1)
+        fe = float(z[f"psr/it{it}/FE_reg"])
+        assert abs(PS.FE - fe) < 1e-6 * abs(fe), (it, PS.FE, fe)
+        assert rel_err(PS.x1[0, 0], torch.from_numpy(z[f"psr/it{it}/x1"])) < 1e-6

@@ -116,3 +116,15 @@ def test_c_oracle_vs_torch_oracle():
     lgn = 3 * (np.log(0.1) + 0.5 * np.log(2 * np.pi))
     t = w[None] - w.logsumexp(0) - ((X[:, None] - mu[None]) ** 2).sum(-1) / (2 * 0.01) - lgn
     assert rel_err(Tc, t.logsumexp(1)) < 1e-6
+
+
+DECIM_CASES = ("rand2d", "rand3d", "grid2d", "dup3d")
+
+
+def test_decimate_oracle_vs_reference():
+    """Greedy decimation (point_sets.py:102-133): identical kept indices, in order."""
+    z = load("decim")
+    for name in DECIM_CASES:
+        kept, rej = R.decimate(T(z[f"{name}/x"]), float(z[f"{name}/R"]))
+        assert kept == z[f"{name}/kept"].tolist(), name
+        assert sorted(kept + rej) == list(range(z[f"{name}/x"].shape[0]))
