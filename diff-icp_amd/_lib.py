@@ -131,7 +131,7 @@ def _stream(device) -> ctypes.c_void_p:
 # Algorithmic cost per (row, column) pair for D = 3 (FMA = 2 flop), counted from the pair
 # operators in csrc/lddmm_ops.hpp and csrc/gmm.hip; one exp2 per pair for all of them.
 FLOPS_PER_PAIR = {
-    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 89,
+    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 79,
     "ode_ext_fwd": 22, "ode_ext_bwd": (36 + 49) / 2, "gmm_estep": 37, "gmm_mstep": 31,
     "gmm_targets": 32,
 }

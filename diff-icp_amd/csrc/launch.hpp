@@ -60,27 +60,40 @@ int blocks_per_cu(K kernel) {
 // chip needs all its wave slots filled: aim at ~g_split_rounds x cap workgroups (chunk
 // granularity kChunkGran columns).  Deterministic for given (M, N, R, cap, knob).
 constexpr int64_t kChunkGran = 64;
-// 0 = automatic: rounds = clamp(M / 16000, 1, 8) (measured on MI355X: 20k rows -> 1,
-// 50k -> 3-4, 200k -> 8; tools/ab_tune.py); > 0 forces a value (dicp_set_option).
+// 0 = automatic: rounds = clamp(M / round_rows, 1, max_rounds), round_rows = 16000 rows for
+// the light passes (ODE forward, E-step: 20k rows -> 1, 50k -> 3, 100k -> 6, 200k -> 12) and
+// 5000 for the VJP (20k -> 4, 50k -> 10, 100k -> 20, 200k -> 24), from the sweep of
+// tools/ab_tune.py --mode rounds on MI355X; > 0 forces a value (dicp_set_option).
+// Many short blocks let the dispatcher balance the chip (uneven finish times across CUs /
+// XCDs) at the price of S x M partial-slab traffic, which stays far below HBM bandwidth.
 inline int& split_rounds() {
   static int r = 0;
   return r;
 }
-inline int64_t rounds_for(int64_t M) {
+inline int64_t rounds_for(int64_t M, int64_t round_rows, int64_t max_rounds) {
   if (split_rounds() > 0) return split_rounds();
-  int64_t r = M / 16000;
-  return r < 1 ? 1 : (r > 8 ? 8 : r);
+  int64_t r = M / round_rows;
+  return r < 1 ? 1 : (r > max_rounds ? max_rounds : r);
 }
+
+// Ops may set kRoundRows / kMaxRounds (per-pair-heavy passes want more, shorter blocks).
+template <class T, class = void>
+struct round_rows_of { static constexpr int64_t rows = 16000, max = 16; };
+template <class T>
+struct round_rows_of<T, std::void_t<decltype(T::kRoundRows)>> {
+  static constexpr int64_t rows = T::kRoundRows, max = T::kMaxRounds;
+};
 
 inline int64_t round_chunk(int64_t N, int64_t S) {
   int64_t chunk = (N + S - 1) / S;
   return (chunk + kChunkGran - 1) / kChunkGran * kChunkGran;
 }
 
-inline int num_splits_cap(int64_t M, int64_t N, int R, int64_t cap) {
+inline int num_splits_cap(int64_t M, int64_t N, int R, int64_t cap, int64_t round_rows = 16000,
+                          int64_t max_rounds = 16) {
   if (M <= 0 || N <= 0) return 1;
   const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
-  int64_t S = (rounds_for(M) * cap + bx - 1) / bx;
+  int64_t S = (rounds_for(M, round_rows, max_rounds) * cap + bx - 1) / bx;
   int64_t smax = (N + kMinChunk - 1) / kMinChunk;
   if (smax < 1) smax = 1;
   if (S > smax) S = smax;
@@ -103,7 +116,8 @@ int64_t rowred_capacity() {
 
 template <class Op, int R>
 int rowred_splits(int64_t M, int64_t N) {
-  return num_splits_cap(M, N, R, rowred_capacity<Op, R>());
+  return num_splits_cap(M, N, R, rowred_capacity<Op, R>(), round_rows_of<Op>::rows,
+                        round_rows_of<Op>::max);
 }
 
 inline int check_launch(const char* what) {

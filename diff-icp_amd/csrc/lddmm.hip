@@ -23,7 +23,7 @@ int env_r(const char* name, int def) {
 }
 int g_r_fwd = -1, g_r_bwd = -1;
 int r_fwd() { if (g_r_fwd < 0) g_r_fwd = env_r("DICP_R_FWD", 2); return g_r_fwd; }
-int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 2); return g_r_bwd; }
+int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd; }
 // eta = 0 VJP pair algebra: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48)
 int g_bwd_alg = 1;
 

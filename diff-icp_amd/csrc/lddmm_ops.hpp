@@ -493,6 +493,7 @@ struct OpOdeSelfFwd {
 // -------------------------------------------------------------------------------------
 template <int D>
 struct OpOdeSelfBwd {
+  static constexpr int64_t kRoundRows = 5000, kMaxRounds = 24;  // launch.hpp rounds_for
   static constexpr int CW4 = cw4(4 * D);
   static constexpr int NACC = 2 * D;
   static constexpr int kNOut = 2;
@@ -559,6 +560,7 @@ struct OpOdeSelfBwd {
 //   gq  = s  sum_j K e
 template <int D>
 struct OpOdeSelfBwd2 {
+  static constexpr int64_t kRoundRows = 5000, kMaxRounds = 24;  // launch.hpp rounds_for
   static constexpr int CW4 = cw4(5 * D);
   static constexpr int NACC = 2 * D;
   static constexpr int kNOut = 2;
@@ -757,6 +759,7 @@ struct OpOdeExtBwdQ {
 // -------------------------------------------------------------------------------------
 template <int D>
 struct OpOdeSelfBwdEta {
+  static constexpr int64_t kRoundRows = 5000, kMaxRounds = 24;  // launch.hpp rounds_for
   static constexpr int CW4 = cw4(4 * D);
   static constexpr int NACC = 2 * D;
   static constexpr int kNOut = 2;

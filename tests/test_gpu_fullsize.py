@@ -169,7 +169,7 @@ def test_estep_fullsize_subset_and_properties(dev):
     gam = torch.exp(t - T64[:, None])
     Y64 = gam @ mu
     assert rel_err(T.cpu()[sub], T64) < 1e-5
-    assert rel_err(T2.cpu()[sub], T64 / math.log(2)) < 1e-5
+    assert rel_err(T2.cpu()[sub], (T64 + lgn) / math.log(2)) < 1e-5     # log2, without lgn
     assert rel_err(stats.cpu()[sub, :3], Y64) < 1e-5
     # M-step column statistics: log sum_n gamma_nc and the gamma-weighted means
     col = _lib.gmm_mstep(f(X), T2, f(mu), f(lpi / math.log(2)), SIG_G).cpu().double()

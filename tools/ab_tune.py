@@ -27,12 +27,47 @@ def t_once(fn, reps=3):
     return e0.elapsed_time(e1) / reps
 
 
+def run_rounds(M, rounds):
+    """Fixed split rounds sweep of the fused ODE passes and the E-step."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    q = torch.rand(M, 3, device=dev)
+    p = 0.01 * torch.randn(M, 3, device=dev)
+    ga = torch.randn(M, 3, device=dev)
+    gb = torch.randn(M, 3, device=dev)
+    gd = torch.ones(1, device=dev)
+    w2 = torch.zeros(M, device=dev)
+    mu2 = (q * q).sum(-1)
+    fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
+           "bwd": lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0),
+           "estep": lambda: _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True)}
+    res = {}
+    reps = 3 if M <= 60000 else 1
+    sweep = (1, 2, 3, 4, 6, 8, 12, 16, 24)
+    for r in sweep:
+        _lib.set_option("split_rounds", r)
+        for fn in fns.values():
+            fn()
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for r in sweep:
+            _lib.set_option("split_rounds", r)
+            for k, fn in fns.items():
+                res.setdefault(k, {}).setdefault(r, []).append(t_once(fn, reps))
+    _lib.set_option("split_rounds", 0)
+    return {k: {str(r): round(min(v), 4) for r, v in d.items()} for k, d in res.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg"])
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds"])
+    ap.add_argument("--Ms", default="20000,50000,200000", help="row counts for --mode rounds")
     a = ap.parse_args()
+    if a.mode == "rounds":
+        print(json.dumps({"rounds_ab": {str(M): run_rounds(int(M), a.rounds) for M in a.Ms.split(",")}}))
+        return
     M, D = a.M, 3
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
