@@ -14,7 +14,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdifficp_hip.so")
+# DICP_LIB_PATH selects an experiment build (tools/ab_libs.py); default: the in-tree library
+LIB_PATH = os.environ.get("DICP_LIB_PATH") or os.path.join(_HERE, "libdifficp_hip.so")
 
 # enum dicp_red_op (include/difficp_hip.h)
 KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRADKSCAL, \

@@ -22,8 +22,23 @@
 
 namespace dicp {
 
+#ifndef DICP_STAGE_EARLY
+#define DICP_STAGE_EARLY 1
+#endif
+#ifndef DICP_PAIR_UNROLL
+#define DICP_PAIR_UNROLL 2
+#endif
+#ifdef DICP_WAVES_PER_EU
+#define DICP_KERNEL_ATTR __attribute__((amdgpu_waves_per_eu(DICP_WAVES_PER_EU)))
+#else
+#define DICP_KERNEL_ATTR
+#endif
+
 constexpr int kBlock = 256;       // threads per workgroup (4 waves)
-constexpr int kTile = 256;        // column records per LDS tile (one per thread)
+#ifndef DICP_TILE
+#define DICP_TILE 256
+#endif
+constexpr int kTile = DICP_TILE;  // column records per LDS tile (<= kBlock, one per staging thread)
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -105,7 +120,7 @@ struct Vec {
 //   Op::kMin -> accumulate by min instead of sum.
 // ------------------------------------------------------------------------------------
 template <class Op, int R>
-__global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
+__global__ __launch_bounds__(kBlock) DICP_KERNEL_ATTR void rowred_kernel(Args args, Scal sc,
                                                         int64_t M, int64_t N, int64_t chunk,
                                                         Outs outs) {
   constexpr int CW4 = Op::CW4;
@@ -150,7 +165,21 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int64_t jn = jt + kTile;
     const int cntn = jn < j1 ? (int)((j1 - jn) < kTile ? (j1 - jn) : kTile) : 0;
+#if DICP_STAGE_EARLY
+    // stage the next tile straight into the free LDS buffer (its previous contents were
+    // consumed before the last barrier): the staging registers die before the pair loop,
+    // which lowers the loop's VGPR peak; the global-load latency is exposed once per tile
+    // per wave and overlapped by the other resident waves.
+    if (tid < cntn) {
+      op_load_col<Op>(args, sc, jn + tid, pre);
+#pragma unroll
+      for (int k = 0; k < CW4; ++k)
+        lds[buf ^ 1][tid * CW4 + k] =
+            make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+    }
+#else
     if (tid < cntn) op_load_col<Op>(args, sc, jn + tid, pre);  // prefetch next tile (registers)
+#endif
 
     float acc[R][NACC];
 #pragma unroll
@@ -158,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
 #pragma unroll
       for (int k = 0; k < NACC; ++k) acc[r][k] = MIN ? __builtin_huge_valf() : 0.f;
     const float4* tile = lds[buf];
-#pragma unroll 2
+#pragma unroll DICP_PAIR_UNROLL
     for (int t = 0; t < cnt; ++t) {
       float rec[CW4 * 4];
 #pragma unroll
@@ -177,12 +206,14 @@ __global__ __launch_bounds__(kBlock) void rowred_kernel(Args args, Scal sc,
 #pragma unroll
       for (int k = 0; k < NACC; ++k)
         tot[r][k] = MIN ? fminf(tot[r][k], acc[r][k]) : tot[r][k] + acc[r][k];
+#if !DICP_STAGE_EARLY
     if (tid < cntn) {
 #pragma unroll
       for (int k = 0; k < CW4; ++k)
         lds[buf ^ 1][tid * CW4 + k] =
             make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
     }
+#endif
     __syncthreads();
     buf ^= 1;
     cnt = cntn;

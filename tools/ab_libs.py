@@ -1,0 +1,70 @@
+"""A/B of experiment builds of the native library (make -C diff-icp_amd/csrc variant
+NAME=... EXTRA=...): each build is timed in its own subprocess (DICP_LIB_PATH), the
+builds are alternated `--passes` times and the per-kernel minimum is reported.
+
+    python tools/ab_libs.py [--M 50000] [--passes 2] base early early_u1 ...
+("base" = the default in-tree library.)
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VAR = os.path.join(ROOT, "diff-icp_amd", "variants")
+
+CHILD = r"""
+import json, sys, torch
+sys.path.insert(0, %r)
+from difficp_amd import _lib
+M = %d
+dev = torch.device("cuda:0")
+torch.manual_seed(0)
+q = torch.rand(M, 3, device=dev); p = 0.01 * torch.randn(M, 3, device=dev)
+ga = torch.randn(M, 3, device=dev); gb = torch.randn(M, 3, device=dev); gd = torch.ones(1, device=dev)
+w2 = torch.zeros(M, device=dev); mu2 = (q * q).sum(-1)
+fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
+       "bwd": lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0),
+       "estep": lambda: _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True),
+       "kred": lambda: _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)}
+out = {}
+for k, fn in fns.items():
+    fn(); fn()
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(); fn(); fn(); fn(); e1.record(); e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) / 3)
+    out[k] = best
+print(json.dumps(out))
+"""
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=50000)
+    ap.add_argument("--passes", type=int, default=2)
+    ap.add_argument("names", nargs="+")
+    a = ap.parse_args()
+    res = {}
+    for _ in range(a.passes):
+        for name in a.names:
+            env = dict(os.environ)
+            if name != "base":
+                env["DICP_LIB_PATH"] = os.path.join(VAR, f"libdifficp_hip_{name}.so")
+            r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, a.M)], env=env,
+                               capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                res.setdefault(name, {})["error"] = r.stderr[-500:]
+                continue
+            t = json.loads(r.stdout.strip().splitlines()[-1])
+            d = res.setdefault(name, {})
+            for k, v in t.items():
+                d[k] = round(min(d.get(k, 1e9), v), 4)
+    print(json.dumps({"M": a.M, "ab_libs": res}))
+
+
+if __name__ == "__main__":
+    main()
