@@ -38,6 +38,9 @@ _SIGNATURES = {
     "dicp_radius_count_f32": [_P, _I64, _P, _I64, _INT, _DBL, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_fwd_f32": [_P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_bwd_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_euler_step_f32": [_P, _P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_euler_adjoint_step_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P,
+                                          _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_ext_fwd_f32": [_P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_ext_bwd_f32": [_P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
                                    _P, _SZ, _P],
@@ -257,6 +260,54 @@ def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = 
                                            _stream(dev)))
     _check_rc(rc, "ode_self_fwd")
     return v, mG, g, h
+
+
+def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=None, p_out=None):
+    """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_f32);
+    q_out / p_out: optional contiguous destinations (must not overlap q, p)."""
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    M, D = q.shape
+    qn = torch.empty_like(q) if q_out is None else q_out
+    pn = torch.empty_like(q) if p_out is None else p_out
+    for t, name in ((qn, "q_out"), (pn, "p_out")):
+        if not t.is_contiguous() or t.shape != q.shape or t.dtype != torch.float32:
+            raise ValueError(f"{name} must be a contiguous float32 tensor shaped like q")
+    g = torch.empty(M, device=q.device, dtype=torch.float32) if (want_div or eta != 0) else None
+    if M == 0:
+        return qn, pn, g
+    ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, q.device)
+    rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), M * M, 4 * M * (4 * D + 1),
+                 lambda: lib().dicp_lddmm_euler_step_f32(_ptr(q), _ptr(p), M, D, float(sigma), float(eta),
+                                                         float(dt), _ptr(qn), _ptr(pn), _ptr(g), _ptr(ws),
+                                                         nb, _stream(q.device)))
+    _check_rc(rc, "euler_step")
+    return qn, pn, g
+
+
+def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, addq=None, addp=None):
+    """(lq + dt gq + addq, lp + dt gp + addp) with (gq, gp) the ODE VJP for cotangents
+    (lq, lp, gdiv) -- one fused pass (dicp_lddmm_euler_adjoint_step_f32)."""
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    lq = _dev(lq, "lq")
+    lp = _dev(lp, "lp")
+    gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
+    addq = None if addq is None else _dev(addq, "addq")
+    addp = None if addp is None else _dev(addp, "addp")
+    M, D = q.shape
+    lqn = torch.empty_like(q)
+    lpn = torch.empty_like(q)
+    if M == 0:
+        return lqn, lpn
+    ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
+    rc = _launch("ode_self_bwd", M * M, 4 * M * 8 * D,
+                 lambda: lib().dicp_lddmm_euler_adjoint_step_f32(
+                     _ptr(q), _ptr(p), _ptr(lq), _ptr(lp), _ptr(gdiv), M, D, float(sigma), float(eta),
+                     float(dt), _ptr(addq), _ptr(addp), _ptr(lqn), _ptr(lpn), _ptr(ws), nb,
+                     _stream(q.device)))
+    _check_rc(rc, "euler_adjoint_step")
+    return lqn, lpn
 
 
 def ode_self_bwd(q, p, gv, gmG, gdiv, sigma: float, eta: float):

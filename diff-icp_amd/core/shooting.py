@@ -57,6 +57,7 @@ class ShootFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div):
+        ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
         M, D = q0.shape
         dev = q0.device
@@ -75,6 +76,14 @@ class ShootFn(torch.autograd.Function):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
             first = t == 0
+            if scheme == "Euler" and not has_x and not first:
+                # fused pass: Q[t+1], P[t+1] written by the reduction's epilogue
+                _, _, g = _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1])
+                if want_div:
+                    torch.add(C[t], g.sum().reshape(1), alpha=dt, out=C[t + 1])
+                else:
+                    C[t + 1].copy_(C[t])
+                continue
             if has_x:
                 out = _f_ext(q, p, x, sigma, eta, want_div, want_h=first)
                 v, mG, div, vx = out[:4]
@@ -156,6 +165,14 @@ class ShootFn(torch.autograd.Function):
         for t in range(nt - 1, -1, -1):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
+            if scheme == "Euler" and not has_x:
+                # fused pass: lambda_t = lambda_{t+1} + dt VJP + the loss's own cotangent at t
+                lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lc if want_div else None, sigma, eta,
+                                                 dt, None if gQ is None else gQ[t],
+                                                 None if gP is None else gP[t])
+                if gC is not None:
+                    lc = lc + gC[t]
+                continue
             if scheme == "Euler":
                 gq, gp, gx = _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div)
                 lq = torch.add(lq, gq, alpha=dt)

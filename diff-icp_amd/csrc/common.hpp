@@ -72,12 +72,26 @@ struct Args {
 
 // Output descriptor: up to 4 output arrays, each (rows, width) row-major.
 // In split mode the kernel writes partial slab `blockIdx.y` of each output at
-// out[k] + blockIdx.y * rows * width[k]; accumulate[k] = 1 means out[k] += value
-// (only honoured when not split; the merge kernel honours it otherwise).
+// out[k] + blockIdx.y * rows * width[k] and the merge applies the epilogue; otherwise the
+// kernel applies it.  Epilogue per element e of output k (the reduced value a):
+//   out[k][e] = (base[k] ? base[k][e] : 0) + alpha[k] * a + (add[k] ? add[k][e] : 0)
+//               (+ out[k][e] first if accumulate[k])
+// which fuses integrator updates such as q_next = q + dt v into the reduction.
 struct Outs {
   float* ptr[4];
   int accumulate[4];
+  const float* base[4];
+  const float* add[4];
+  float alpha[4];
 };
+
+__device__ __forceinline__ float epilogue(const Outs& o, int k, int64_t e, float a) {
+  float v = o.alpha[k] * a;
+  if (o.base[k]) v += o.base[k][e];
+  if (o.add[k]) v += o.add[k][e];
+  if (o.accumulate[k]) v += o.ptr[k][e];
+  return v;
+}
 
 // Ops may define load_row_s / load_col_s, which also see the launch scalars (e.g. to stage
 // a scalar-premultiplied copy of a column field in LDS once per column instead of
@@ -236,14 +250,9 @@ __global__ __launch_bounds__(kBlock) DICP_KERNEL_ATTR void rowred_kernel(Args ar
           float* dst = base + (int64_t)blockIdx.y * M * w + i * w;
 #pragma unroll
           for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
-        } else if (outs.accumulate[k]) {
-          float* dst = base + i * w;
-#pragma unroll
-          for (int e = 0; e < w; ++e) dst[e] += vals[off + e];
         } else {
-          float* dst = base + i * w;
 #pragma unroll
-          for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
+          for (int e = 0; e < w; ++e) base[i * w + e] = epilogue(outs, k, i * w + e, vals[off + e]);
         }
       }
       off += w;
@@ -251,19 +260,29 @@ __global__ __launch_bounds__(kBlock) DICP_KERNEL_ATTR void rowred_kernel(Args ar
   }
 }
 
-// Fixed-order merge of split partial slabs: dst[e] (+)= sum_{s<S} slab[s][e]  (or min).
+// Fixed-order merge of split partial slabs, a = sum_{s<S} slab[s][e] (or min), then the
+// Outs epilogue, for up to 4 outputs in ONE launch (blockIdx.y = output index k; the
+// slab of output k starts at slab[k]).
+struct MergeSet {
+  const float* slab[4];
+  int64_t n[4];
+  int k[4];  // output index in Outs
+};
+
 template <bool MIN>
-__global__ __launch_bounds__(kBlock) void merge_slabs_kernel(const float* __restrict__ slab,
-                                                             int64_t n, int S, float* dst,
-                                                             int accumulate) {
+__global__ __launch_bounds__(kBlock) void merge_slabs_kernel(MergeSet m, Outs o, int S) {
+  const int j = blockIdx.y;
+  const int64_t n = m.n[j];
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n) return;
+  const float* __restrict__ slab = m.slab[j];
   float a = slab[e];
   for (int s = 1; s < S; ++s) {
     const float b = slab[(int64_t)s * n + e];
     a = MIN ? fminf(a, b) : a + b;
   }
-  dst[e] = accumulate ? dst[e] + a : a;
+  const int k = m.k[j];
+  o.ptr[k][e] = epilogue(o, k, e, a);
 }
 
 }  // namespace dicp

@@ -173,12 +173,20 @@ int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, in
   rowred_kernel<Op, R><<<grid, block, 0, st>>>(a, sc, M, N, chunk, part);
   int rc = check_launch(name);
   if (rc) return rc;
+  MergeSet ms;
+  int nk = 0;
+  int64_t nmax = 0;
   for (int k = 0; k < Op::kNOut; ++k) {
     if (!fin.ptr[k]) continue;
-    const int64_t n = M * Op::kOutW[k];
-    const int64_t nb = (n + kBlock - 1) / kBlock;
-    merge_slabs_kernel<Op::kMin><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(
-        part.ptr[k], n, S, fin.ptr[k], fin.accumulate[k]);
+    ms.slab[nk] = part.ptr[k];
+    ms.n[nk] = M * Op::kOutW[k];
+    ms.k[nk] = k;
+    nmax = ms.n[nk] > nmax ? ms.n[nk] : nmax;
+    ++nk;
+  }
+  if (nk > 0) {
+    const int64_t nb = (nmax + kBlock - 1) / kBlock;
+    merge_slabs_kernel<Op::kMin><<<dim3((unsigned)nb, (unsigned)nk), dim3(kBlock), 0, st>>>(ms, fin, S);
     rc = check_launch(name);
     if (rc) return rc;
   }
@@ -203,7 +211,12 @@ inline Outs make_outs(float* p0, float* p1 = nullptr, float* p2 = nullptr, float
   o.ptr[1] = p1;
   o.ptr[2] = p2;
   o.ptr[3] = p3;
-  for (int k = 0; k < 4; ++k) o.accumulate[k] = 0;
+  for (int k = 0; k < 4; ++k) {
+    o.accumulate[k] = 0;
+    o.base[k] = nullptr;
+    o.add[k] = nullptr;
+    o.alpha[k] = 1.f;
+  }
   return o;
 }
 

@@ -161,15 +161,14 @@ extern "C" int dicp_radius_count_f32(const float* x, int64_t M, const float* y, 
 namespace {
 
 template <int D>
-int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, double eta, float* v,
-                   float* mG, float* g, float* h, void* ws, size_t wsb, hipStream_t st) {
+int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, double eta,
+                   const Outs& o, void* ws, size_t wsb, hipStream_t st) {
   Args a = {q, p, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
-  const Outs o = make_outs(v, mG, g, h);
   if (eta != 0.0)
     return launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
-  if (g != nullptr)
+  if (o.ptr[2] != nullptr)
     return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
 }
@@ -186,19 +185,17 @@ size_t ode_self_fwd_ws(int64_t M) {
 
 template <int D>
 int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float* gmG,
-                   const float* gdiv, int64_t M, double sigma, double eta, float* gq, float* gp,
+                   const float* gdiv, int64_t M, double sigma, double eta, const Outs& o,
                    void* ws, size_t wsb, hipStream_t st) {
   Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
   if (eta != 0.0) {
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
-    const Outs o = make_outs(gq, gp);
     return launch_r<OpOdeSelfBwdEta<D>>(r_bwd(), "ode_self_bwd_eta", a, sc, M, M, o, ws, wsb, st);
   }
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
-  const Outs o = make_outs(gq, gp);
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
@@ -278,8 +275,8 @@ extern "C" int dicp_lddmm_ode_self_fwd_f32(const float* q, const float* p, int64
     return DICP_ERR_INVALID;
   }
   switch (D) {
-    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, v, mG, g, h, ws, ws_bytes, st);
-    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, v, mG, g, h, ws, ws_bytes, st);
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, make_outs(v, mG, g, h), ws, ws_bytes, st);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, make_outs(v, mG, g, h), ws, ws_bytes, st);
     default: set_error("ode_self_fwd: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
@@ -295,9 +292,65 @@ extern "C" int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const
     return DICP_ERR_INVALID;
   }
   switch (D) {
-    case 2: return ode_self_bwd_d<2>(q, p, gv, gmG, gdiv, M, sigma, eta, gq, gp, ws, ws_bytes, st);
-    case 3: return ode_self_bwd_d<3>(q, p, gv, gmG, gdiv, M, sigma, eta, gq, gp, ws, ws_bytes, st);
+    case 2: return ode_self_bwd_d<2>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, ws_bytes, st);
+    case 3: return ode_self_bwd_d<3>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, ws_bytes, st);
     default: set_error("ode_self_bwd: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+// One explicit-Euler step of the shooting ODE with the state update fused into the
+// reduction's epilogue: q_next = q + dt v(q,p), p_next = p + dt mG(q,p), g rows as in
+// dicp_lddmm_ode_self_fwd_f32 (integrators.py:20-33 EulerIntegrator over LDDMM.py:176-227).
+extern "C" int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t M, int D,
+                                         double sigma, double eta, double dt, float* q_next,
+                                         float* p_next, float* g, void* ws, size_t ws_bytes,
+                                         dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || (M > 0 && (!q || !p || !q_next || !p_next)) || !(sigma > 0) ||
+      (M > 0 && (q_next == q || q_next == p || p_next == q || p_next == p))) {
+    set_error("dicp_lddmm_euler_step_f32: invalid arguments (outputs must not alias inputs)");
+    return DICP_ERR_INVALID;
+  }
+  Outs o = make_outs(q_next, p_next, g, nullptr);
+  o.base[0] = q;
+  o.base[1] = p;
+  o.alpha[0] = o.alpha[1] = (float)dt;
+  switch (D) {
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, o, ws, ws_bytes, st);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, o, ws, ws_bytes, st);
+    default: set_error("euler_step: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+// The matching adjoint step (exact discrete adjoint of the Euler step):
+//   lq_next = lq + dt * d/dq[lq.v + lp.mG + gdiv sum g] + addq,
+//   lp_next = lp + dt * d/dp[...]                        + addp
+// (addq / addp: the loss's own cotangent on the state at this time, or NULL).
+extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
+                                                 const float* lp, const float* gdiv, int64_t M,
+                                                 int D, double sigma, double eta, double dt,
+                                                 const float* addq, const float* addp,
+                                                 float* lq_next, float* lp_next, void* ws,
+                                                 size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const float* ins[4] = {q, p, lq, lp};
+  bool alias = false;
+  for (const float* x : ins) alias = alias || x == lq_next || x == lp_next;
+  if (M < 0 || (M > 0 && (!q || !p || !lq || !lp || !lq_next || !lp_next || alias)) ||
+      !(sigma > 0)) {
+    set_error("dicp_lddmm_euler_adjoint_step_f32: invalid arguments (outputs must not alias inputs)");
+    return DICP_ERR_INVALID;
+  }
+  Outs o = make_outs(lq_next, lp_next);
+  o.base[0] = lq;
+  o.base[1] = lp;
+  o.add[0] = addq;
+  o.add[1] = addp;
+  o.alpha[0] = o.alpha[1] = (float)dt;
+  switch (D) {
+    case 2: return ode_self_bwd_d<2>(q, p, lq, lp, gdiv, M, sigma, eta, o, ws, ws_bytes, st);
+    case 3: return ode_self_bwd_d<3>(q, p, lq, lp, gdiv, M, sigma, eta, o, ws, ws_bytes, st);
+    default: set_error("euler_adjoint_step: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
 

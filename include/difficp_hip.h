@@ -106,6 +106,24 @@ int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const float* gv,
                                 double sigma, double eta, float* gq, float* gp, void* ws,
                                 size_t ws_bytes, dicp_stream_t stream);
 
+/* One explicit-Euler step with the state update fused into the pass's epilogue
+ * (integrators.py:20-33 EulerIntegrator over LDDMMModel.ODE, LDDMM.py:176-227):
+ *   q_next = q + dt v(q,p),  p_next = p + dt mG(q,p),  g (M,) as above or NULL.
+ * Outputs must not alias inputs.  Workspace kind DICP_WS_ODE_SELF_FWD. */
+int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t M, int D, double sigma,
+                              double eta, double dt, float* q_next, float* p_next, float* g,
+                              void* ws, size_t ws_bytes, dicp_stream_t stream);
+
+/* Its exact discrete adjoint (the reverse sweep of optim.py:46's backward through the Euler
+ * loop): with (gq, gp) the VJP of dicp_lddmm_ode_self_bwd_f32 for cotangents (lq, lp, gdiv),
+ *   lq_next = lq + dt gq + addq,  lp_next = lp + dt gp + addp   (addq/addp (M,D) or NULL).
+ * Outputs must not alias inputs.  Workspace kind DICP_WS_ODE_SELF_BWD. */
+int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
+                                      const float* lp, const float* gdiv, int64_t M, int D,
+                                      double sigma, double eta, double dt, const float* addq,
+                                      const float* addp, float* lq_next, float* lp_next,
+                                      void* ws, size_t ws_bytes, dicp_stream_t stream);
+
 /* External data points x (N,D) carried by the flow (LDDMM.py:219-227):
  *   vx_i = v(x_i) (LDDMM.py:226), gx_i = per-row terms of mdivsum(x,q,p) (LDDMM.py:223),
  *   summed in row (x) order; gx may be NULL. */

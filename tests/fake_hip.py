@@ -95,6 +95,28 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta):
     return _out(gq, q), _out(gp, q)
 
 
+def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None):
+    v, mG, g, _ = ode_self_fwd(q, p, sigma, eta, want_div)
+    qn, pn = q + dt * v, p + dt * mG
+    if q_out is not None:
+        q_out.copy_(qn)
+        qn = q_out
+    if p_out is not None:
+        p_out.copy_(pn)
+        pn = p_out
+    return qn, pn, g
+
+
+def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None):
+    gq, gp = ode_self_bwd(q, p, lq, lp, gdiv, sigma, eta)
+    lqn, lpn = lq + dt * gq, lp + dt * gp
+    if addq is not None:
+        lqn = lqn + addq
+    if addp is not None:
+        lpn = lpn + addp
+    return lqn, lpn
+
+
 def _ext_terms(x, q, p, sigma, eta):
     s = 1.0 / sigma ** 2
     D = x.shape[1]
@@ -169,7 +191,7 @@ def radius_count(x, y, radius):
     return _out((d <= radius ** 2).sum(1).to(torch.float64), x)
 
 
-_ENTRIES = ("radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+_ENTRIES = ("euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 
