@@ -177,7 +177,7 @@ def test_fused_euler_steps(dev, M, eta):
     assert torch.equal(g2, gr)
     Qo, Po = torch.empty_like(q), torch.empty_like(q)
     L.euler_step(q, p, 0.1, eta, dt, False, q_out=Qo, p_out=Po)
-    assert rel_err(Qo, qn) < 1e-7 and rel_err(Po, pn) < 1e-7
+    assert rel_err(Qo, qn) < 1e-6 and rel_err(Po, pn) < 1e-6   # other variant: other split order
     gq, gp = L.ode_self_bwd(q, p, lq, lp, gd, 0.1, eta)
     for addq in (None, aq):
         lqn, lpn = L.euler_adjoint_step(q, p, lq, lp, gd, 0.1, eta, dt, addq, None)
