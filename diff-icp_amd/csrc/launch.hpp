@@ -89,11 +89,18 @@ inline int64_t round_chunk(int64_t N, int64_t S) {
   return (chunk + kChunkGran - 1) / kChunkGran * kChunkGran;
 }
 
+// Experiment knob (dicp_set_option "force_splits"): > 0 forces the split count.
+inline int& force_splits() {
+  static int s = 0;
+  return s;
+}
+
 inline int num_splits_cap(int64_t M, int64_t N, int R, int64_t cap, int64_t round_rows = 16000,
                           int64_t max_rounds = 16) {
   if (M <= 0 || N <= 0) return 1;
   const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
   int64_t S = (rounds_for(M, round_rows, max_rounds) * cap + bx - 1) / bx;
+  if (force_splits() > 0) S = force_splits();
   int64_t smax = (N + kMinChunk - 1) / kMinChunk;
   if (smax < 1) smax = 1;
   if (S > smax) S = smax;

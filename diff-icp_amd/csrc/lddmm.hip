@@ -2,6 +2,7 @@
 // the fused LDDMM geodesic-shooting ODE (LDDMMModel.ODE, LDDMM.py:176-227) for gfx950.
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
+#include "lddmm_sym.hpp"
 
 #include <stdlib.h>
 
@@ -24,8 +25,9 @@ int env_r(const char* name, int def) {
 int g_r_fwd = -1, g_r_bwd = -1;
 int r_fwd() { if (g_r_fwd < 0) g_r_fwd = env_r("DICP_R_FWD", 2); return g_r_fwd; }
 int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd; }
-// eta = 0 VJP pair algebra: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48)
-int g_bwd_alg = 1;
+// eta = 0 VJP: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48), 2 = symmetric
+// pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair)
+int g_bwd_alg = 2;
 
 template <class Op>
 int launch_r(int R, const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
@@ -87,8 +89,13 @@ extern "C" int dicp_set_option(const char* name, int value) {
     split_rounds() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "force_splits")) {
+    if (value < 0 || value > 65536) return DICP_ERR_INVALID;
+    force_splits() = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "bwd_alg")) {
-    if (value != 0 && value != 1) return DICP_ERR_INVALID;
+    if (value < 0 || value > 2) return DICP_ERR_INVALID;
     g_bwd_alg = value;
     return DICP_OK;
   }
@@ -196,6 +203,7 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
+  if (g_bwd_alg == 2) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st);
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
@@ -411,7 +419,9 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
       size_t b = D == 2 ? ws_r<OpOdeSelfBwdEta<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwdEta<3>>(r_bwd(), M, M);
       size_t c = D == 2 ? ws_r<OpOdeSelfBwd2<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd2<3>>(r_bwd(), M, M);
       a = a > b ? a : b;
-      return a > c ? a : c;
+      a = a > c ? a : c;
+      const size_t d = sym_ws_bytes(M, D);
+      return a > d ? a : d;
     }
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);
     case DICP_WS_ODE_EXT_BWD: return D == 2 ? ode_ext_bwd_ws<2>(N, M) : ode_ext_bwd_ws<3>(N, M);

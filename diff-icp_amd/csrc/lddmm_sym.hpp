@@ -1,0 +1,349 @@
+// Symmetric (pair-once) VJP of the fused LDDMM ODE, eta = 0 (classic / hybrid models).
+//
+// The self-interaction VJP of OpOdeSelfBwd2 is a sum over ORDERED pairs (i, j) whose pair
+// quantities are symmetric: K_ij = K_ji, pp, zb, zu, iap and w are equal for (i, j) and
+// (j, i), while z, db, u and e = w z - u flip sign.  Evaluating every UNORDERED pair once
+// and scattering it to both rows needs ~63 VALU per unordered pair instead of 2 x 49, and
+// one exp instead of two ("Symmetric VJP").
+//
+// Work decomposition (all deterministic, no atomics):
+//  * points are grouped in groups of kSymG = 128 (one wave: 64 lanes x 2 rows);
+//  * a workgroup = kSymQ = 4 waves = 4 consecutive row groups A = 4Q + w ("quad" Q) and
+//    a chunk of kSymL consecutive column groups B in [4Q + k L, 4Q + (k+1) L);
+//  * wave A vs group B: A < B -> every pair once ("sym" mode: row side into registers,
+//    column side through a rotating accumulator); A == B -> the 128 x 128 ordered pairs,
+//    row side only ("diag" mode, self pair included); A > B -> nothing (that pair of groups
+//    is done by wave B of the same workgroup);
+//  * column side: at step k lane l pairs its two rows with column (l + k) mod 64 of the
+//    current 64-column half (per-lane LDS reads, conflict-free planes); the column's
+//    running sum rides along in a register that a wave_rol:1 DPP rotation hands to the
+//    lane that owns that column at the next step, so after 64 steps it has collected all
+//    128 rows of the wave without any cross-lane reduction tree;
+//  * the 4 waves' column sums are added in LDS in wave order and written to partial slot Q
+//    of group B; each wave's row sums go to slot (Q_A + 1 + k) of its group A; a merge pass
+//    adds the slots of every row in slot order and applies the Outs epilogue.
+#pragma once
+#include "launch.hpp"
+#include "lddmm_ops.hpp"
+
+namespace dicp {
+
+constexpr int kSymG = 128;   // points per group (= rows of one wave)
+constexpr int kSymQ = 4;     // row groups (waves) per workgroup
+constexpr int kSymL = 4;     // column groups per workgroup
+constexpr float kFar = 1.0e12f;  // padding coordinate: K = exp2(-|z|^2) = 0 against real points
+
+struct SymGeom {
+  int64_t M;
+  int nG;     // groups
+  int nQ;     // quads
+  int L;      // column groups per workgroup
+  int Kmax;   // chunks of quad 0
+  int nslot;  // slots per row (max)
+};
+
+inline SymGeom sym_geom(int64_t M) {
+  SymGeom g;
+  g.M = M;
+  g.nG = (int)((M + kSymG - 1) / kSymG);
+  g.nQ = (g.nG + kSymQ - 1) / kSymQ;
+  g.L = kSymL;
+  g.Kmax = (g.nG + g.L - 1) / g.L;
+  g.nslot = g.nQ + 1 + g.Kmax;
+  return g;
+}
+
+// slots used by the rows of group T: column slots 0..Q_T, row slots Q_T+1 .. Q_T+K_{Q_T}
+__host__ __device__ inline int sym_nslots(int T, int nG, int L) {
+  const int Q = T / kSymQ;
+  return Q + 1 + (nG - kSymQ * Q + L - 1) / L;
+}
+
+template <int D>
+struct SymBwd {
+  static constexpr int CW = cw4(5 * D);  // float4 planes per column record
+  static constexpr int W = 2 * D;        // accumulators per point: gp / s1 (D), gq / s (D)
+
+  // Per-row state (scaled coordinates as OpOdeSelfBwd2, plus a / s1 for the column side).
+  struct Row {
+    float q[D], p[D], b[D], ia_a[D], sia_p[D], gp[D], ap[D];
+  };
+
+  __device__ static void load_row(const Args& a, const Scal& sc, int64_t i, bool valid, Row& r) {
+    const float ia = 1.0f / a.scale, sia = sc.aux1 * ia, is1 = 1.0f / sc.aux1, gam = sc.aux0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float q = valid ? a.r0[i * D + d] : 0.f;
+      const float p = valid ? a.r1[i * D + d] : 0.f;
+      const float av = valid ? a.r2[i * D + d] : 0.f;
+      const float b = valid ? a.r3[i * D + d] : 0.f;
+      r.q[d] = valid ? a.scale * q : kFar;
+      r.p[d] = p;
+      r.b[d] = b;
+      r.ia_a[d] = ia * av;
+      r.sia_p[d] = sia * p;
+      r.gp[d] = gam * p;
+      r.ap[d] = is1 * av;
+    }
+  }
+
+  // column record: q' (D), p (D), a / s1 (D), b (D), gam p (D)
+  __device__ static void load_col(const Args& a, const Scal& sc, int64_t j, bool valid, float* rec) {
+    const float is1 = 1.0f / sc.aux1, gam = sc.aux0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float q = valid ? a.c0[j * D + d] : 0.f;
+      const float p = valid ? a.c1[j * D + d] : 0.f;
+      const float av = valid ? a.c2[j * D + d] : 0.f;
+      const float b = valid ? a.c3[j * D + d] : 0.f;
+      rec[d] = valid ? a.scale * q : kFar;
+      rec[D + d] = p;
+      rec[2 * D + d] = is1 * av;
+      rec[3 * D + d] = b;
+      rec[4 * D + d] = gam * p;
+    }
+#pragma unroll
+    for (int k = 5 * D; k < 4 * CW; ++k) rec[k] = 0.f;
+  }
+
+  // ordered pair (i, j), row side only (== OpOdeSelfBwd2::pair)
+  __device__ static void pair_row(float gam, const Row& r, const float* rec, float* acc) {
+    float z[D], db[D], u[D];
+    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+    const float* gpj = rec + 4 * D;
+    const float pp = dot<D>(r.p, pj);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      db[d] = r.b[d] - bj[d];
+      u[d] = fmaf(-pp, db[d], r.gp[d] - gpj[d]);
+    }
+    const float zu = dot<D>(z, u);
+    const float zb = dot<D>(z, db);
+    const float iap = dot<D>(r.ia_a, pj) + dot<D>(aj, r.sia_p);
+    const float w = fmaf(kS2, zu, -iap);
+    const float Kzb = K * zb;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(Kzb, pj[d], fmaf(K, fmaf(-gam, z[d], aj[d]), acc[d]));
+      acc[D + d] = fmaf(K, fmaf(w, z[d], -u[d]), acc[D + d]);
+    }
+  }
+
+  // unordered pair {i, j}: row side into acc, column side (the (j, i) terms) into ct
+  // (FIRST: ct is initialised instead of accumulated).
+  template <bool FIRST>
+  __device__ static void pair_sym(float gam, const Row& r, const float* rec, float* acc, float* ct) {
+    float z[D], db[D], u[D];
+    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+    const float* gpj = rec + 4 * D;
+    const float pp = dot<D>(r.p, pj);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      db[d] = r.b[d] - bj[d];
+      u[d] = fmaf(-pp, db[d], r.gp[d] - gpj[d]);
+    }
+    const float zu = dot<D>(z, u);
+    const float zb = dot<D>(z, db);
+    const float iap = dot<D>(r.ia_a, pj) + dot<D>(aj, r.sia_p);
+    const float w = fmaf(kS2, zu, -iap);
+    const float Kzb = K * zb;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float e = fmaf(w, z[d], -u[d]);
+      acc[d] = fmaf(Kzb, pj[d], fmaf(K, fmaf(-gam, z[d], aj[d]), acc[d]));  // gp_i / s1
+      acc[D + d] = fmaf(K, e, acc[D + d]);                                   // gq_i / s
+      const float t = fmaf(gam, z[d], r.ap[d]);                              // a_i/s1 + gam z
+      ct[d] = fmaf(Kzb, r.p[d], FIRST ? K * t : fmaf(K, t, ct[d]));          // gp_j / s1
+      ct[D + d] = FIRST ? -K * e : fmaf(-K, e, ct[D + d]);                   // gq_j / s
+    }
+  }
+};
+
+__device__ __forceinline__ float rol1(float x) {
+  // wave_rol:1 -- lane l receives lane (l + 1) mod 64
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x134, 0xF, 0xF, false));
+}
+
+// slab layout: slab[slot][row][W]
+template <int D>
+__global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+                                                      float* __restrict__ slab, int64_t slot_stride) {
+  using S = SymBwd<D>;
+  constexpr int CW = S::CW, W = S::W;
+  __shared__ float4 planes[2][CW][kSymG];
+  __shared__ float colacc[kSymQ][kSymG][W];
+  if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
+  const float gam = sc.aux0;
+
+  const int Q = blockIdx.y, kc = blockIdx.x;
+  const int B0 = kSymQ * Q + kc * L;
+  if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
+  const int B1 = min(B0 + L, nG);
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int A = kSymQ * Q + wv;
+
+  typename S::Row row[2];
+  int64_t ri[2];
+  bool rv[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    ri[r] = (int64_t)A * kSymG + r * 64 + l;
+    rv[r] = A < nG && ri[r] < M;
+    S::load_row(a, sc, rv[r] ? ri[r] : 0, rv[r], row[r]);
+  }
+  float racc[2][W];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int k = 0; k < W; ++k) racc[r][k] = 0.f;
+
+  auto stage = [&](int B, int buf) {
+    if (tid < kSymG) {
+      const int64_t j = (int64_t)B * kSymG + tid;
+      float rec[4 * CW];
+      S::load_col(a, sc, j < M ? j : 0, j < M, rec);
+#pragma unroll
+      for (int m = 0; m < CW; ++m)
+        planes[buf][m][tid] = make_float4(rec[4 * m], rec[4 * m + 1], rec[4 * m + 2], rec[4 * m + 3]);
+    }
+  };
+
+  int buf = 0;
+  stage(B0, 0);
+  __syncthreads();
+  for (int B = B0; B < B1; ++B) {
+    if (B + 1 < B1) stage(B + 1, buf ^ 1);
+    const bool sym = A < B;          // wave-uniform
+    const bool diag = A == B;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float cacc[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+      if (sym) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int c = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW];
+#pragma unroll
+          for (int m = 0; m < CW; ++m) {
+            const float4 v = planes[buf][m][c];
+            rec[4 * m] = v.x;
+            rec[4 * m + 1] = v.y;
+            rec[4 * m + 2] = v.z;
+            rec[4 * m + 3] = v.w;
+          }
+          float ct[W];
+          S::template pair_sym<true>(gam, row[0], rec, racc[0], ct);
+          S::template pair_sym<false>(gam, row[1], rec, racc[1], ct);
+          // cacc belonged to column (l + k2 - 1); bring column (l + k2)'s sum to this lane
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+        }
+        // lane l holds column (l + 63) & 63; one more rotation aligns lane l with column l
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+      } else if (diag) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int c = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW];
+#pragma unroll
+          for (int m = 0; m < CW; ++m) {
+            const float4 v = planes[buf][m][c];
+            rec[4 * m] = v.x;
+            rec[4 * m + 1] = v.y;
+            rec[4 * m + 2] = v.z;
+            rec[4 * m + 3] = v.w;
+          }
+          S::pair_row(gam, row[0], rec, racc[0]);
+          S::pair_row(gam, row[1], rec, racc[1]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) colacc[wv][h * 64 + l][k] = cacc[k];
+    }
+    __syncthreads();
+    if (tid < kSymG) {
+      const int64_t j = (int64_t)B * kSymG + tid;
+      if (j < M) {
+        float* dst = slab + (int64_t)Q * slot_stride + j * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+          dst[k] = ((colacc[0][tid][k] + colacc[1][tid][k]) + colacc[2][tid][k]) + colacc[3][tid][k];
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  // row sums of this workgroup's column chunk -> slot Q + 1 + kc of group A
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (!rv[r]) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = racc[r][k];
+  }
+}
+
+// out0 = gq = s * sum(gq/s), out1 = gp = s1 * sum(gp/s1), with the Outs epilogue.
+template <int D>
+__global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
+                                                        int64_t slot_stride, int64_t M, int nG,
+                                                        int L, float s, float s1, Outs o) {
+  constexpr int W = 2 * D;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= M * W) return;
+  const int64_t row = e / W;
+  const int c = (int)(e - row * W);
+  const int ns = sym_nslots((int)(row / kSymG), nG, L);
+  float acc = slab[e];
+  for (int t = 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
+  if (c < D) {
+    const int64_t idx = row * D + c;
+    o.ptr[1][idx] = epilogue(o, 1, idx, s1 * acc);
+  } else {
+    const int64_t idx = row * D + (c - D);
+    o.ptr[0][idx] = epilogue(o, 0, idx, s * acc);
+  }
+}
+
+inline size_t sym_ws_bytes(int64_t M, int D) {
+  if (M <= 0) return 0;
+  const SymGeom g = sym_geom(M);
+  return (size_t)g.nslot * (size_t)M * (size_t)(2 * D) * sizeof(float);
+}
+
+template <int D>
+int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                   hipStream_t st) {
+  if (M <= 0) return DICP_OK;
+  const SymGeom g = sym_geom(M);
+  const size_t need = sym_ws_bytes(M, D);
+  if (ws == nullptr || wsb < need) {
+    set_error("ode_self_bwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  if (o.ptr[0] == nullptr || o.ptr[1] == nullptr) {
+    set_error("ode_self_bwd(sym): both outputs are required");
+    return DICP_ERR_INVALID;
+  }
+  float* slab = reinterpret_cast<float*>(ws);
+  const int64_t stride = M * 2 * D;
+  sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
+      a, sc, M, g.nG, g.L, slab, stride);
+  int rc = check_launch("ode_self_bwd(sym)");
+  if (rc) return rc;
+  const int64_t n = M * 2 * D;
+  sym_merge_kernel<D><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+      slab, stride, M, g.nG, g.L, sc.s, sc.aux1, o);
+  return check_launch("ode_self_bwd(sym merge)");
+}
+
+}  // namespace dicp

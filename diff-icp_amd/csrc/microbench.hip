@@ -62,7 +62,22 @@ __global__ __launch_bounds__(256) void pkfma_probe(float* out, int iters, float 
   if (s == 12345.f) out[threadIdx.x] = s;
 }
 
+template <int CTRL>
+__global__ __launch_bounds__(64) void dpp_probe(int* out) {
+  const int l = threadIdx.x;
+  out[l] = __builtin_amdgcn_update_dpp(-1, l, CTRL, 0xF, 0xF, false);
+}
+
 }  // namespace
+
+// Lane map of a wave-wide DPP rotate: out[l] = source lane read by lane l
+// (which = 0: wave_rol:1 (0x134), 1: wave_ror:1 (0x13C)); one wave64.
+extern "C" int dicp_mb_dpp(int which, int* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (which == 0) dpp_probe<0x134><<<1, 64, 0, st>>>(out);
+  else dpp_probe<0x13C><<<1, 64, 0, st>>>(out);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 // kind: 0 = exp2, 1 = fma, 2 = pk_fma.  Returns 0 on success.  ops per launch:
 // blocks*256*iters*kChains (x2 lanes for pk_fma).

@@ -105,7 +105,7 @@ def test_ode_self_fwd(dev, version, M, D):
         assert rel_err(gdiv.sum().cpu(), c64) <= _tol(c64, c32)
 
 
-@pytest.mark.parametrize("M,D", [(3, 2), (300, 2), (700, 3), (2100, 3)])
+@pytest.mark.parametrize("M,D", [(3, 2), (300, 2), (700, 3), (2100, 3), (4700, 3)])
 @pytest.mark.parametrize("withlogdet,gradcomp", [(False, False), (True, False), (True, True), (False, True)])
 def test_ode_self_bwd(dev, M, D, withlogdet, gradcomp):
     L = _lib()
@@ -120,12 +120,12 @@ def test_ode_self_bwd(dev, M, D, withlogdet, gradcomp):
     Lf = (a * v).sum() + (bm * mG).sum() + (gam * c).sum()
     gq64, gp64 = torch.autograd.grad(Lf, (q, p))
     f = lambda t: t.detach().float().to(dev)
-    for alg in (0, 1):  # both eta = 0 pair-algebra variants (lddmm_ops.hpp)
+    for alg in (0, 1, 2):  # eta = 0 variants: pair algebras (lddmm_ops.hpp), symmetric kernel
         L.set_option("bwd_alg", alg)
         try:
             gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, m.eta)
         finally:
-            L.set_option("bwd_alg", 1)
+            L.set_option("bwd_alg", 2)
         assert rel_err(gq.cpu(), gq64) < 2e-5, (alg, rel_err(gq.cpu(), gq64))
         assert rel_err(gp.cpu(), gp64) < 2e-5, (alg, rel_err(gp.cpu(), gp64))
 
@@ -183,3 +183,38 @@ def test_fused_euler_steps(dev, M, eta):
         lqn, lpn = L.euler_adjoint_step(q, p, lq, lp, gd, 0.1, eta, dt, addq, None)
         ref_q = lq + dt * gq + (0 if addq is None else addq)
         assert rel_err(lqn, ref_q) < 1e-6 and rel_err(lpn, lp + dt * gp) < 1e-6
+
+
+def test_dpp_wave_rol_semantics(dev):
+    """The symmetric VJP rotates column sums with DPP wave_rol:1 assuming lane l reads lane
+    l + 1 (lddmm_sym.hpp rol1); pin that on the hardware."""
+    import ctypes
+    import os
+    mb = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                  "diff-icp_amd", "libdifficp_microbench.so"))
+    out = torch.zeros(64, dtype=torch.int32, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert mb.dicp_mb_dpp(0, ctypes.c_void_p(out.data_ptr()), st) == 0
+    assert out.cpu().tolist() == [(l + 1) % 64 for l in range(64)]
+
+
+@pytest.mark.parametrize("M", [128, 129, 1000, 5000])
+def test_sym_bwd_vs_ordered(dev, M):
+    """Symmetric pair-once VJP == ordered kernel (alg 1) up to fp32 summation order, incl.
+    partial last groups and quads; deterministic run to run."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 1)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    a = torch.randn(M, 3, generator=g).to(dev)
+    b = torch.randn(M, 3, generator=g).to(dev)
+    gd = torch.full((1,), -0.4, device=dev)
+    L.set_option("bwd_alg", 1)
+    try:
+        gq1, gp1 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+    finally:
+        L.set_option("bwd_alg", 2)
+    gq2, gp2 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+    gq3, gp3 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+    assert rel_err(gq2, gq1) < 2e-6 and rel_err(gp2, gp1) < 2e-6
+    assert torch.equal(gq2, gq3) and torch.equal(gp2, gp3)

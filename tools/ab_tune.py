@@ -58,13 +58,45 @@ def run_rounds(M, rounds):
     return {k: {str(r): round(min(v), 4) for r, v in d.items()} for k, d in res.items()}
 
 
+def run_splits(M, rounds):
+    """Forced split-count sweep (force_splits) of the ODE forward and VJP at M rows: shows the
+    wave-quantisation sawtooth (period = resident slots / row blocks)."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    q = torch.rand(M, 3, device=dev)
+    p = 0.01 * torch.randn(M, 3, device=dev)
+    ga = torch.randn(M, 3, device=dev)
+    gb = torch.randn(M, 3, device=dev)
+    gd = torch.ones(1, device=dev)
+    fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
+           "bwd": lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0)}
+    auto = {"fwd": _lib.num_splits(1, M, M), "bwd": _lib.num_splits(2, M, M)}
+    sweep = list(range(8, 97, 2))
+    res = {}
+    for s in sweep:
+        _lib.set_option("force_splits", s)
+        for fn in fns.values():
+            fn()
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for s in sweep:
+            _lib.set_option("force_splits", s)
+            for k, fn in fns.items():
+                res.setdefault(k, {}).setdefault(s, []).append(t_once(fn, 2))
+    _lib.set_option("force_splits", 0)
+    return {"auto": auto, **{k: {str(s): round(min(v), 4) for s, v in d.items()} for k, d in res.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds"])
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits"])
     ap.add_argument("--Ms", default="20000,50000,200000", help="row counts for --mode rounds")
     a = ap.parse_args()
+    if a.mode == "splits":
+        print(json.dumps({"splits_ab": run_splits(a.M, a.rounds)}))
+        return
     if a.mode == "rounds":
         print(json.dumps({"rounds_ab": {str(M): run_rounds(int(M), a.rounds) for M in a.Ms.split(",")}}))
         return
@@ -88,6 +120,7 @@ def main():
         for alg in (0, 1):
             for r in (1, 2, 4):
                 variants.append((f"bwd_alg{alg}_r{r}", {"bwd_alg": alg, "r_bwd": r, "split_rounds": 0}, bwd))
+        variants.append(("bwd_alg2_sym", {"bwd_alg": 2, "split_rounds": 0}, bwd))
         variants.append(("fwd_r2", {"r_fwd": 2, "split_rounds": 0}, fwd))
     res = {v[0]: [] for v in variants}
 
