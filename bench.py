@@ -204,6 +204,8 @@ def _main(out):
                     "traffic": traffic, "kernel": dom, "launches": d["launches"],
                     "avg_launch_ms": round(d["ms"] / d["launches"], 4),
                     "pairs_per_launch": d["pairs"] / d["launches"],
+                    "flops_per_pair": _lib.FLOPS_PER_PAIR.get(dom),
+                    "flops_source": "SURVEY.md 8(d) per-unit figure x ordered pairs (M^2)",
                     "alg_bytes_per_launch": d["bytes"] / d["launches"],
                     "alg_hbm_GBps": round(d["bytes"] / d["launches"] / avg_s / 1e9, 3),
                     "share_of_step_time": round(d["ms"] * 1e-3 / elapsed, 3),

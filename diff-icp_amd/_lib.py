@@ -132,10 +132,14 @@ def _stream(device) -> ctypes.c_void_p:
 # ---------------------------------------------------------------------------------------
 # Optional live kernel accounting (bench.py): HIP events around each launch on the launch
 # stream, algorithmic pair / flop / byte counts per launch.
-# Algorithmic cost per (row, column) pair for D = 3 (FMA = 2 flop), counted from the pair
-# operators in csrc/lddmm_ops.hpp and csrc/gmm.hip; one exp2 per pair for all of them.
+# Algorithmic cost per ordered (row, column) pair for D = 3 (FMA = 2 flop; one exp2 per pair):
+# the per-unit figures of SURVEY.md 8(d) where it gives one (KRed 15, fused ODE forward 33,
+# fused VJP ~70), otherwise counted from the pair operators (csrc/lddmm_ops.hpp, gmm.hip).
+# These price the OPERATION, not a kernel's instruction stream: the symmetric VJP
+# (lddmm_sym.hpp) executes ~53 flop per ordered pair because it evaluates each unordered
+# pair once, so its effective rate can exceed the rate of executed arithmetic.
 FLOPS_PER_PAIR = {
-    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 79,
+    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 70,
     "ode_ext_fwd": 22, "ode_ext_bwd": (36 + 49) / 2, "gmm_estep": 37, "gmm_mstep": 31,
     "gmm_targets": 32,
 }

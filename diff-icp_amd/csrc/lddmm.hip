@@ -89,6 +89,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     split_rounds() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "sym_L")) {
+    if (value < 1 || value > 64) return DICP_ERR_INVALID;
+    sym_L() = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "force_splits")) {
     if (value < 0 || value > 65536) return DICP_ERR_INVALID;
     force_splits() = value;

@@ -9,7 +9,7 @@
 // Work decomposition (all deterministic, no atomics):
 //  * points are grouped in groups of kSymG = 128 (one wave: 64 lanes x 2 rows);
 //  * a workgroup = kSymQ = 4 waves = 4 consecutive row groups A = 4Q + w ("quad" Q) and
-//    a chunk of kSymL consecutive column groups B in [4Q + k L, 4Q + (k+1) L);
+//    a chunk of L consecutive column groups B in [4Q + k L, 4Q + (k+1) L);
 //  * wave A vs group B: A < B -> every pair once ("sym" mode: row side into registers,
 //    column side through a rotating accumulator); A == B -> the 128 x 128 ordered pairs,
 //    row side only ("diag" mode, self pair included); A > B -> nothing (that pair of groups
@@ -30,7 +30,11 @@ namespace dicp {
 
 constexpr int kSymG = 128;   // points per group (= rows of one wave)
 constexpr int kSymQ = 4;     // row groups (waves) per workgroup
-constexpr int kSymL = 4;     // column groups per workgroup
+// column groups per workgroup (dicp_set_option "sym_L"; default from an MI355X sweep)
+inline int& sym_L() {
+  static int L = 4;
+  return L;
+}
 constexpr float kFar = 1.0e12f;  // padding coordinate: K = exp2(-|z|^2) = 0 against real points
 
 struct SymGeom {
@@ -47,7 +51,7 @@ inline SymGeom sym_geom(int64_t M) {
   g.M = M;
   g.nG = (int)((M + kSymG - 1) / kSymG);
   g.nQ = (g.nG + kSymQ - 1) / kSymQ;
-  g.L = kSymL;
+  g.L = sym_L();
   g.Kmax = (g.nG + g.L - 1) / g.L;
   g.nslot = g.nQ + 1 + g.Kmax;
   return g;
@@ -64,13 +68,16 @@ struct SymBwd {
   static constexpr int CW = cw4(5 * D);  // float4 planes per column record
   static constexpr int W = 2 * D;        // accumulators per point: gp / s1 (D), gq / s (D)
 
-  // Per-row state (scaled coordinates as OpOdeSelfBwd2, plus a / s1 for the column side).
+  // Accumulator units: gp / alpha and gq / s (alpha = coordinate scale, s = 1/sigma^2):
+  //   gp_i / alpha = sum_j K (ia_a_j - gt z) + (c K zb) p_j,   ia_a = a / alpha,
+  //   gt = gam s1 / alpha, c = s1 / alpha (s1 = s / alpha), and iap = ia_a_i.p_j + ia_a_j.p_i,
+  // which keeps the row state at 5 D floats (q', p, b, a / alpha, gam p).
   struct Row {
-    float q[D], p[D], b[D], ia_a[D], sia_p[D], gp[D], ap[D];
+    float q[D], p[D], b[D], ia_a[D], gp[D];
   };
 
   __device__ static void load_row(const Args& a, const Scal& sc, int64_t i, bool valid, Row& r) {
-    const float ia = 1.0f / a.scale, sia = sc.aux1 * ia, is1 = 1.0f / sc.aux1, gam = sc.aux0;
+    const float ia = 1.0f / a.scale, gam = sc.aux0;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float q = valid ? a.r0[i * D + d] : 0.f;
@@ -81,15 +88,13 @@ struct SymBwd {
       r.p[d] = p;
       r.b[d] = b;
       r.ia_a[d] = ia * av;
-      r.sia_p[d] = sia * p;
       r.gp[d] = gam * p;
-      r.ap[d] = is1 * av;
     }
   }
 
-  // column record: q' (D), p (D), a / s1 (D), b (D), gam p (D)
+  // column record: q' (D), p (D), a / alpha (D), b (D), gam p (D)
   __device__ static void load_col(const Args& a, const Scal& sc, int64_t j, bool valid, float* rec) {
-    const float is1 = 1.0f / sc.aux1, gam = sc.aux0;
+    const float ia = 1.0f / a.scale, gam = sc.aux0;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float q = valid ? a.c0[j * D + d] : 0.f;
@@ -98,7 +103,7 @@ struct SymBwd {
       const float b = valid ? a.c3[j * D + d] : 0.f;
       rec[d] = valid ? a.scale * q : kFar;
       rec[D + d] = p;
-      rec[2 * D + d] = is1 * av;
+      rec[2 * D + d] = ia * av;
       rec[3 * D + d] = b;
       rec[4 * D + d] = gam * p;
     }
@@ -106,10 +111,15 @@ struct SymBwd {
     for (int k = 5 * D; k < 4 * CW; ++k) rec[k] = 0.f;
   }
 
-  // ordered pair (i, j), row side only (== OpOdeSelfBwd2::pair)
-  __device__ static void pair_row(float gam, const Row& r, const float* rec, float* acc) {
-    float z[D], db[D], u[D];
-    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
+  struct Shared {
+    float z[D], u[D];
+    float K, w, cKzb;
+  };
+
+  // the pair quantities common to (i, j) and (j, i) (sign of z, u as seen from row i)
+  __device__ static void shared_terms(float c, const Row& r, const float* rec, Shared& t) {
+    float db[D];
+    t.K = fast_exp2(-diff_sq<D>(r.q, rec, t.z));
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
     const float* bj = rec + 3 * D;
@@ -118,49 +128,45 @@ struct SymBwd {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       db[d] = r.b[d] - bj[d];
-      u[d] = fmaf(-pp, db[d], r.gp[d] - gpj[d]);
+      t.u[d] = fmaf(-pp, db[d], r.gp[d] - gpj[d]);
     }
-    const float zu = dot<D>(z, u);
-    const float zb = dot<D>(z, db);
-    const float iap = dot<D>(r.ia_a, pj) + dot<D>(aj, r.sia_p);
-    const float w = fmaf(kS2, zu, -iap);
-    const float Kzb = K * zb;
+    const float zu = dot<D>(t.z, t.u);
+    const float zb = dot<D>(t.z, db);
+    const float iap = dot<D>(r.ia_a, pj) + dot<D>(aj, r.p);
+    t.w = fmaf(kS2, zu, -iap);
+    t.cKzb = (c * zb) * t.K;
+  }
+
+  // ordered pair (i, j), row side only
+  __device__ static void pair_row(float gt, float c, const Row& r, const float* rec, float* acc) {
+    Shared t;
+    shared_terms(c, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      acc[d] = fmaf(Kzb, pj[d], fmaf(K, fmaf(-gam, z[d], aj[d]), acc[d]));
-      acc[D + d] = fmaf(K, fmaf(w, z[d], -u[d]), acc[D + d]);
+      acc[d] = fmaf(t.cKzb, pj[d], fmaf(t.K, fmaf(-gt, t.z[d], aj[d]), acc[d]));  // gp_i / alpha
+      acc[D + d] = fmaf(t.K, fmaf(t.w, t.z[d], -t.u[d]), acc[D + d]);            // gq_i / s
     }
   }
 
   // unordered pair {i, j}: row side into acc, column side (the (j, i) terms) into ct
   // (FIRST: ct is initialised instead of accumulated).
   template <bool FIRST>
-  __device__ static void pair_sym(float gam, const Row& r, const float* rec, float* acc, float* ct) {
-    float z[D], db[D], u[D];
-    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
+  __device__ static void pair_sym(float gt, float c, const Row& r, const float* rec, float* acc,
+                                  float* ct) {
+    Shared t;
+    shared_terms(c, r, rec, t);
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
-    const float* bj = rec + 3 * D;
-    const float* gpj = rec + 4 * D;
-    const float pp = dot<D>(r.p, pj);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      db[d] = r.b[d] - bj[d];
-      u[d] = fmaf(-pp, db[d], r.gp[d] - gpj[d]);
-    }
-    const float zu = dot<D>(z, u);
-    const float zb = dot<D>(z, db);
-    const float iap = dot<D>(r.ia_a, pj) + dot<D>(aj, r.sia_p);
-    const float w = fmaf(kS2, zu, -iap);
-    const float Kzb = K * zb;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float e = fmaf(w, z[d], -u[d]);
-      acc[d] = fmaf(Kzb, pj[d], fmaf(K, fmaf(-gam, z[d], aj[d]), acc[d]));  // gp_i / s1
-      acc[D + d] = fmaf(K, e, acc[D + d]);                                   // gq_i / s
-      const float t = fmaf(gam, z[d], r.ap[d]);                              // a_i/s1 + gam z
-      ct[d] = fmaf(Kzb, r.p[d], FIRST ? K * t : fmaf(K, t, ct[d]));          // gp_j / s1
-      ct[D + d] = FIRST ? -K * e : fmaf(-K, e, ct[D + d]);                   // gq_j / s
+      const float e = fmaf(t.w, t.z[d], -t.u[d]);
+      acc[d] = fmaf(t.cKzb, pj[d], fmaf(t.K, fmaf(-gt, t.z[d], aj[d]), acc[d]));  // gp_i / alpha
+      acc[D + d] = fmaf(t.K, e, acc[D + d]);                                       // gq_i / s
+      const float tt = fmaf(gt, t.z[d], r.ia_a[d]);                                // (j,i): z -> -z
+      ct[d] = fmaf(t.cKzb, r.p[d], FIRST ? t.K * tt : fmaf(t.K, tt, ct[d]));       // gp_j / alpha
+      ct[D + d] = FIRST ? -t.K * e : fmaf(-t.K, e, ct[D + d]);                     // gq_j / s
     }
   }
 };
@@ -172,14 +178,23 @@ __device__ __forceinline__ float rol1(float x) {
 
 // slab layout: slab[slot][row][W]
 template <int D>
-__global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+#ifndef DICP_SYM_WAVES
+#define DICP_SYM_WAVES 0  // no occupancy hint: waves_per_eu(5) (91 VGPRs) measured 16% slower
+#endif
+#if DICP_SYM_WAVES > 0
+#define DICP_SYM_ATTR __attribute__((amdgpu_waves_per_eu(DICP_SYM_WAVES)))
+#else
+#define DICP_SYM_ATTR
+#endif
+__global__ __launch_bounds__(256) DICP_SYM_ATTR void sym_bwd_kernel(Args a, Scal sc, int64_t M, int nG, int L,
                                                       float* __restrict__ slab, int64_t slot_stride) {
   using S = SymBwd<D>;
   constexpr int CW = S::CW, W = S::W;
   __shared__ float4 planes[2][CW][kSymG];
   __shared__ float colacc[kSymQ][kSymG][W];
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
-  const float gam = sc.aux0;
+  const float cs = sc.aux1 / a.scale;    // s1 / alpha
+  const float gt = sc.aux0 * cs;         // gam s1 / alpha
 
   const int Q = blockIdx.y, kc = blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
@@ -229,19 +244,19 @@ __global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M
       if (sym) {
 #pragma unroll 2
         for (int k2 = 0; k2 < 64; ++k2) {
-          const int c = h * 64 + ((l + k2) & 63);
+          const int col = h * 64 + ((l + k2) & 63);
           float rec[4 * CW];
 #pragma unroll
           for (int m = 0; m < CW; ++m) {
-            const float4 v = planes[buf][m][c];
+            const float4 v = planes[buf][m][col];
             rec[4 * m] = v.x;
             rec[4 * m + 1] = v.y;
             rec[4 * m + 2] = v.z;
             rec[4 * m + 3] = v.w;
           }
           float ct[W];
-          S::template pair_sym<true>(gam, row[0], rec, racc[0], ct);
-          S::template pair_sym<false>(gam, row[1], rec, racc[1], ct);
+          S::template pair_sym<true>(gt, cs, row[0], rec, racc[0], ct);
+          S::template pair_sym<false>(gt, cs, row[1], rec, racc[1], ct);
           // cacc belonged to column (l + k2 - 1); bring column (l + k2)'s sum to this lane
 #pragma unroll
           for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
@@ -252,18 +267,18 @@ __global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M
       } else if (diag) {
 #pragma unroll 2
         for (int k2 = 0; k2 < 64; ++k2) {
-          const int c = h * 64 + ((l + k2) & 63);
+          const int col = h * 64 + ((l + k2) & 63);
           float rec[4 * CW];
 #pragma unroll
           for (int m = 0; m < CW; ++m) {
-            const float4 v = planes[buf][m][c];
+            const float4 v = planes[buf][m][col];
             rec[4 * m] = v.x;
             rec[4 * m + 1] = v.y;
             rec[4 * m + 2] = v.z;
             rec[4 * m + 3] = v.w;
           }
-          S::pair_row(gam, row[0], rec, racc[0]);
-          S::pair_row(gam, row[1], rec, racc[1]);
+          S::pair_row(gt, cs, row[0], rec, racc[0]);
+          S::pair_row(gt, cs, row[1], rec, racc[1]);
         }
       }
 #pragma unroll
@@ -292,11 +307,11 @@ __global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M
   }
 }
 
-// out0 = gq = s * sum(gq/s), out1 = gp = s1 * sum(gp/s1), with the Outs epilogue.
+// out0 = gq = s * sum(gq/s), out1 = gp = alpha * sum(gp/alpha), with the Outs epilogue.
 template <int D>
 __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
                                                         int64_t slot_stride, int64_t M, int nG,
-                                                        int L, float s, float s1, Outs o) {
+                                                        int L, float s, float alpha, Outs o) {
   constexpr int W = 2 * D;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= M * W) return;
@@ -307,7 +322,7 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
   for (int t = 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
   if (c < D) {
     const int64_t idx = row * D + c;
-    o.ptr[1][idx] = epilogue(o, 1, idx, s1 * acc);
+    o.ptr[1][idx] = epilogue(o, 1, idx, alpha * acc);
   } else {
     const int64_t idx = row * D + (c - D);
     o.ptr[0][idx] = epilogue(o, 0, idx, s * acc);
@@ -342,7 +357,7 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   if (rc) return rc;
   const int64_t n = M * 2 * D;
   sym_merge_kernel<D><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-      slab, stride, M, g.nG, g.L, sc.s, sc.aux1, o);
+      slab, stride, M, g.nG, g.L, sc.s, a.scale, o);
   return check_launch("ode_self_bwd(sym merge)");
 }
 

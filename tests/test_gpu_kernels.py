@@ -198,7 +198,7 @@ def test_dpp_wave_rol_semantics(dev):
     assert out.cpu().tolist() == [(l + 1) % 64 for l in range(64)]
 
 
-@pytest.mark.parametrize("M", [128, 129, 1000, 5000])
+@pytest.mark.parametrize("M", [128, 129, 1000, 5000, 50000])
 def test_sym_bwd_vs_ordered(dev, M):
     """Symmetric pair-once VJP == ordered kernel (alg 1) up to fp32 summation order, incl.
     partial last groups and quads; deterministic run to run."""

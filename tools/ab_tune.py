@@ -120,7 +120,8 @@ def main():
         for alg in (0, 1):
             for r in (1, 2, 4):
                 variants.append((f"bwd_alg{alg}_r{r}", {"bwd_alg": alg, "r_bwd": r, "split_rounds": 0}, bwd))
-        variants.append(("bwd_alg2_sym", {"bwd_alg": 2, "split_rounds": 0}, bwd))
+        for L in (1, 2, 4, 8):
+            variants.append((f"bwd_alg2_sym_L{L}", {"bwd_alg": 2, "sym_L": L, "split_rounds": 0}, bwd))
         variants.append(("fwd_r2", {"r_fwd": 2, "split_rounds": 0}, fwd))
     res = {v[0]: [] for v in variants}
 
