@@ -15,9 +15,10 @@ import json
 import os
 import sys
 
-NAMES = {"OpOdeSelfBwd": "ode_self_bwd", "OpOdeSelfFwd": "ode_self_fwd", "OpGmmE": "gmm_estep",
-         "OpGmmM": "gmm_mstep", "OpGmmTargets": "gmm_targets", "merge_slabs": "merge_slabs",
-         "lse_finalize": "lse_finalize"}
+NAMES = {"sym_bwd_kernel": "ode_self_bwd", "sym_merge_kernel": "sym_merge",
+         "OpOdeSelfBwd": "ode_self_bwd_ordered", "OpOdeSelfFwd": "ode_self_fwd",
+         "OpGmmE": "gmm_estep", "OpGmmM": "gmm_mstep", "OpGmmTargets": "gmm_targets",
+         "merge_slabs": "merge_slabs", "lse_finalize": "lse_finalize"}
 
 
 def short(kname):
