@@ -57,10 +57,16 @@ def probe_peaks():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     blocks, iters = 256 * 8 * 4, 4096
     res = {}
-    for kind, name, mult in ((0, "exp2_per_s", 1), (1, "fma_flops", 2), (2, "pk_fma_flops", 4)):
+    for kind, name, mult in ((0, "exp2_per_s", 1), (1, "fma_flops", 2), (2, "pk_fma_flops", 4),
+                             (3, "dpp_wave_rol_add_per_s", 1), (4, "dpp_row_ror_add_per_s", 1),
+                             (5, "fma_flops_with_1exp_per_8fma", 2)):
         t = timed(lambda: mb.dicp_mb_launch(kind, blocks, iters, ctypes.c_void_p(out.data_ptr()), st),
                   warm=2, reps=5)
         res[name] = blocks * 256 * iters * chains * mult / t
+    # SIMD cycles per wave64 instruction at the nominal 2.4 GHz, 1024 SIMDs
+    res["cycles_per_wave_instr"] = {k: 1024 * 2.4e9 * 64 * m / res[k] for k, m in (
+        ("exp2_per_s", 1), ("fma_flops", 2), ("dpp_wave_rol_add_per_s", 1),
+        ("dpp_row_ror_add_per_s", 1))}
     return res
 
 

@@ -22,7 +22,7 @@ KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRAD
     GRADLAPKSCAL, MIN_SQDIST, MIN_SQDIST_OTHER = range(14)
 # enum dicp_ws_kind
 WS_RED, WS_ODE_SELF_FWD, WS_ODE_SELF_BWD, WS_ODE_EXT_FWD, WS_ODE_EXT_BWD, WS_GMM_ESTEP, \
-    WS_GMM_MSTEP, WS_GMM_TARGETS = range(8)
+    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG = range(9)
 
 _lock = threading.Lock()
 _lib = None
@@ -47,6 +47,7 @@ _SIGNATURES = {
     "dicp_gmm_estep_f32": [_P, _I64, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _SZ, _P],
     "dicp_gmm_mstep_f32": [_P, _P, _I64, _P, _P, _I64, _INT, _DBL, _P, _P, _SZ, _P],
     "dicp_gmm_targets_f32": [_P, _P, _I64, _P, _P, _DBL, _P, _P, _I64, _INT, _P, _P, _SZ, _P],
+    "dicp_kernel_ridge_cg_f32": [_P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _INT, _INT, _P, _SZ, _P],
     "dicp_workspace_bytes": [_INT, _I64, _I64, _INT],
     "dicp_last_error": [],
     "dicp_version": [],
@@ -78,6 +79,8 @@ def lib():
                     "`make -C diff-icp_amd/csrc`. There is no CPU fallback.")
             handle = ctypes.CDLL(LIB_PATH)
             for name, args in _SIGNATURES.items():
+                if os.environ.get("DICP_LIB_PATH") and not hasattr(handle, name):
+                    continue  # older experiment build (tools/ab_libs.py) without this entry
                 fn = getattr(handle, name)
                 fn.argtypes = args
                 fn.restype = _RESTYPES.get(name, _INT)
@@ -141,7 +144,7 @@ def _stream(device) -> ctypes.c_void_p:
 FLOPS_PER_PAIR = {
     "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 70,
     "ode_ext_fwd": 22, "ode_ext_bwd": (36 + 49) / 2, "gmm_estep": 37, "gmm_mstep": 31,
-    "gmm_targets": 32,
+    "gmm_targets": 32, "ridge_cg": 15,
 }
 
 
@@ -437,3 +440,47 @@ def gmm_targets(X, T2, mu_old, w2_old, sigma_old: float, mu_new, lpi_new):
                                     _ptr(rows), _ptr(ws), nb, _stream(X.device)))
     _check_rc(rc, "gmm_targets")
     return rows
+
+
+# ---------------------------------------------------------------------------------------
+# Kernel ridge solve (v2p)
+# ---------------------------------------------------------------------------------------
+CG_DONE_NAMES = {0: "running", 1: "converged", 2: "breakdown"}
+
+
+def kernel_ridge_cg(x, v, sigma: float, alpha: float, eps: float = 1e-6, maxiter: int = 5000,
+                    chunk: int = 32):
+    """b with (K(x,x) + alpha I) b = v by conjugate gradients on the device
+    (dicp_kernel_ridge_cg_f32; KeOps LazyTensor.solve semantics, kernel.py:239-241: one CG on
+    the flattened (M,D) system, stop when |r|^2 < M*D*eps^2).  Launches `chunk` iterations at
+    a time and reads the 16-byte device status between chunks.  Returns (b, info) with
+    info = {"status", "iterations", "residual2", "threshold"}."""
+    x = _dev(x, "x")
+    v = _dev(v, "v")
+    M, D = x.shape
+    if v.shape != x.shape:
+        raise ValueError("v must have the shape of x")
+    b = torch.zeros_like(v)
+    info = {"status": "converged", "iterations": 0, "residual2": 0.0, "threshold": 0.0}
+    if M == 0:
+        return b, info
+    ws, nb = _workspace(WS_RIDGE_CG, M, 0, D, x.device)
+    st = _stream(x.device)
+    done, it = 0, 0
+    start = 1
+    while it < maxiter:
+        n = min(int(chunk), maxiter - it)
+        rc = _launch("ridge_cg", M * M * n, 4 * (3 * M * D + 4 * M * D) * n,
+                     lambda: lib().dicp_kernel_ridge_cg_f32(_ptr(x), M, D, float(sigma), float(alpha),
+                                                            float(eps), _ptr(v), _ptr(b), start, n,
+                                                            _ptr(ws), nb, st))
+        _check_rc(rc, "kernel_ridge_cg")
+        start = 0
+        head = ws[:16].cpu()          # one 16-byte read per chunk (synchronises the stream)
+        done, it = (int(t) for t in head[:8].view(torch.int32))
+        if done:
+            break
+    rr, thr = (float(t) for t in head[8:16].view(torch.float32))
+    info = {"status": CG_DONE_NAMES.get(done, str(done)) if done else "maxiter",
+            "iterations": it, "residual2": rr, "threshold": thr}
+    return b, info

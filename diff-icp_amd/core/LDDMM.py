@@ -145,8 +145,11 @@ class LDDMMModel:
         rhs = v if self.eta == 0 else v + self.eta * self.Kernel.GradKRed(q, q)
         if version == "pinv":
             return self.Kernel.KpinvSolve(q, rhs, rcond)
-        elif version in ("ridge_keops", "ridge_pytorch", "ridge_hip"):
-            return self.Kernel.KridgeSolve(q, rhs, alpha)
+        elif version in ("ridge_keops", "ridge_hip"):
+            # device CG with the KRed mat-vec (KeOps LazyTensor.solve semantics)
+            return self.Kernel.KridgeSolve_keops(q, rhs, alpha)
+        elif version == "ridge_pytorch":
+            return self.Kernel.KridgeSolve_pytorch(q, rhs, alpha)
         raise ValueError("unknown version")
 
     def random_p(self, q, rcond=1e-3, alpha=1e-4, version="svd"):

@@ -105,6 +105,11 @@ struct has_col_s : std::false_type {};
 template <class T>
 struct has_col_s<T, std::void_t<decltype(&T::load_col_s)>> : std::true_type {};
 
+template <class T, class = void>
+struct skip_on_aux0 : std::false_type {};
+template <class T>
+struct skip_on_aux0<T, std::void_t<decltype(T::kSkipOnAux0)>> : std::bool_constant<T::kSkipOnAux0> {};
+
 template <class Op>
 __device__ __forceinline__ void op_load_row(const Args& a, const Scal& sc, int64_t i,
                                             typename Op::Row& r) {
@@ -144,6 +149,12 @@ __global__ __launch_bounds__(kBlock) DICP_KERNEL_ATTR void rowred_kernel(Args ar
   // is consumed from LDS; one barrier per tile.
   __shared__ float4 lds[2][kTile * CW4];
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];  // device-resident scalar (no host sync)
+  // ops flagged kSkipOnAux0 treat that device scalar as a "skip this launch" flag (iterative
+  // solvers launch ahead of their convergence test).  Kept out of Scal on purpose: one more
+  // kernel argument changed the register allocation of unrelated kernels (~12% on the VJP).
+  if constexpr (skip_on_aux0<Op>::value) {
+    if (sc.aux0 != 0.f) return;
+  }
 
   const int tid = threadIdx.x;
   const int64_t ibase = (int64_t)blockIdx.x * (kBlock * R) + tid;

@@ -28,6 +28,13 @@ int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd;
 // eta = 0 VJP: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48), 2 = symmetric
 // pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair)
 int g_bwd_alg = 2;
+// eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, default: measured ~3% faster on MI355X),
+// 1 = symmetric pair-once kernel (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair
+// instead of 20 + 1, but issue-stalled on its rotating column sums)
+#ifndef DICP_FWD_ALG
+#define DICP_FWD_ALG 0
+#endif
+int g_fwd_alg = DICP_FWD_ALG;
 
 template <class Op>
 int launch_r(int R, const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
@@ -97,6 +104,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
   if (!strcmp(name, "force_splits")) {
     if (value < 0 || value > 65536) return DICP_ERR_INVALID;
     force_splits() = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "fwd_alg")) {
+    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    g_fwd_alg = value;
     return DICP_OK;
   }
   if (!strcmp(name, "bwd_alg")) {
@@ -180,6 +192,9 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   scale_coords(a, sc, sigma);
   if (eta != 0.0)
     return launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
+  if (g_fwd_alg == 1)
+    return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st)
+                               : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st);
   if (o.ptr[2] != nullptr)
     return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
@@ -192,7 +207,9 @@ size_t ode_self_fwd_ws(int64_t M) {
   size_t b = ws_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), M, M);
   size_t c = ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), M, M);
   a = a > b ? a : b;
-  return a > c ? a : c;
+  a = a > c ? a : c;
+  const size_t d = sym_ws_bytes(M, 3 * D);
+  return a > d ? a : d;
 }
 
 template <int D>
@@ -425,7 +442,7 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
       size_t c = D == 2 ? ws_r<OpOdeSelfBwd2<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd2<3>>(r_bwd(), M, M);
       a = a > b ? a : b;
       a = a > c ? a : c;
-      const size_t d = sym_ws_bytes(M, D);
+      const size_t d = sym_ws_bytes(M, 2 * D);
       return a > d ? a : d;
     }
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);

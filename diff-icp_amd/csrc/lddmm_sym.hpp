@@ -35,7 +35,18 @@ inline int& sym_L() {
   static int L = 4;
   return L;
 }
-constexpr float kFar = 1.0e12f;  // padding coordinate: K = exp2(-|z|^2) = 0 against real points
+constexpr float kFar = 1.0e12f;
+// s_waitcnt lgkmcnt(0) with vmcnt / expcnt left at their maxima (gfx9 encoding)
+constexpr int kLgkm0 = 0xC07F;
+#ifndef DICP_SYM_PREFETCH
+#define DICP_SYM_PREFETCH 1
+#endif
+#ifndef DICP_SYMBWD_WAVES
+#define DICP_SYMBWD_WAVES 4
+#endif
+#ifndef DICP_SYMFWD_WAVES
+#define DICP_SYMFWD_WAVES 8
+#endif  // padding coordinate: K = exp2(-|z|^2) = 0 against real points
 
 struct SymGeom {
   int64_t M;
@@ -66,7 +77,19 @@ __host__ __device__ inline int sym_nslots(int T, int nG, int L) {
 template <int D>
 struct SymBwd {
   static constexpr int CW = cw4(5 * D);  // float4 planes per column record
+  static constexpr int kUsed = 5 * D;    // live floats of a record
   static constexpr int W = 2 * D;        // accumulators per point: gp / s1 (D), gq / s (D)
+  // occupancy cap: at <= 4 waves/SIMD the compiler keeps ~127 VGPRs and more pairs in
+  // flight per wave; the 5-wave allocation (94 VGPRs) measured ~10% slower on MI355X
+  static constexpr int kMaxWaves = DICP_SYMBWD_WAVES;
+
+  struct Prm {
+    float gt, c;  // gam s1 / alpha, s1 / alpha
+  };
+  __device__ static Prm params(const Args& a, const Scal& sc) {
+    const float cs = sc.aux1 / a.scale;
+    return Prm{sc.aux0 * cs, cs};
+  }
 
   // Accumulator units: gp / alpha and gq / s (alpha = coordinate scale, s = 1/sigma^2):
   //   gp_i / alpha = sum_j K (ia_a_j - gt z) + (c K zb) p_j,   ia_a = a / alpha,
@@ -138,9 +161,10 @@ struct SymBwd {
   }
 
   // ordered pair (i, j), row side only
-  __device__ static void pair_row(float gt, float c, const Row& r, const float* rec, float* acc) {
+  __device__ static void pair_row(const Prm& prm, const Row& r, const float* rec, float* acc) {
+    const float gt = prm.gt;
     Shared t;
-    shared_terms(c, r, rec, t);
+    shared_terms(prm.c, r, rec, t);
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
 #pragma unroll
@@ -153,10 +177,11 @@ struct SymBwd {
   // unordered pair {i, j}: row side into acc, column side (the (j, i) terms) into ct
   // (FIRST: ct is initialised instead of accumulated).
   template <bool FIRST>
-  __device__ static void pair_sym(float gt, float c, const Row& r, const float* rec, float* acc,
+  __device__ static void pair_sym(const Prm& prm, const Row& r, const float* rec, float* acc,
                                   float* ct) {
+    const float gt = prm.gt;
     Shared t;
-    shared_terms(c, r, rec, t);
+    shared_terms(prm.c, r, rec, t);
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
 #pragma unroll
@@ -171,22 +196,82 @@ struct SymBwd {
   }
 };
 
+// Symmetric (pair-once) fused ODE forward, eta = 0 (classic / hybrid models): per point
+//   V_i = sum_j K p_j,  Gs_i = sum_j K (p_i.p_j) z'_ij,  Z_i = sum_j K z'_ij  (z' = alpha z),
+// the accumulators of OpOdeSelfFwd<D, false, DIV> (lddmm_ops.hpp).  K and p_i.p_j are
+// symmetric, z' flips sign, so the column side of an unordered pair is
+//   V_j += K p_i,  Gs_j -= K pp z',  Z_j -= K z'.
+// The merge turns them into v = V, mG = (s/alpha) Gs, g = -(s/alpha) p.Z, h = p.V / 2.
+template <int D, bool DIV>
+struct SymFwd {
+  static constexpr int kMaxWaves = DICP_SYMFWD_WAVES;
+  static constexpr int CW = cw4(2 * D);
+  static constexpr int kUsed = 2 * D;
+  static constexpr int W = DIV ? 3 * D : 2 * D;
+  struct Prm {};
+  __device__ static Prm params(const Args&, const Scal&) { return Prm{}; }
+  struct Row {
+    float q[D], p[D];
+  };
+  __device__ static void load_row(const Args& a, const Scal&, int64_t i, bool valid, Row& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      r.q[d] = valid ? a.scale * a.r0[i * D + d] : kFar;
+      r.p[d] = valid ? a.r1[i * D + d] : 0.f;
+    }
+  }
+  __device__ static void load_col(const Args& a, const Scal&, int64_t j, bool valid, float* rec) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      rec[d] = valid ? a.scale * a.c0[j * D + d] : kFar;
+      rec[D + d] = valid ? a.c1[j * D + d] : 0.f;
+    }
+#pragma unroll
+    for (int k = 2 * D; k < 4 * CW; ++k) rec[k] = 0.f;
+  }
+  __device__ static void pair_row(const Prm&, const Row& r, const float* rec, float* acc) {
+    float z[D];
+    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
+    const float* pj = rec + D;
+    const float Kpp = K * dot<D>(r.p, pj);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, pj[d], acc[d]);
+      acc[D + d] = fmaf(Kpp, z[d], acc[D + d]);
+      if (DIV) acc[2 * D + d] = fmaf(K, z[d], acc[2 * D + d]);
+    }
+  }
+  template <bool FIRST>
+  __device__ static void pair_sym(const Prm&, const Row& r, const float* rec, float* acc, float* ct) {
+    float z[D];
+    const float K = fast_exp2(-diff_sq<D>(r.q, rec, z));
+    const float* pj = rec + D;
+    const float Kpp = K * dot<D>(r.p, pj);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = fmaf(K, pj[d], acc[d]);
+      acc[D + d] = fmaf(Kpp, z[d], acc[D + d]);
+      ct[d] = FIRST ? K * r.p[d] : fmaf(K, r.p[d], ct[d]);
+      ct[D + d] = FIRST ? -Kpp * z[d] : fmaf(-Kpp, z[d], ct[D + d]);
+      if (DIV) {
+        acc[2 * D + d] = fmaf(K, z[d], acc[2 * D + d]);
+        ct[2 * D + d] = FIRST ? -K * z[d] : fmaf(-K, z[d], ct[2 * D + d]);
+      }
+    }
+  }
+};
+
 __device__ __forceinline__ float rol1(float x) {
   // wave_rol:1 -- lane l receives lane (l + 1) mod 64
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x134, 0xF, 0xF, false));
 }
 
 // slab layout: slab[slot][row][W]
+// The VJP keeps its own kernel body (the generic sym_kernel below compiles the SAME pair
+// algebra into a schedule measured ~12% slower on MI355X: the hipcc schedule of this loop is
+// sensitive to the surrounding code, so this instance is kept as first tuned).
 template <int D>
-#ifndef DICP_SYM_WAVES
-#define DICP_SYM_WAVES 0  // no occupancy hint: waves_per_eu(5) (91 VGPRs) measured 16% slower
-#endif
-#if DICP_SYM_WAVES > 0
-#define DICP_SYM_ATTR __attribute__((amdgpu_waves_per_eu(DICP_SYM_WAVES)))
-#else
-#define DICP_SYM_ATTR
-#endif
-__global__ __launch_bounds__(256) DICP_SYM_ATTR void sym_bwd_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+__global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M, int nG, int L,
                                                       float* __restrict__ slab, int64_t slot_stride) {
   using S = SymBwd<D>;
   constexpr int CW = S::CW, W = S::W;
@@ -195,6 +280,7 @@ __global__ __launch_bounds__(256) DICP_SYM_ATTR void sym_bwd_kernel(Args a, Scal
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
   const float cs = sc.aux1 / a.scale;    // s1 / alpha
   const float gt = sc.aux0 * cs;         // gam s1 / alpha
+  const typename S::Prm prm{gt, cs};
 
   const int Q = blockIdx.y, kc = blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
@@ -255,8 +341,8 @@ __global__ __launch_bounds__(256) DICP_SYM_ATTR void sym_bwd_kernel(Args a, Scal
             rec[4 * m + 3] = v.w;
           }
           float ct[W];
-          S::template pair_sym<true>(gt, cs, row[0], rec, racc[0], ct);
-          S::template pair_sym<false>(gt, cs, row[1], rec, racc[1], ct);
+          S::template pair_sym<true>(prm, row[0], rec, racc[0], ct);
+          S::template pair_sym<false>(prm, row[1], rec, racc[1], ct);
           // cacc belonged to column (l + k2 - 1); bring column (l + k2)'s sum to this lane
 #pragma unroll
           for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
@@ -277,8 +363,167 @@ __global__ __launch_bounds__(256) DICP_SYM_ATTR void sym_bwd_kernel(Args a, Scal
             rec[4 * m + 2] = v.z;
             rec[4 * m + 3] = v.w;
           }
-          S::pair_row(gt, cs, row[0], rec, racc[0]);
-          S::pair_row(gt, cs, row[1], rec, racc[1]);
+          S::pair_row(prm, row[0], rec, racc[0]);
+          S::pair_row(prm, row[1], rec, racc[1]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) colacc[wv][h * 64 + l][k] = cacc[k];
+    }
+    __syncthreads();
+    if (tid < kSymG) {
+      const int64_t j = (int64_t)B * kSymG + tid;
+      if (j < M) {
+        float* dst = slab + (int64_t)Q * slot_stride + j * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+          dst[k] = ((colacc[0][tid][k] + colacc[1][tid][k]) + colacc[2][tid][k]) + colacc[3][tid][k];
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  // row sums of this workgroup's column chunk -> slot Q + 1 + kc of group A
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (!rv[r]) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = racc[r][k];
+  }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxWaves))) void sym_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+                                                  float* __restrict__ slab, int64_t slot_stride) {
+  constexpr int CW = S::CW, W = S::W;
+  __shared__ float4 planes[2][CW][kSymG];
+  __shared__ float colacc[kSymQ][kSymG][W];
+  if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
+  const typename S::Prm prm = S::params(a, sc);
+
+  const int Q = blockIdx.y, kc = blockIdx.x;
+  const int B0 = kSymQ * Q + kc * L;
+  if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
+  const int B1 = min(B0 + L, nG);
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int A = kSymQ * Q + wv;
+
+  typename S::Row row[2];
+  int64_t ri[2];
+  bool rv[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    ri[r] = (int64_t)A * kSymG + r * 64 + l;
+    rv[r] = A < nG && ri[r] < M;
+    S::load_row(a, sc, rv[r] ? ri[r] : 0, rv[r], row[r]);
+  }
+  float racc[2][W];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int k = 0; k < W; ++k) racc[r][k] = 0.f;
+
+  auto stage = [&](int B, int buf) {
+    if (tid < kSymG) {
+      const int64_t j = (int64_t)B * kSymG + tid;
+      float rec[4 * CW];
+      S::load_col(a, sc, j < M ? j : 0, j < M, rec);
+#pragma unroll
+      for (int m = 0; m < CW; ++m)
+        planes[buf][m][tid] = make_float4(rec[4 * m], rec[4 * m + 1], rec[4 * m + 2], rec[4 * m + 3]);
+    }
+  };
+
+  int buf = 0;
+  // read a column record; only the S::kUsed live floats (a dead padding lane read into a
+  // register would be a WAW hazard the waitcnt pass resolves by waiting on the read)
+  auto ldrec = [&](int col, float* rec) {
+    constexpr int kLast = S::kUsed - 4 * (CW - 1);  // live floats of the last plane (1..4)
+#pragma unroll
+    for (int m = 0; m < CW; ++m) {
+      const float* src = reinterpret_cast<const float*>(&planes[buf][m][col]);
+      if (m < CW - 1 || kLast == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = v.z, rec[4 * m + 3] = v.w;
+      } else if (kLast == 3) {
+        const float3 v = *reinterpret_cast<const float3*>(src);
+        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = v.z, rec[4 * m + 3] = 0.f;
+      } else if (kLast == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = rec[4 * m + 3] = 0.f;
+      } else {
+        rec[4 * m] = src[0], rec[4 * m + 1] = rec[4 * m + 2] = rec[4 * m + 3] = 0.f;
+      }
+    }
+  };
+  stage(B0, 0);
+  __syncthreads();
+  for (int B = B0; B < B1; ++B) {
+    if (B + 1 < B1) stage(B + 1, buf ^ 1);
+    const bool sym = A < B;          // wave-uniform
+    const bool diag = A == B;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float cacc[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+      if (sym) {
+#if DICP_SYM_PREFETCH
+        // register double-buffer: the record of step k2 + 1 is read from LDS while step k2
+        // computes, so the LDS latency is not exposed once per step (the compiler's own
+        // schedule varies between builds: waits right after the reads cost ~13% on the VJP)
+        float rec[4 * CW];
+        ldrec(h * 64 + (l & 63), rec);
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          float nxt[4 * CW];
+          // this step's record was read one step ago: wait for it here (no stall), then
+          // issue the next reads and pin them at the top (the compiler otherwise sinks
+          // them next to their use and waits on them right away)
+          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          ldrec(h * 64 + ((l + k2 + 1) & 63), nxt);  // k2 = 63 wraps to column l: harmless
+          __builtin_amdgcn_sched_barrier(0);
+          float ct[W];
+          S::template pair_sym<true>(prm, row[0], rec, racc[0], ct);
+          S::template pair_sym<false>(prm, row[1], rec, racc[1], ct);
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+#pragma unroll
+          for (int k = 0; k < 4 * CW; ++k) rec[k] = nxt[k];
+        }
+#else
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW];
+          ldrec(col, rec);
+          float ct[W];
+          S::template pair_sym<true>(prm, row[0], rec, racc[0], ct);
+          S::template pair_sym<false>(prm, row[1], rec, racc[1], ct);
+          // cacc belonged to column (l + k2 - 1); bring column (l + k2)'s sum to this lane
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+        }
+#endif
+        // lane l holds column (l + 63) & 63; one more rotation aligns lane l with column l
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+      } else if (diag) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW];
+#pragma unroll
+          for (int m = 0; m < CW; ++m) {
+            const float4 v = planes[buf][m][col];
+            rec[4 * m] = v.x;
+            rec[4 * m + 1] = v.y;
+            rec[4 * m + 2] = v.z;
+            rec[4 * m + 3] = v.w;
+          }
+          S::pair_row(prm, row[0], rec, racc[0]);
+          S::pair_row(prm, row[1], rec, racc[1]);
         }
       }
 #pragma unroll
@@ -329,10 +574,70 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
   }
 }
 
-inline size_t sym_ws_bytes(int64_t M, int D) {
+// W = accumulators per point (SymBwd: 2D, SymFwd: 3D with the divergence, else 2D)
+inline size_t sym_ws_bytes(int64_t M, int W) {
   if (M <= 0) return 0;
   const SymGeom g = sym_geom(M);
-  return (size_t)g.nslot * (size_t)M * (size_t)(2 * D) * sizeof(float);
+  return (size_t)g.nslot * (size_t)M * (size_t)W * sizeof(float);
+}
+
+// Forward merge: one thread per row sums its slots (slot order) and applies the epilogue to
+// v = V, mG = sa Gs, g = -sa p.Z, h = p.V / 2 (null outputs skipped).
+template <int D, bool DIV>
+__global__ __launch_bounds__(256) void sym_fwd_merge_kernel(const float* __restrict__ slab,
+                                                            int64_t slot_stride, int64_t M, int nG,
+                                                            int L, const float* __restrict__ p,
+                                                            float sa, Outs o) {
+  constexpr int W = SymFwd<D, DIV>::W;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M) return;
+  const int ns = sym_nslots((int)(i / kSymG), nG, L);
+  float t[W];
+  const float* src = slab + i * W;
+#pragma unroll
+  for (int k = 0; k < W; ++k) t[k] = src[k];
+  for (int u = 1; u < ns; ++u) {
+    const float* s2 = src + (int64_t)u * slot_stride;
+#pragma unroll
+    for (int k = 0; k < W; ++k) t[k] += s2[k];
+  }
+  float pv = 0.f, pz = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float pd = p[i * D + d];
+    pv = fmaf(pd, t[d], pv);
+    if (DIV) pz = fmaf(pd, t[2 * D + d], pz);
+    o.ptr[0][i * D + d] = epilogue(o, 0, i * D + d, t[d]);
+    o.ptr[1][i * D + d] = epilogue(o, 1, i * D + d, sa * t[D + d]);
+  }
+  if (o.ptr[2]) o.ptr[2][i] = epilogue(o, 2, i, DIV ? -sa * pz : 0.f);
+  if (o.ptr[3]) o.ptr[3][i] = epilogue(o, 3, i, 0.5f * pv);
+}
+
+template <int D, bool DIV>
+int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                   hipStream_t st) {
+  using S = SymFwd<D, DIV>;
+  if (M <= 0) return DICP_OK;
+  const SymGeom g = sym_geom(M);
+  const size_t need = sym_ws_bytes(M, S::W);
+  if (ws == nullptr || wsb < need) {
+    set_error("ode_self_fwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  if (o.ptr[0] == nullptr || o.ptr[1] == nullptr) {
+    set_error("ode_self_fwd(sym): v and mG outputs are required");
+    return DICP_ERR_INVALID;
+  }
+  float* slab = reinterpret_cast<float*>(ws);
+  const int64_t stride = M * S::W;
+  sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
+                                                                              slab, stride);
+  int rc = check_launch("ode_self_fwd(sym)");
+  if (rc) return rc;
+  sym_fwd_merge_kernel<D, DIV><<<dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st>>>(
+      slab, stride, M, g.nG, g.L, a.r1, sc.aux1, o);
+  return check_launch("ode_self_fwd(sym merge)");
 }
 
 template <int D>
@@ -340,7 +645,7 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
                    hipStream_t st) {
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M);
-  const size_t need = sym_ws_bytes(M, D);
+  const size_t need = sym_ws_bytes(M, 2 * D);
   if (ws == nullptr || wsb < need) {
     set_error("ode_self_bwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
     return DICP_ERR_WORKSPACE;

@@ -62,6 +62,48 @@ __global__ __launch_bounds__(256) void pkfma_probe(float* out, int iters, float 
   if (s == 12345.f) out[threadIdx.x] = s;
 }
 
+// DPP-add throughput: a[k] = dpp(a[k]) + b[k] on kChains independent chains
+// (CTRL 0x134 = wave_rol:1, 0x121 = row_ror:1).
+template <int CTRL>
+__global__ __launch_bounds__(256) void dppadd_probe(float* out, int iters, float seed) {
+  float a[kChains], b[kChains];
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) {
+    a[k] = seed * (threadIdx.x + k);
+    b[k] = seed * 0.5f + k;
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k)
+      a[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a[k]), CTRL, 0xF, 0xF, false)) + b[k];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) s += a[k];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
+// Co-issue probe: per iteration kChains FMAs and ONE exp2 on an independent chain; compare
+// its time with fma_probe (same FMAs, no exp) and exp_probe.
+__global__ __launch_bounds__(256) void mix_probe(float* out, int iters, float seed) {
+  float a[kChains], b[kChains];
+  float e = seed * threadIdx.x * 1e-7f;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) {
+    a[k] = seed * (threadIdx.x + k);
+    b[k] = seed * 0.5f + k;
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k) a[k] = fmaf(a[k], b[k], 0.999f);
+    e = __builtin_amdgcn_exp2f(e) - 1.0f;
+  }
+  float s = e;
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) s += a[k];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
 template <int CTRL>
 __global__ __launch_bounds__(64) void dpp_probe(int* out) {
   const int l = threadIdx.x;
@@ -79,14 +121,18 @@ extern "C" int dicp_mb_dpp(int which, int* out, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-// kind: 0 = exp2, 1 = fma, 2 = pk_fma.  Returns 0 on success.  ops per launch:
+// kind: 0 = exp2, 1 = fma, 2 = pk_fma, 3 = dpp(wave_rol:1)+add, 4 = dpp(row_ror:1)+add,
+// 5 = kChains fma + 1 exp2 per iteration.  Returns 0 on success.  ops per launch:
 // blocks*256*iters*kChains (x2 lanes for pk_fma).
 extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 g(blocks), b(256);
   if (kind == 0) exp_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 1) fma_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
-  else pkfma_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 2) pkfma_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 3) dppadd_probe<0x134><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 4) dppadd_probe<0x121><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else mix_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

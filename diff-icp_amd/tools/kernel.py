@@ -211,13 +211,29 @@ class GenKernel:
         b = Vh.t() @ (Sinv[:, None] * (U.t() @ v.double()))
         return b.to(**spec).contiguous()
 
-    def KridgeSolve(self, x, v, alpha=1e-4):
+    def KridgeSolve_torch(self, x, v, alpha=1e-4):
+        """Dense ridge solve (K + alpha I) b = v (kernel.py:234-237), on the device."""
         K = self.K_torch(x, x)
         return torch.linalg.solve(K + alpha * torch.eye(K.shape[0], dtype=K.dtype, device=K.device), v)
 
-    KridgeSolve_torch = KridgeSolve
-    KridgeSolve_pytorch = KridgeSolve   # LDDMM.py:251 calls this (missing in the reference)
-    KridgeSolve_keops = KridgeSolve
+    KridgeSolve_pytorch = KridgeSolve_torch   # LDDMM.py:251 calls this (missing in the reference)
+
+    # KeOps-style iterative ridge solve (kernel.py:239-241: LazyTensor.solve = conjugate
+    # gradients with the kernel mat-vec): HIP CG with the KRed reduction, O(M) memory, so it
+    # scales to the 50k-200k support sets where the dense solves cannot run.
+    cg_eps = 1e-6
+    cg_maxiter = 5000
+
+    def KridgeSolve_keops(self, x, v, alpha=1e-4):
+        getspec(x, v)
+        b, info = _lib.kernel_ridge_cg(x.detach(), v.detach(), self.sigma, alpha,
+                                       eps=self.cg_eps, maxiter=self.cg_maxiter)
+        self.last_solve_info = info
+        if info["status"] != "converged":
+            warnings.warn(f"KridgeSolve_keops: CG stopped ({info})")
+        return b
+
+    KridgeSolve = KridgeSolve_keops
 
 
 class GaussKernel(GenKernel):

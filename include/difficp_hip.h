@@ -176,13 +176,30 @@ int dicp_gmm_targets_f32(const float* X, const float* T2, int64_t N, const float
                          const float* lpi_new, int64_t C, int D, float* rows, void* ws,
                          size_t ws_bytes, dicp_stream_t stream);
 
+/* ------------------------------------------------------------------------------------
+ * Momenta from speeds (LDDMMModel.v2p, LDDMM.py:235-253): ridge solve
+ *   (K(x,x) + alpha I) b = v,   x (M,D), v, b (M,D)
+ * by conjugate gradients with the KRed reduction as mat-vec.  Replaces KridgeSolve_keops
+ * (kernel.py:239-241: KeOps LazyTensor.solve, i.e. CG on the flattened (M,D) system with the
+ * stopping rule |r|^2 < M*D*eps^2) and KridgeSolve_torch (kernel.py:234-237, dense solve).
+ * start = 1 initialises (b = 0, r = v); each call then launches `iters` CG iterations,
+ * stream-ordered, without synchronising the host; iterations after convergence are no-ops
+ * (device flag).  Call again with start = 0 to continue.  The first 16 bytes of `ws` hold the
+ * solver status { int32 done (0 running, 1 converged, 2 breakdown), int32 iterations,
+ * float |r|^2, float threshold }, which the caller reads between chunks.
+ * Workspace kind DICP_WS_RIDGE_CG (the state must persist across calls: same ws). */
+int dicp_kernel_ridge_cg_f32(const float* x, int64_t M, int D, double sigma, double alpha,
+                             double eps, const float* v, float* b, int start, int iters,
+                             void* ws, size_t ws_bytes, dicp_stream_t stream);
+
 /* ------------------------------------------------------------------------------------ */
 /* Scratch bytes needed by entry `kind` (one of the DICP_WS_* below) at these sizes.
  * LDDMM kinds: M = support points, N = columns (RED) or external points (EXT).
  * GMM kinds: M = data points N, N = components C. */
 enum dicp_ws_kind {
   DICP_WS_RED = 0, DICP_WS_ODE_SELF_FWD = 1, DICP_WS_ODE_SELF_BWD = 2, DICP_WS_ODE_EXT_FWD = 3,
-  DICP_WS_ODE_EXT_BWD = 4, DICP_WS_GMM_ESTEP = 5, DICP_WS_GMM_MSTEP = 6, DICP_WS_GMM_TARGETS = 7
+  DICP_WS_ODE_EXT_BWD = 4, DICP_WS_GMM_ESTEP = 5, DICP_WS_GMM_MSTEP = 6, DICP_WS_GMM_TARGETS = 7,
+  DICP_WS_RIDGE_CG = 8 /* M = points, N unused */
 };
 size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D);
 

@@ -139,6 +139,39 @@ def decimate(x, R):                                   # point_sets.py:102-133, r
 # ---------------------------------------------------------------------------------------
 # LDDMM (diffICP/core/LDDMM.py:100-227, 286-334)
 # ---------------------------------------------------------------------------------------
+def KridgeSolve_torch(x, v, sigma, alpha):            # kernel.py:234-237 (dense ridge)
+    Kxx = K(x, x, sigma)
+    return torch.linalg.solve(Kxx + alpha * torch.eye(Kxx.shape[0], dtype=Kxx.dtype), v)
+
+
+def KridgeSolve_cg(x, v, sigma, alpha, eps=1e-6, maxiter=100000):
+    """kernel.py:239-241 KridgeSolve_keops = K_keops(Vi(x),Vj(x)).solve(Vi(v), alpha).  The
+    algorithm lives in the third-party pykeops (absent here, no pinned version, setup.py:3-10):
+    its published ConjugateGradientSolver runs ONE CG on the flattened (M,D) system with
+    linop(p) = K p + alpha p and stops when |r|^2 < size(v) * eps^2.  Restated as written;
+    returns (b, iterations)."""
+    delta = v.numel() * eps ** 2
+    r = v.clone()
+    nr2 = (r ** 2).sum()
+    if nr2 < delta:
+        return 0 * r, 0
+    a = torch.zeros_like(v)
+    p = r.clone()
+    k = 0
+    while k < maxiter:
+        Mp = KRed(x, x, p, sigma) + alpha * p
+        alp = nr2 / (p * Mp).sum()
+        a += alp * p
+        r -= alp * Mp
+        nr2new = (r ** 2).sum()
+        k += 1
+        if nr2new < delta:
+            break
+        p = r + (nr2new / nr2) * p
+        nr2 = nr2new
+    return a, k
+
+
 class LDDMM:
     """Functional restatement of LDDMMModel's numerics (no optimizer state)."""
 

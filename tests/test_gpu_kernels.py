@@ -97,12 +97,18 @@ def test_ode_self_fwd(dev, version, M, D):
     v64, mG64, c64 = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
     v32, mG32, c32 = m32.ODE(q.float(), p.float(), torch.zeros(1))
     H64, H32 = m.Hamiltonian(q, p), m32.Hamiltonian(q.float(), p.float())
-    v, mG, gdiv, h = L.ode_self_fwd(q.float().to(dev), p.float().to(dev), 0.15, m.eta, wl, want_h=True)
-    assert rel_err(v.cpu(), v64) <= _tol(v64, v32)
-    assert rel_err(mG.cpu(), mG64) <= _tol(mG64, mG32)
-    assert rel_err(h.sum().cpu(), H64) <= _tol(H64, H32)
-    if wl:
-        assert rel_err(gdiv.sum().cpu(), c64) <= _tol(c64, c32)
+    for alg in (0, 1):  # eta = 0: ordered rows (OpOdeSelfFwd), symmetric pair-once kernel
+        L.set_option("fwd_alg", alg)
+        try:
+            v, mG, gdiv, h = L.ode_self_fwd(q.float().to(dev), p.float().to(dev), 0.15, m.eta, wl,
+                                            want_h=True)
+        finally:
+            L.set_option("fwd_alg", 0)
+        assert rel_err(v.cpu(), v64) <= _tol(v64, v32), alg
+        assert rel_err(mG.cpu(), mG64) <= _tol(mG64, mG32), alg
+        assert rel_err(h.sum().cpu(), H64) <= _tol(H64, H32), alg
+        if wl:
+            assert rel_err(gdiv.sum().cpu(), c64) <= _tol(c64, c32), alg
 
 
 @pytest.mark.parametrize("M,D", [(3, 2), (300, 2), (700, 3), (2100, 3), (4700, 3)])
@@ -218,3 +224,32 @@ def test_sym_bwd_vs_ordered(dev, M):
     gq3, gp3 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
     assert rel_err(gq2, gq1) < 2e-6 and rel_err(gp2, gp1) < 2e-6
     assert torch.equal(gq2, gq3) and torch.equal(gp2, gp3)
+
+
+@pytest.mark.parametrize("M", [1, 127, 128, 129, 1000, 5000, 50000])
+@pytest.mark.parametrize("want_div", [True, False])
+def test_sym_fwd_vs_ordered(dev, M, want_div):
+    """Symmetric pair-once forward == ordered-row forward up to fp32 summation order (partial
+    last groups and quads included), every output incl. the fused Euler epilogue;
+    deterministic run to run."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 11)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    ref = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)      # default: ordered rows
+    qn0, pn0, _ = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div)
+    L.set_option("fwd_alg", 1)
+    try:
+        out = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)
+        out2 = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)
+        qn1, pn1, _ = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div)
+    finally:
+        L.set_option("fwd_alg", 0)
+    for k, (a, b) in enumerate(zip(out, ref)):
+        if b is None:
+            continue
+        assert rel_err(a, b) < 2e-6, (k, rel_err(a, b))
+    for a, b in zip(out, out2):
+        if a is not None:
+            assert torch.equal(a, b)
+    assert rel_err(qn1, qn0) < 1e-7 and rel_err(pn1, pn0) < 2e-6

@@ -128,3 +128,15 @@ def test_decimate_oracle_vs_reference():
         kept, rej = R.decimate(T(z[f"{name}/x"]), float(z[f"{name}/R"]))
         assert kept == z[f"{name}/kept"].tolist(), name
         assert sorted(kept + rej) == list(range(z[f"{name}/x"].shape[0]))
+
+
+def test_oracle_ridge_cg_matches_dense():
+    """The restated KeOps CG (KridgeSolve_keops, kernel.py:239-241) converges to the dense
+    ridge solution (KridgeSolve_torch, kernel.py:234-237) in float64."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(200, 3, generator=g, dtype=torch.float64)
+    v = torch.randn(200, 3, generator=g, dtype=torch.float64)
+    b, k = R.KridgeSolve_cg(x, v, 0.1, 0.5, eps=1e-10)
+    ref = R.KridgeSolve_torch(x, v, 0.1, 0.5)
+    assert 0 < k < 200
+    assert float((b - ref).norm() / ref.norm()) < 1e-8
