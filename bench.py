@@ -39,6 +39,10 @@ METRIC = "PSR iterations/sec + kernel-sum HBM GB/s, 100k-pt 3D, 1/2/4/8 MI355X"
 WORKLOADS = {
     "two_set_50k": dict(kind="two_set", N=50000),
     "two_set_200k": dict(kind="two_set", N=200000),
+    # SURVEY C2': the exact ICP_two_set model (gradcomponent=True, eta = 1/lambda), a0 from
+    # the device ridge CG (v2p version "ridge_keops", alpha 1e-3, PSR.py:402)
+    "two_set_50k_exact": dict(kind="two_set", N=50000, version="logdet",
+                              v2p_args={"version": "ridge_keops", "alpha": 1e-3}),
     "atlas_c4": dict(kind="atlas", K_per_rank=4, N=20000, C=512, S=1),
     "c5": dict(kind="atlas", K_per_rank=8, N=7500, C=256, S=4),
 }
@@ -76,7 +80,7 @@ def cpu_baseline(pair_counts, M_work, budget_s=15.0):
     rates = {k: M * M / (sum(v) / len(v)) for k, v in times.items()}
     reps = len(times["fwd"])
     kind_of = {"ode_self_fwd": "fwd", "ode_self_fwd_eta": "fwd", "ode_ext_fwd": "fwd",
-               "gauss_red": "fwd", "ode_self_bwd": "bwd", "ode_ext_bwd": "bwd",
+               "gauss_red": "fwd", "ridge_cg": "fwd", "ode_self_bwd": "bwd", "ode_self_bwd_eta": "bwd", "ode_ext_bwd": "bwd",
                "gmm_estep": "em", "gmm_mstep": "em", "gmm_targets": "em"}
     secs = sum(v / rates[kind_of.get(k, "fwd")] for k, v in pair_counts.items())
     return {"value": 1.0 / secs, "unit": "PSR iterations/sec", "cores": threads, "kind": "port",
@@ -135,10 +139,12 @@ def _main(out):
     t_setup = time.perf_counter()
     if wl["kind"] == "two_set":
         # replicas: every rank registers its own copy (two-set does not shard)
-        psr = workloads.build_two_set(wl["N"], dev, seed=0)
+        version = wl.get("version", "hybrid")
+        psr = workloads.build_two_set(wl["N"], dev, seed=0, version=version,
+                                      v2p_args=wl.get("v2p_args"))
         cfg = {"workload": f"two-set 3D {wl['N']} vs {wl['N']} (BASELINE configs[1]" +
-               (")" if wl["N"] == 50000 else "/[2])"),
-               "points_per_set": wl["N"], "lddmm": "hybrid sigma=0.1 lambda=1e3 Euler nt=10 dense",
+               (")" if wl["N"] == 50000 else "/[2])") + (" exact ICP_two_set model" if version == "logdet" else ""),
+               "points_per_set": wl["N"], "lddmm": f"{version} sigma=0.1 lambda=1e3 Euler nt=10 dense",
                "gmm": "mu=xB fixed, sigma optimised", "max_repeat_GMM": 10, "tol": 1e-3,
                "parallelism": f"replicas x{world}"}
         scaling = "weak"

@@ -142,7 +142,7 @@ def _stream(device) -> ctypes.c_void_p:
 # (lddmm_sym.hpp) executes ~53 flop per ordered pair because it evaluates each unordered
 # pair once, so its effective rate can exceed the rate of executed arithmetic.
 FLOPS_PER_PAIR = {
-    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 70,
+    "gauss_red": 15, "ode_self_fwd": 33, "ode_self_fwd_eta": 70, "ode_self_bwd": 70, "ode_self_bwd_eta": 120,
     "ode_ext_fwd": 22, "ode_ext_bwd": (36 + 49) / 2, "gmm_estep": 37, "gmm_mstep": 31,
     "gmm_targets": 32, "ridge_cg": 15,
 }
@@ -308,7 +308,7 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
     if M == 0:
         return lqn, lpn
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
-    rc = _launch("ode_self_bwd", M * M, 4 * M * 8 * D,
+    rc = _launch(("ode_self_bwd_eta" if eta else "ode_self_bwd"), M * M, 4 * M * 8 * D,
                  lambda: lib().dicp_lddmm_euler_adjoint_step_f32(
                      _ptr(q), _ptr(p), _ptr(lq), _ptr(lp), _ptr(gdiv), M, D, float(sigma), float(eta),
                      float(dt), _ptr(addq), _ptr(addp), _ptr(lqn), _ptr(lpn), _ptr(ws), nb,
@@ -330,7 +330,7 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma: float, eta: float):
     if M == 0:
         return gq, gp
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
-    rc = _launch("ode_self_bwd", M * M, 4 * M * 6 * D,
+    rc = _launch(("ode_self_bwd_eta" if eta else "ode_self_bwd"), M * M, 4 * M * 6 * D,
                  lambda: lib().dicp_lddmm_ode_self_bwd_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv), M,
                                            D, float(sigma), float(eta), _ptr(gq), _ptr(gp),
                                            _ptr(ws), nb, _stream(q.device)))

@@ -192,8 +192,14 @@ class MultiPSR:
 class DiffPSR(MultiPSR):
     """MultiPSR with LDDMM registrations (PSR.py:354-569)."""
 
-    def __init__(self, x, GMMi, LMi: LDDMMModel, dataspec=defspec, compspec=defspec, comm=None):
+    def __init__(self, x, GMMi, LMi: LDDMMModel, dataspec=defspec, compspec=defspec, comm=None,
+                 v2p_args=None):
+        """v2p_args (extension, default None = the reference's v2p defaults): keyword arguments
+        of every v2p call made by initialize_a0 / update_a0 when the caller gives none, e.g.
+        {"version": "ridge_keops", "alpha": 1e-3} -- the alternative PSR.py:402 leaves
+        commented out, which is the only one that scales to 50k+ support points (device CG)."""
         super().__init__(x, GMMi, dataspec=dataspec, compspec=compspec, comm=comm)
+        self.v2p_args = dict(v2p_args or {})
         if LMi.Kernel.spec != compspec:
             raise ValueError("Spec (dtype+device) error : LDDMMmodel kernel 'spec' and diffPSR "
                              "'compspec' attributes should be the same")
@@ -208,11 +214,14 @@ class DiffPSR(MultiPSR):
 
     def initialize_a0(self, **v2p_args):
         """a0 giving zero initial speeds (PSR.py:406-413)."""
+        v2p_args = v2p_args or self.v2p_args
         for k in range(self.K):
             v0 = torch.zeros(self.q0[k].shape, **self.compspec)
             self.a0[k] = self.LMi.v2p(self.q0[k], v0, **v2p_args)
 
     def update_a0(self, q0_prev, a0_prev=None, **v2p_args):
+        if self.v2p_args and not v2p_args.get("version"):
+            v2p_args = {**self.v2p_args, **{k: v for k, v in v2p_args.items() if k != "rcond"}}
         if a0_prev is None:
             a0_prev = self.a0
         for k in range(self.K):

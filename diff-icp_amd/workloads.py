@@ -64,15 +64,17 @@ def multi_structure_frames(K, S, N, seed=0):
 
 
 def build_two_set(N, device, seed=0, sigma_gmm=0.05, sigma_lddmm=0.1, lam=1e3, nt=10,
-                  scheme="Euler", version="hybrid"):
+                  scheme="Euler", version="hybrid", v2p_args=None):
     """ICP_two_set (ICP_two_set.py:176-226): GMM with mu = xB, w frozen, sigma optimised;
-    LDDMM hybrid (withlogdet, gradcomponent False), Euler nt=10, dense support."""
+    LDDMM hybrid (withlogdet, gradcomponent False), Euler nt=10, dense support.
+    version="logdet" is the exact ICP_two_set model (gradcomponent=True, ICP_two_set.py:203-207;
+    SURVEY C2'): its a0 is initialised by v2p, here the device ridge CG (v2p_args)."""
     spec = {"device": device, "dtype": torch.float32}
     xA, xB = two_set_points(N, seed)
     G = GaussianMixtureUnif(xB.to(device), sigma=sigma_gmm, spec=spec)
     G.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
     LM = LDDMMModel(sigma=sigma_lddmm, D=3, lambd=lam, version=version, scheme=scheme, nt=nt, spec=spec)
-    psr = DiffPSR(xA.to(device), G, LM, dataspec=spec, compspec=spec)
+    psr = DiffPSR(xA.to(device), G, LM, dataspec=spec, compspec=spec, v2p_args=v2p_args)
     psr.printstuff = False
     return psr
 

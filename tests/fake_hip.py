@@ -191,7 +191,13 @@ def radius_count(x, y, radius):
     return _out((d <= radius ** 2).sum(1).to(torch.float64), x)
 
 
-_ENTRIES = ("euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+def kernel_ridge_cg(x, v, sigma, alpha, eps=1e-6, maxiter=5000, chunk=32):
+    b, k = R.KridgeSolve_cg(_d(x), _d(v), sigma, alpha, eps=eps, maxiter=maxiter)
+    st = "converged" if k < maxiter else "maxiter"
+    return _out(b, v), {"status": st, "iterations": k, "residual2": 0.0, "threshold": 0.0}
+
+
+_ENTRIES = ("kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 

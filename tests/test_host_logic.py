@@ -165,3 +165,19 @@ def test_decim_psr_trace_host_logic_fp64(fake):
         fe = float(z[f"psr/it{it}/FE_reg"])
         assert abs(PS.FE - fe) < 1e-6 * abs(fe), (it, PS.FE, fe)
         assert rel_err(PS.x1[0, 0], torch.from_numpy(z[f"psr/it{it}/x1"])) < 1e-6
+
+
+def test_exact_two_set_ridge_init(fake):
+    """DiffPSR(v2p_args=ridge_keops) for the exact ICP_two_set model (gradcomponent=True): the
+    zero-speed a0 (PSR.py:404-413) is the ridge solution of K a0 = eta GradKRed(q,q)
+    (kernel.py:234-241), and one PSR iteration runs through the host path."""
+    from difficp_amd import workloads
+    from difficp_amd.core.LDDMM import LDDMMModel  # noqa: F401
+    psr = workloads.build_two_set(300, torch.device("cpu"), seed=1, version="logdet",
+                                  v2p_args={"version": "ridge_keops", "alpha": 1e-3})
+    q = psr.q0[0].double()
+    rhs = (1.0 / 1e3) * R.GradKRed(q, q, 0.1)
+    ref = R.KridgeSolve_torch(q, rhs, 0.1, 1e-3)
+    assert rel_err(psr.a0[0], ref) < 1e-2   # CG stops at |r|^2 < n eps^2; cond(K + 1e-3 I) ~ 1e5
+    workloads.psr_iteration(psr)
+    assert psr.FE == psr.FE  # finite
