@@ -7,16 +7,18 @@ A "step" is one diff-ICP iteration on the workload -- GMM_opt(max_repeat_GMM=10,
 + Reg_opt(nmax=1, tol=1e-3), the loop body of ICP_two_set.py:254-282 / ICP_atlas.py:269-298 --
 with every point set resident in HBM.  Default workload (BASELINE.json configs[1]):
 two-point-set 3D match, 50k vs 50k synthetic points, hybrid LDDMM (sigma 0.1, lambda 1e3,
-Euler nt=10, dense support), GMM on xB with sigma optimised.  The two-set case does not
-shard (one frame), so for N > 1 every rank runs an independent replica ("replicas only",
-weak scaling); the atlas workloads shard frames over ranks with an RCCL exchange of the
-GMM sufficient statistics.
+Euler nt=10, dense support), GMM on xB with sigma optimised.  The atlas workloads shard
+frames over ranks with an RCCL exchange of the GMM sufficient statistics.
 
 Rank 0 prints ONE JSON line (value = iterations of all ranks / max-over-ranks time) with a
 "roofline" object for the dominant kernel (algorithmic flop per launch / average launch
 time from HIP events on the launch stream, vs the 157.3 TFLOP/s fp32 peak) and a
 "cpu_baseline" object (the oracle's C restatement timed on this host on a bounded sample,
 extrapolated to one iteration of the same workload from the live pair counts).
+
+Two-set workloads at N > 1 row-split the ONE match over the ranks by default (SURVEY f1,
+core/rowsplit.py; "scaling": "strong", value = iterations of that match per second);
+--replicas runs N independent copies instead (weak scaling).
 """
 import argparse
 import json
@@ -120,16 +122,27 @@ def _main(out):
     ap.add_argument("--workload", default="two_set_50k", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip live per-kernel events")
+    ap.add_argument("--replicas", action="store_true",
+                    help="two-set workloads at N > 1: N independent replicas (weak scaling) "
+                         "instead of row-splitting the one match over the N GPUs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal on a 1-GPU box (never the driver's runs): DICP_BENCH_REHEARSE=1 puts every rank
+    # on cuda:0 and uses gloo, which RCCL cannot do (one rank per GPU)
+    rehearse = os.environ.get("DICP_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -138,16 +151,22 @@ def _main(out):
     wl = WORKLOADS[args.workload]
     t_setup = time.perf_counter()
     if wl["kind"] == "two_set":
-        # replicas: every rank registers its own copy (two-set does not shard)
+        # N > 1: the ONE match is row-split over the ranks (core/rowsplit.py: per ODE step an
+        # RCCL all-gather of the new row slices, per adjoint step an all-reduce of the VJP
+        # parts) -- strong scaling; --replicas: N independent copies (weak scaling)
         version = wl.get("version", "hybrid")
         psr = workloads.build_two_set(wl["N"], dev, seed=0, version=version,
                                       v2p_args=wl.get("v2p_args"))
+        split = world > 1 and not args.replicas
+        if split:
+            psr.LMi.set_row_split()
         cfg = {"workload": f"two-set 3D {wl['N']} vs {wl['N']} (BASELINE configs[1]" +
                (")" if wl["N"] == 50000 else "/[2])") + (" exact ICP_two_set model" if version == "logdet" else ""),
                "points_per_set": wl["N"], "lddmm": f"{version} sigma=0.1 lambda=1e3 Euler nt=10 dense",
                "gmm": "mu=xB fixed, sigma optimised", "max_repeat_GMM": 10, "tol": 1e-3,
-               "parallelism": f"replicas x{world}"}
-        scaling = "weak"
+               "parallelism": (f"row-split x{world} (RCCL all-gather / all-reduce per ODE step)" if split
+                               else f"replicas x{world}")}
+        scaling = "strong" if split else "weak"
     else:
         K = wl["K_per_rank"] * world
         comm = True if world > 1 else None
@@ -193,7 +212,8 @@ def _main(out):
         elapsed = float(t.item())
 
     if rank == 0:
-        iters = args.steps * world
+        # row-split: all ranks advance the SAME match; replicas / atlas: every rank's own work
+        iters = args.steps * (1 if scaling == "strong" else world)
         value = iters / elapsed
         summ = prof.summary() if prof is not None else {}
         roof = None

@@ -22,7 +22,7 @@ KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRAD
     GRADLAPKSCAL, MIN_SQDIST, MIN_SQDIST_OTHER = range(14)
 # enum dicp_ws_kind
 WS_RED, WS_ODE_SELF_FWD, WS_ODE_SELF_BWD, WS_ODE_EXT_FWD, WS_ODE_EXT_BWD, WS_GMM_ESTEP, \
-    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG = range(9)
+    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG, WS_ODE_SELF_FWD_ROWS, WS_ODE_SELF_BWD_PART = range(11)
 
 _lock = threading.Lock()
 _lib = None
@@ -47,6 +47,12 @@ _SIGNATURES = {
     "dicp_gmm_estep_f32": [_P, _I64, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _SZ, _P],
     "dicp_gmm_mstep_f32": [_P, _P, _I64, _P, _P, _I64, _INT, _DBL, _P, _P, _SZ, _P],
     "dicp_gmm_targets_f32": [_P, _P, _I64, _P, _P, _DBL, _P, _P, _I64, _INT, _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_self_fwd_rows_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P,
+                                         _P, _SZ, _P],
+    "dicp_lddmm_euler_step_rows_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P,
+                                       _P, _SZ, _P],
+    "dicp_lddmm_ode_self_bwd_part_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _INT, _INT, _P,
+                                         _P, _P, _SZ, _P],
     "dicp_kernel_ridge_cg_f32": [_P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _INT, _INT, _P, _SZ, _P],
     "dicp_workspace_bytes": [_INT, _I64, _I64, _INT],
     "dicp_last_error": [],
@@ -484,3 +490,78 @@ def kernel_ridge_cg(x, v, sigma: float, alpha: float, eps: float = 1e-6, maxiter
     info = {"status": CG_DONE_NAMES.get(done, str(done)) if done else "maxiter",
             "iterations": it, "residual2": rr, "threshold": thr}
     return b, info
+
+
+# ---------------------------------------------------------------------------------------
+# Row-split of one frame over ranks (core/rowsplit.py)
+# ---------------------------------------------------------------------------------------
+def ode_self_fwd_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, want_div: bool,
+                      want_h: bool = False):
+    """Rows [row0, row0 + nrows) of ode_self_fwd against all columns
+    (dicp_lddmm_ode_self_fwd_rows_f32).  Returns (v, mG, g, h) for the slice."""
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    M, D = q.shape
+    dev = q.device
+    v = torch.empty((nrows, D), device=dev, dtype=torch.float32)
+    mG = torch.empty_like(v)
+    g = torch.empty(nrows, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
+    h = torch.empty(nrows, device=dev, dtype=torch.float32) if want_h else None
+    if nrows == 0:
+        return v, mG, g, h
+    ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
+    rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), nrows * M, 4 * (nrows * (2 * D + 2) + 2 * M * D),
+                 lambda: lib().dicp_lddmm_ode_self_fwd_rows_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                                                                float(sigma), float(eta), _ptr(v), _ptr(mG),
+                                                                _ptr(g), _ptr(h), _ptr(ws), nb, _stream(dev)))
+    _check_rc(rc, "ode_self_fwd_rows")
+    return v, mG, g, h
+
+
+def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: float,
+                    want_div: bool, q_out=None, p_out=None):
+    """Rows [row0, row0 + nrows) of euler_step (dicp_lddmm_euler_step_rows_f32):
+    (q + dt v, p + dt mG, g) for the slice; q_out / p_out: optional contiguous (nrows, D)."""
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    M, D = q.shape
+    dev = q.device
+    qn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if q_out is None else q_out
+    pn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if p_out is None else p_out
+    for t, name in ((qn, "q_out"), (pn, "p_out")):
+        if not t.is_contiguous() or tuple(t.shape) != (nrows, D) or t.dtype != torch.float32:
+            raise ValueError(f"{name} must be a contiguous float32 ({nrows}, {D}) tensor")
+    g = torch.empty(nrows, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
+    if nrows == 0:
+        return qn, pn, g
+    ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
+    rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), nrows * M, 4 * (nrows * (4 * D + 1) + 2 * M * D),
+                 lambda: lib().dicp_lddmm_euler_step_rows_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                                                              float(sigma), float(eta), float(dt), _ptr(qn),
+                                                              _ptr(pn), _ptr(g), _ptr(ws), nb, _stream(dev)))
+    _check_rc(rc, "euler_step_rows")
+    return qn, pn, g
+
+
+def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, nparts: int):
+    """Part `part` of `nparts` of ode_self_bwd (dicp_lddmm_ode_self_bwd_part_f32): (gq, gp)
+    over a pair subset; the sum over the parts is the full VJP."""
+    q = _dev(q, "q")
+    p = _dev(p, "p")
+    gv = _dev(gv, "gv")
+    gmG = _dev(gmG, "gmG")
+    gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
+    M, D = q.shape
+    gq = torch.empty_like(q)
+    gp = torch.empty_like(q)
+    if M == 0:
+        return gq, gp
+    ws, nb = _workspace(WS_ODE_SELF_BWD_PART, M, nparts, D, q.device)
+    pairs = (M * M) // nparts
+    rc = _launch(("ode_self_bwd_eta" if eta else "ode_self_bwd"), pairs, 4 * M * 6 * D,
+                 lambda: lib().dicp_lddmm_ode_self_bwd_part_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv),
+                                                                M, D, float(sigma), float(eta), int(part),
+                                                                int(nparts), _ptr(gq), _ptr(gp), _ptr(ws), nb,
+                                                                _stream(q.device)))
+    _check_rc(rc, "ode_self_bwd_part")
+    return gq, gp

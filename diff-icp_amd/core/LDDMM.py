@@ -64,6 +64,14 @@ class LDDMMModel:
         self.scheme, self.Integrator = None, None
         self.set_integration_scheme(scheme)
         self.try_trajcost_optim = False
+        self.row_split = None
+
+    def set_row_split(self, group=None, enable=True):
+        """Split every dense Euler shooting of this model over the ranks of a torch.distributed
+        group (extension; core/rowsplit.py): all ranks must make the same
+        calls (the host logic runs replicated).  enable=False restores single-device shooting."""
+        from .rowsplit import RowSplit
+        self.row_split = RowSplit(group) if enable else None
 
     def set_integration_scheme(self, scheme: str):
         self.scheme = scheme
@@ -177,7 +185,8 @@ class LDDMMModel:
             return self.Integrator(self.ODE, (q0, p0, cost0), self.nt)
         outs = ShootFn.apply(q0.contiguous(), p0.contiguous(),
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
-                             float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet))
+                             float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet),
+                             self.row_split)
         if x0 is None:
             Q, P, C, H0 = outs
             return Shoot(Q, P, C, None, H0)

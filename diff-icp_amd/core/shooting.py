@@ -56,9 +56,14 @@ class ShootFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div):
+    def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None):
         ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
+        # row-split over ranks (core/rowsplit.py): dense Euler shooting only; other schemes
+        # run replicated on every rank
+        if split is not None and (has_x or scheme != "Euler" or split.world == 1):
+            split = None
+        ctx.split = split
         M, D = q0.shape
         dev = q0.device
         dt = 1.0 / nt
@@ -76,6 +81,29 @@ class ShootFn(torch.autograd.Function):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
             first = t == 0
+            if split is not None:
+                r0, n, _ = split.rows(M)
+                if first:
+                    v_l, mG_l, g_l, h_l = _lib.ode_self_fwd_rows(q, p, r0, n, sigma, eta, want_div,
+                                                                 want_h=True)
+                    loc = torch.stack([h_l.sum(), g_l.sum() if g_l is not None else h_l.sum() * 0])
+                    (v0, mG0), _ = split.gather_rows([v_l, mG_l], M)
+                    sums = split.all_reduce_(loc)   # (H0, div): identical on every rank
+                    H0 = sums[0]
+                    torch.add(q, v0, alpha=dt, out=Q[t + 1])
+                    torch.add(p, mG0, alpha=dt, out=P[t + 1])
+                    div = sums[1:2]
+                else:
+                    qn_l, pn_l, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div)
+                    gs = g_l.sum().reshape(1) if g_l is not None else None
+                    (qn, pn), div = split.gather_rows([qn_l, pn_l], M, scalar=gs)
+                    Q[t + 1].copy_(qn)
+                    P[t + 1].copy_(pn)
+                if want_div:
+                    torch.add(C[t], div, alpha=dt, out=C[t + 1])
+                else:
+                    C[t + 1].copy_(C[t])
+                continue
             if scheme == "Euler" and not has_x and not first:
                 # fused pass: Q[t+1], P[t+1] written by the reduction's epilogue
                 _, _, g = _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1])
@@ -138,6 +166,7 @@ class ShootFn(torch.autograd.Function):
         gX, gH = rest if len(rest) == 2 else (None, rest[0])
         sigma, eta, nt, scheme, want_div, has_x = \
             ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x
+        split = ctx.split
         saved = ctx.saved_tensors
         Q, P, v0, mG0 = saved[:4]
         X = saved[4] if has_x else None
@@ -165,6 +194,20 @@ class ShootFn(torch.autograd.Function):
         for t in range(nt - 1, -1, -1):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
+            if split is not None:
+                # this rank's part of the pair-once VJP, summed over ranks (one all-reduce)
+                gq_l, gp_l = _lib.ode_self_bwd_part(q, p, lq, lp, lc if want_div else None, sigma,
+                                                    eta, split.rank, split.world)
+                g = split.all_reduce_(torch.cat([gq_l, gp_l], 1))
+                lq = torch.add(lq, g[:, :D], alpha=dt)
+                lp = torch.add(lp, g[:, D:], alpha=dt)
+                if gQ is not None:
+                    lq = lq + gQ[t]
+                if gP is not None:
+                    lp = lp + gP[t]
+                if gC is not None:
+                    lc = lc + gC[t]
+                continue
             if scheme == "Euler" and not has_x:
                 # fused pass: lambda_t = lambda_{t+1} + dt VJP + the loss's own cotangent at t
                 lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lc if want_div else None, sigma, eta,
@@ -208,7 +251,7 @@ class ShootFn(torch.autograd.Function):
         if gH is not None:
             lq = lq - gH * mG0
             lp = lp + gH * v0
-        return lq, lp, (lx if has_x else None), None, None, None, None, None
+        return lq, lp, (lx if has_x else None), None, None, None, None, None, None
 
 
 class HamiltonianFn(torch.autograd.Function):

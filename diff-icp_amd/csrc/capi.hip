@@ -33,7 +33,7 @@ extern "C" size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D) {
   size_t b = 0;
   if (kind == DICP_WS_RIDGE_CG)
     b = dicp_solve_ws(kind, M, D);
-  else if (kind >= DICP_WS_GMM_ESTEP)
+  else if (kind >= DICP_WS_GMM_ESTEP && kind <= DICP_WS_GMM_TARGETS)
     b = dicp_gmm_ws(kind, M, N, D);
   else
     b = dicp_lddmm_ws(kind, M, N, D);

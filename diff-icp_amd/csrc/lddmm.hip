@@ -184,20 +184,35 @@ extern "C" int dicp_radius_count_f32(const float* x, int64_t M, const float* y, 
 // ---------------------------------------------------------------------------------------
 namespace {
 
+// rows [row0, row0 + nrows) of the pass against all M columns (row-split over ranks);
+// nrows < 0: all rows.  Output pointers in `o` address the row slice.
 template <int D>
 int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, double eta,
-                   const Outs& o, void* ws, size_t wsb, hipStream_t st) {
-  Args a = {q, p, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
+                   const Outs& o, void* ws, size_t wsb, hipStream_t st, int64_t row0 = 0,
+                   int64_t nrows = -1) {
+  const bool all = nrows < 0;
+  if (all) nrows = M;
+  Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
   if (eta != 0.0)
-    return launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
-  if (g_fwd_alg == 1)
+    return launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
+  if (g_fwd_alg == 1 && all)
     return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st)
                                : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st);
   if (o.ptr[2] != nullptr)
-    return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
-  return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, M, M, o, ws, wsb, st);
+    return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
+  return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
+}
+
+template <int D>
+size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
+  size_t m = 0;
+  for (size_t v : {ws_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), nrows, M),
+                   ws_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), nrows, M),
+                   ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), nrows, M)})
+    m = v > m ? v : m;
+  return m;
 }
 
 template <int D>
@@ -229,6 +244,56 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
+}
+
+// Pair subset `part` of `nparts` of the VJP (row-split over ranks; the sum over parts is
+// the full VJP): eta = 0 symmetric kernel -> the quads Q = part (mod nparts), written to all
+// rows; otherwise (ordered kernels) the row slice [part * ceil(M/nparts), ...) against all
+// columns, other rows zero.  Outputs plain (no epilogue).
+template <int D>
+int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const float* gmG,
+                        const float* gdiv, int64_t M, double sigma, double eta, int part,
+                        int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
+  if (eta == 0.0 && g_bwd_alg == 2) {
+    Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
+    Scal sc = make_scal(sigma, 0.0);
+    scale_coords(a, sc, sigma);
+    sc.dev0 = gdiv;
+    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts);
+  }
+  const int64_t per = (M + nparts - 1) / nparts;
+  const int64_t r0 = per * part < M ? per * part : M;
+  const int64_t r1 = r0 + per < M ? r0 + per : M;
+  if (hipMemsetAsync(gq, 0, (size_t)M * D * sizeof(float), st) != hipSuccess ||
+      hipMemsetAsync(gp, 0, (size_t)M * D * sizeof(float), st) != hipSuccess) {
+    set_error("ode_self_bwd_part: hipMemsetAsync failed");
+    return DICP_ERR_HIP;
+  }
+  if (r1 <= r0) return DICP_OK;
+  const int64_t o0 = r0 * D;
+  Args a = {q + o0, p + o0, gv + o0, gmG + o0, q, p, gv, gmG, 0.f};
+  const Outs o = make_outs(gq + o0, gp + o0);
+  if (eta != 0.0) {
+    Scal sc = make_scal(sigma, eta);
+    sc.dev0 = gdiv;
+    return launch_r<OpOdeSelfBwdEta<D>>(r_bwd(), "ode_self_bwd_eta", a, sc, r1 - r0, M, o, ws, wsb, st);
+  }
+  Scal sc = make_scal(sigma, 0.0);
+  scale_coords(a, sc, sigma);
+  sc.dev0 = gdiv;
+  if (g_bwd_alg == 1)
+    return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, r1 - r0, M, o, ws, wsb, st);
+  return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, r1 - r0, M, o, ws, wsb, st);
+}
+
+template <int D>
+size_t ode_self_bwd_part_ws(int64_t M, int nparts) {
+  const int64_t per = (M + nparts - 1) / nparts;
+  size_t m = sym_ws_bytes(M, 2 * D);
+  for (size_t v : {ws_r<OpOdeSelfBwd<D>>(r_bwd(), per, M), ws_r<OpOdeSelfBwdEta<D>>(r_bwd(), per, M),
+                   ws_r<OpOdeSelfBwd2<D>>(r_bwd(), per, M)})
+    m = v > m ? v : m;
+  return m;
 }
 
 template <int D>
@@ -418,6 +483,69 @@ extern "C" int dicp_lddmm_ode_ext_bwd_f32(const float* x, int64_t N, const float
   }
 }
 
+// Row-split (multi-GPU single frame): rows [row0, row0 + nrows) of the fused
+// forward against all M columns; outputs address the slice (nrows rows).
+extern "C" int dicp_lddmm_ode_self_fwd_rows_f32(const float* q, const float* p, int64_t M,
+                                                int64_t row0, int64_t nrows, int D,
+                                                double sigma, double eta, float* v, float* mG,
+                                                float* g, float* h, void* ws, size_t ws_bytes,
+                                                dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
+      (nrows > 0 && (!q || !p || !v || !mG)) || !(sigma > 0)) {
+    set_error("dicp_lddmm_ode_self_fwd_rows_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  if (nrows == 0) return DICP_OK;
+  switch (D) {
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, make_outs(v, mG, g, h), ws, ws_bytes, st, row0, nrows);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, make_outs(v, mG, g, h), ws, ws_bytes, st, row0, nrows);
+    default: set_error("ode_self_fwd_rows: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+extern "C" int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, int64_t M,
+                                              int64_t row0, int64_t nrows, int D, double sigma,
+                                              double eta, double dt, float* q_next,
+                                              float* p_next, float* g, void* ws,
+                                              size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
+      (nrows > 0 && (!q || !p || !q_next || !p_next)) || !(sigma > 0)) {
+    set_error("dicp_lddmm_euler_step_rows_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  if (nrows == 0) return DICP_OK;
+  Outs o = make_outs(q_next, p_next, g, nullptr);
+  o.base[0] = q + row0 * D;
+  o.base[1] = p + row0 * D;
+  o.alpha[0] = o.alpha[1] = (float)dt;
+  switch (D) {
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows);
+    default: set_error("euler_step_rows: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+extern "C" int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, const float* gv,
+                                                const float* gmG, const float* gdiv, int64_t M,
+                                                int D, double sigma, double eta, int part,
+                                                int nparts, float* gq, float* gp, void* ws,
+                                                size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || nparts < 1 || part < 0 || part >= nparts ||
+      (M > 0 && (!q || !p || !gv || !gmG || !gq || !gp)) || !(sigma > 0)) {
+    set_error("dicp_lddmm_ode_self_bwd_part_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  if (M == 0) return DICP_OK;
+  switch (D) {
+    case 2: return ode_self_bwd_part_d<2>(q, p, gv, gmG, gdiv, M, sigma, eta, part, nparts, gq, gp, ws, ws_bytes, st);
+    case 3: return ode_self_bwd_part_d<3>(q, p, gv, gmG, gdiv, M, sigma, eta, part, nparts, gq, gp, ws, ws_bytes, st);
+    default: set_error("ode_self_bwd_part: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
 // Workspace sizes for the LDDMM entries (the GMM ones live in gmm.hip).
 size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
   if (!supported_dim(D)) return 0;
@@ -447,6 +575,12 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
     }
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);
     case DICP_WS_ODE_EXT_BWD: return D == 2 ? ode_ext_bwd_ws<2>(N, M) : ode_ext_bwd_ws<3>(N, M);
+    case DICP_WS_ODE_SELF_FWD_ROWS:
+      return D == 2 ? ode_self_fwd_rows_ws<2>(M, N) : ode_self_fwd_rows_ws<3>(M, N);
+    case DICP_WS_ODE_SELF_BWD_PART: {
+      const int np = N < 1 ? 1 : (int)N;
+      return D == 2 ? ode_self_bwd_part_ws<2>(M, np) : ode_self_bwd_part_ws<3>(M, np);
+    }
     default: return 0;
   }
 }

@@ -272,7 +272,8 @@ __device__ __forceinline__ float rol1(float x) {
 // sensitive to the surrounding code, so this instance is kept as first tuned).
 template <int D>
 __global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M, int nG, int L,
-                                                      float* __restrict__ slab, int64_t slot_stride) {
+                                                      float* __restrict__ slab, int64_t slot_stride,
+                                                      int qoff, int qstride) {
   using S = SymBwd<D>;
   constexpr int CW = S::CW, W = S::W;
   __shared__ float4 planes[2][CW][kSymG];
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(256) void sym_bwd_kernel(Args a, Scal sc, int64_t M
   const float gt = sc.aux0 * cs;         // gam s1 / alpha
   const typename S::Prm prm{gt, cs};
 
-  const int Q = blockIdx.y, kc = blockIdx.x;
+  const int Q = qoff + qstride * (int)blockIdx.y, kc = blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
   if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
   const int B1 = min(B0 + L, nG);
@@ -553,18 +554,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxW
 }
 
 // out0 = gq = s * sum(gq/s), out1 = gp = alpha * sum(gp/alpha), with the Outs epilogue.
+// Pair-subset mode (row-split over ranks): only the quads Q = qoff (mod qstride) ran, so a
+// row of quad Q_T sums its column slots Q <= Q_T of those quads and, if Q_T is one of them,
+// its row slots; (qoff, qstride) = (0, 1) is every slot in slot order.
 template <int D>
 __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
                                                         int64_t slot_stride, int64_t M, int nG,
-                                                        int L, float s, float alpha, Outs o) {
+                                                        int L, float s, float alpha, Outs o,
+                                                        int qoff, int qstride) {
   constexpr int W = 2 * D;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= M * W) return;
   const int64_t row = e / W;
   const int c = (int)(e - row * W);
-  const int ns = sym_nslots((int)(row / kSymG), nG, L);
-  float acc = slab[e];
-  for (int t = 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
+  const int T = (int)(row / kSymG);
+  const int QT = T / kSymQ;
+  const int ns = sym_nslots(T, nG, L);
+  float acc = 0.f;
+  for (int q = qoff; q <= QT; q += qstride) acc += slab[(int64_t)q * slot_stride + e];
+  if (QT >= qoff && (QT - qoff) % qstride == 0)
+    for (int t = QT + 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
   if (c < D) {
     const int64_t idx = row * D + c;
     o.ptr[1][idx] = epilogue(o, 1, idx, alpha * acc);
@@ -642,7 +651,7 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
 
 template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
-                   hipStream_t st) {
+                   hipStream_t st, int part = 0, int nparts = 1) {
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M);
   const size_t need = sym_ws_bytes(M, 2 * D);
@@ -656,13 +665,16 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   }
   float* slab = reinterpret_cast<float*>(ws);
   const int64_t stride = M * 2 * D;
-  sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
-      a, sc, M, g.nG, g.L, slab, stride);
-  int rc = check_launch("ode_self_bwd(sym)");
-  if (rc) return rc;
+  const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
+  if (nq_own > 0) {
+    sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+        a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    int rc = check_launch("ode_self_bwd(sym)");
+    if (rc) return rc;
+  }
   const int64_t n = M * 2 * D;
   sym_merge_kernel<D><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-      slab, stride, M, g.nG, g.L, sc.s, a.scale, o);
+      slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts);
   return check_launch("ode_self_bwd(sym merge)");
 }
 

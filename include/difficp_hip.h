@@ -140,6 +140,38 @@ int dicp_lddmm_ode_ext_bwd_f32(const float* x, int64_t N, const float* q, const 
                                size_t ws_bytes, dicp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Row-split of ONE frame over ranks (C2/C3 two-set matches across GPUs).
+ * The reference has no multi-device path; these split LDDMMModel.ODE (LDDMM.py:176-227) and
+ * its VJP (optim.py:46) so that every rank holds the full (q, p) (M x 2D floats), computes a
+ * slice, and the host exchanges O(M) floats per ODE evaluation (all-gather of the forward
+ * slices, all-reduce of the VJP parts).
+ * ---------------------------------------------------------------------------------- */
+
+/* Rows [row0, row0 + nrows) of dicp_lddmm_ode_self_fwd_f32 against all M columns; v, mG
+ * (nrows, D), g, h (nrows,) address the slice.  Workspace kind DICP_WS_ODE_SELF_FWD_ROWS
+ * (M = nrows, N = M). */
+int dicp_lddmm_ode_self_fwd_rows_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                     int64_t nrows, int D, double sigma, double eta, float* v,
+                                     float* mG, float* g, float* h, void* ws, size_t ws_bytes,
+                                     dicp_stream_t stream);
+
+/* Rows [row0, row0 + nrows) of dicp_lddmm_euler_step_f32: q_next = q[rows] + dt v(rows),
+ * p_next = p[rows] + dt mG(rows), g (nrows,) or NULL.  Same workspace kind as above. */
+int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                   int64_t nrows, int D, double sigma, double eta, double dt,
+                                   float* q_next, float* p_next, float* g, void* ws,
+                                   size_t ws_bytes, dicp_stream_t stream);
+
+/* Part `part` of `nparts` of dicp_lddmm_ode_self_bwd_f32: gq, gp (M, D) over a subset of
+ * the pairs such that the SUM over the parts is the full VJP (eta = 0: the symmetric
+ * kernel's quads Q = part mod nparts, every row touched; eta != 0: a row slice, other rows 0).
+ * Workspace kind DICP_WS_ODE_SELF_BWD_PART (M, N = nparts). */
+int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, const float* gv,
+                                     const float* gmG, const float* gdiv, int64_t M, int D,
+                                     double sigma, double eta, int part, int nparts, float* gq,
+                                     float* gp, void* ws, size_t ws_bytes, dicp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * GMM EM step reductions (GaussianMixtureUnif.EM_step_torch, GMM.py:236-325).
  * log2-domain internally; outputs in natural log.
  * ---------------------------------------------------------------------------------- */
@@ -199,7 +231,9 @@ int dicp_kernel_ridge_cg_f32(const float* x, int64_t M, int D, double sigma, dou
 enum dicp_ws_kind {
   DICP_WS_RED = 0, DICP_WS_ODE_SELF_FWD = 1, DICP_WS_ODE_SELF_BWD = 2, DICP_WS_ODE_EXT_FWD = 3,
   DICP_WS_ODE_EXT_BWD = 4, DICP_WS_GMM_ESTEP = 5, DICP_WS_GMM_MSTEP = 6, DICP_WS_GMM_TARGETS = 7,
-  DICP_WS_RIDGE_CG = 8 /* M = points, N unused */
+  DICP_WS_RIDGE_CG = 8,          /* M = points, N unused */
+  DICP_WS_ODE_SELF_FWD_ROWS = 9, /* M = rows of the slice, N = all points (columns) */
+  DICP_WS_ODE_SELF_BWD_PART = 10 /* M = points, N = nparts */
 };
 size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D);
 

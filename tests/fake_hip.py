@@ -197,7 +197,32 @@ def kernel_ridge_cg(x, v, sigma, alpha, eps=1e-6, maxiter=5000, chunk=32):
     return _out(b, v), {"status": st, "iterations": k, "residual2": 0.0, "threshold": 0.0}
 
 
-_ENTRIES = ("kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False):
+    v, mG, g, h = ode_self_fwd(q, p, sigma, eta, want_div, want_h)
+    sl = slice(row0, row0 + nrows)
+    return v[sl].contiguous(), mG[sl].contiguous(), None if g is None else g[sl].contiguous(), \
+        None if h is None else h[sl].contiguous()
+
+
+def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_out=None):
+    v, mG, g, _ = ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div)
+    sl = slice(row0, row0 + nrows)
+    return q[sl] + dt * v, p[sl] + dt * mG, g
+
+
+def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts):
+    """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
+    its rows, zeros elsewhere; the sum over parts is the VJP."""
+    gq, gp = ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta)
+    M = q.shape[0]
+    per = -(-M // nparts)
+    r0, r1 = min(per * part, M), min(per * part + per, M)
+    mask = torch.zeros(M, 1, dtype=gq.dtype)
+    mask[r0:r1] = 1
+    return gq * mask, gp * mask
+
+
+_ENTRIES = ("ode_self_fwd_rows", "euler_step_rows", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 

@@ -65,6 +65,7 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     import torch.distributed as dist
+    torch.set_num_threads(1)  # no OpenMP oversubscription across the worker processes
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = _run(world, rank, True)

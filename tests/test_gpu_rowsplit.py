@@ -1,0 +1,127 @@
+"""GPU parity of the row-split entry points: row slices of the fused forward /
+Euler step concatenate to the full pass, the VJP parts sum to the full VJP (symmetric
+kernel's quad partition for eta = 0, row slices for eta != 0), incl. parts that own no pairs;
+and a world-2 gloo run of a two-set iteration on the GPU (both ranks on cuda:0) matches the
+single-process run.  Tolerances: fp32 summation-order differences only (2e-6 relative)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _lib():
+    from difficp_amd import _lib
+    return _lib
+
+
+def _state(M, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    a = torch.randn(M, 3, generator=g).to(dev)
+    b = torch.randn(M, 3, generator=g).to(dev)
+    return q, p, a, b
+
+
+@pytest.mark.parametrize("M", [1, 130, 3000, 50000])
+@pytest.mark.parametrize("W", [2, 3, 8])
+@pytest.mark.parametrize("eta", [0.0, 0.02])
+def test_fwd_rows_concatenate(dev, M, W, eta):
+    L = _lib()
+    q, p, _, _ = _state(M, M + W, dev)
+    v, mG, g, h = L.ode_self_fwd(q, p, 0.1, eta, True, want_h=True)
+    qn, pn, gn = L.euler_step(q, p, 0.1, eta, 0.1, True)
+    per = -(-M // W)
+    parts, steps = [], []
+    for r in range(W):
+        r0 = min(per * r, M)
+        n = min(r0 + per, M) - r0
+        parts.append(L.ode_self_fwd_rows(q, p, r0, n, 0.1, eta, True, want_h=True))
+        steps.append(L.euler_step_rows(q, p, r0, n, 0.1, eta, 0.1, True))
+    for k, full in enumerate((v, mG, g, h)):
+        cat = torch.cat([pp[k] for pp in parts], 0)
+        assert cat.shape == full.shape
+        assert rel_err(cat, full) < 2e-6, (k, rel_err(cat, full))
+    for k, full in enumerate((qn, pn, gn)):
+        cat = torch.cat([s[k] for s in steps], 0)
+        assert rel_err(cat, full) < 2e-6, (k, rel_err(cat, full))
+
+
+@pytest.mark.parametrize("M", [1, 130, 3000, 50000])
+@pytest.mark.parametrize("W", [2, 3, 8])
+@pytest.mark.parametrize("eta", [0.0, 0.02])
+def test_bwd_parts_sum(dev, M, W, eta):
+    L = _lib()
+    q, p, a, b = _state(M, 7 * M + W, dev)
+    gd = torch.full((1,), 0.3, device=dev)
+    gq, gp = L.ode_self_bwd(q, p, a, b, gd, 0.1, eta)
+    sq, sp = torch.zeros_like(gq), torch.zeros_like(gp)
+    for r in range(W):
+        pq, pp = L.ode_self_bwd_part(q, p, a, b, gd, 0.1, eta, r, W)
+        sq += pq
+        sp += pp
+    assert rel_err(sq, gq) < 2e-6, rel_err(sq, gq)
+    assert rel_err(sp, gp) < 2e-6, rel_err(sp, gp)
+    one = L.ode_self_bwd_part(q, p, a, b, gd, 0.1, eta, 0, 1)   # one part = the full VJP
+    assert torch.equal(one[0], gq) and torch.equal(one[1], gp)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _two_set(split):
+    sys.path.insert(0, ROOT)
+    from difficp_amd import workloads
+    dev = torch.device("cuda:0")
+    psr = workloads.build_two_set(3000, dev, seed=4, nt=5)
+    if split:
+        psr.LMi.set_row_split()
+    workloads.psr_iteration(psr, max_repeat_GMM=3, tol=1e-6)
+    return {"FE": float(psr.FE), "a0": psr.a0[0].detach().cpu().clone(),
+            "x1": psr.x1[0, 0].detach().cpu().clone()}
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = _two_set(True)
+        q.put((rank, res["FE"], res["a0"].numpy(), res["x1"].numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rowsplit_two_set_on_gpu(dev):
+    import numpy as np
+    single = _two_set(False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=100) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, fe, a0, x1 in out:
+        assert abs(fe - single["FE"]) < 1e-5 * abs(single["FE"]), (rank, fe, single["FE"])
+        assert np.abs(x1 - single["x1"].numpy()).max() < 1e-3
+    assert out[0][1] == out[1][1]
+    assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])
