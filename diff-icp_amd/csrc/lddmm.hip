@@ -97,7 +97,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "sym_L")) {
-    if (value < 1 || value > 64) return DICP_ERR_INVALID;
+    if (value < 0 || value > 64) return DICP_ERR_INVALID;  // 0 = automatic
     sym_L() = value;
     return DICP_OK;
   }
@@ -289,7 +289,7 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
 template <int D>
 size_t ode_self_bwd_part_ws(int64_t M, int nparts) {
   const int64_t per = (M + nparts - 1) / nparts;
-  size_t m = sym_ws_bytes(M, 2 * D);
+  size_t m = sym_ws_bytes(M, 2 * D, nparts);
   for (size_t v : {ws_r<OpOdeSelfBwd<D>>(r_bwd(), per, M), ws_r<OpOdeSelfBwdEta<D>>(r_bwd(), per, M),
                    ws_r<OpOdeSelfBwd2<D>>(r_bwd(), per, M)})
     m = v > m ? v : m;

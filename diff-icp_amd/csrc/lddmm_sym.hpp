@@ -30,11 +30,12 @@ namespace dicp {
 
 constexpr int kSymG = 128;   // points per group (= rows of one wave)
 constexpr int kSymQ = 4;     // row groups (waves) per workgroup
-// column groups per workgroup (dicp_set_option "sym_L"; default from an MI355X sweep)
+// column groups per workgroup: dicp_set_option "sym_L" forces a value; 0 = automatic
 inline int& sym_L() {
-  static int L = 4;
+  static int L = 0;
   return L;
 }
+// padding coordinate: K = exp2(-|z|^2) = 0 against real points
 constexpr float kFar = 1.0e12f;
 // s_waitcnt lgkmcnt(0) with vmcnt / expcnt left at their maxima (gfx9 encoding)
 constexpr int kLgkm0 = 0xC07F;
@@ -46,7 +47,7 @@ constexpr int kLgkm0 = 0xC07F;
 #endif
 #ifndef DICP_SYMFWD_WAVES
 #define DICP_SYMFWD_WAVES 8
-#endif  // padding coordinate: K = exp2(-|z|^2) = 0 against real points
+#endif
 
 struct SymGeom {
   int64_t M;
@@ -57,12 +58,21 @@ struct SymGeom {
   int nslot;  // slots per row (max)
 };
 
-inline SymGeom sym_geom(int64_t M) {
+// L = 4 on one device (an MI355X sweep at 50k: L = 2..4 within 1%, 8 and 16 slower); a
+// pair-subset launch (nparts > 1, row-split over ranks) has 1/nparts of the blocks, so L
+// shrinks until a part still has >= 2048 workgroups (2 x 256 CUs x 4 resident) to fill the
+// chip; smaller L = more (shorter) blocks and more partial slots.
+inline SymGeom sym_geom(int64_t M, int nparts = 1) {
   SymGeom g;
   g.M = M;
   g.nG = (int)((M + kSymG - 1) / kSymG);
   g.nQ = (g.nG + kSymQ - 1) / kSymQ;
-  g.L = sym_L();
+  int L = sym_L();
+  if (L <= 0) {
+    L = 4;
+    while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0) L /= 2;
+  }
+  g.L = L;
   g.Kmax = (g.nG + g.L - 1) / g.L;
   g.nslot = g.nQ + 1 + g.Kmax;
   return g;
@@ -584,9 +594,9 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
 }
 
 // W = accumulators per point (SymBwd: 2D, SymFwd: 3D with the divergence, else 2D)
-inline size_t sym_ws_bytes(int64_t M, int W) {
+inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
   if (M <= 0) return 0;
-  const SymGeom g = sym_geom(M);
+  const SymGeom g = sym_geom(M, nparts);
   return (size_t)g.nslot * (size_t)M * (size_t)W * sizeof(float);
 }
 
@@ -653,8 +663,8 @@ template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
                    hipStream_t st, int part = 0, int nparts = 1) {
   if (M <= 0) return DICP_OK;
-  const SymGeom g = sym_geom(M);
-  const size_t need = sym_ws_bytes(M, 2 * D);
+  const SymGeom g = sym_geom(M, nparts);
+  const size_t need = sym_ws_bytes(M, 2 * D, nparts);
   if (ws == nullptr || wsb < need) {
     set_error("ode_self_bwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
     return DICP_ERR_WORKSPACE;

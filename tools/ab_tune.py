@@ -91,7 +91,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd"])
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL"])
     ap.add_argument("--Ms", default="20000,50000,200000", help="row counts for --mode rounds")
     a = ap.parse_args()
     if a.mode == "splits":
@@ -116,6 +116,9 @@ def main():
             for r in (1, 2):
                 variants.append((f"fwd_r{r}_s{sr}", {"r_fwd": r, "split_rounds": sr}, fwd))
                 variants.append((f"bwd_r{r}_s{sr}", {"r_bwd": r, "split_rounds": sr}, bwd))
+    elif a.mode == "symL":  # symmetric VJP column groups per workgroup (0 = automatic)
+        for L in (0, 1, 2, 4):
+            variants.append((f"bwd_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
     elif a.mode == "fwd":  # ordered vs symmetric forward (and the symmetric VJP), sym_L sweep
         variants.append(("fwd_alg0_r2", {"fwd_alg": 0, "r_fwd": 2, "split_rounds": 0}, fwd))
         for L in (2, 4, 8, 16):
