@@ -275,9 +275,10 @@ def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = 
     return v, mG, g, h
 
 
-def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=None, p_out=None):
+def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=None, p_out=None,
+               g_out=None):
     """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_f32);
-    q_out / p_out: optional contiguous destinations (must not overlap q, p)."""
+    q_out / p_out / g_out: optional contiguous destinations (must not overlap q, p)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
@@ -286,7 +287,11 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
     for t, name in ((qn, "q_out"), (pn, "p_out")):
         if not t.is_contiguous() or t.shape != q.shape or t.dtype != torch.float32:
             raise ValueError(f"{name} must be a contiguous float32 tensor shaped like q")
-    g = torch.empty(M, device=q.device, dtype=torch.float32) if (want_div or eta != 0) else None
+    g = None
+    if want_div or eta != 0:
+        g = torch.empty(M, device=q.device, dtype=torch.float32) if g_out is None else g_out
+        if not g.is_contiguous() or g.shape != (M,) or g.dtype != torch.float32:
+            raise ValueError("g_out must be a contiguous float32 (M,) tensor")
     if M == 0:
         return qn, pn, g
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, q.device)

@@ -77,6 +77,7 @@ class ShootFn(torch.autograd.Function):
             X[0].copy_(x0)
         mids = []  # Ralston intermediate states (needed by the adjoint)
         H0 = v0 = mG0 = None
+        Gd, fused_from = None, None  # fused Euler steps: per-step divergence rows, first step
         for t in range(nt):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
@@ -105,12 +106,13 @@ class ShootFn(torch.autograd.Function):
                     C[t + 1].copy_(C[t])
                 continue
             if scheme == "Euler" and not has_x and not first:
-                # fused pass: Q[t+1], P[t+1] written by the reduction's epilogue
-                _, _, g = _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1])
-                if want_div:
-                    torch.add(C[t], g.sum().reshape(1), alpha=dt, out=C[t + 1])
-                else:
-                    C[t + 1].copy_(C[t])
+                # fused pass: Q[t+1], P[t+1] written by the reduction's epilogue; the per-row
+                # divergence terms go to Gd[t] and the cost is accumulated once after the loop
+                if Gd is None:
+                    Gd = torch.empty((nt, M), device=dev, dtype=q0.dtype) if want_div else False
+                _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1],
+                                g_out=Gd[t] if want_div else None)
+                fused_from = t if fused_from is None else fused_from
                 continue
             if has_x:
                 out = _f_ext(q, p, x, sigma, eta, want_div, want_h=first)
@@ -149,6 +151,14 @@ class ShootFn(torch.autograd.Function):
                 if has_x:
                     X[t + 1].copy_(x + (0.25 * dt) * (vx + 3.0 * vx2))
                 mids.append((qi, pi, xi))
+        if fused_from is not None:
+            # cost of the fused steps: C[t+1] = C[t] + dt sum_i g_i(t), one reduction + scan
+            if want_div:
+                inc = Gd[fused_from:].sum(1, keepdim=True).mul_(dt)
+                torch.cumsum(inc, 0, out=C[fused_from + 1:])
+                C[fused_from + 1:].add_(C[fused_from])
+            else:
+                C[fused_from + 1:].copy_(C[fused_from].expand(nt - fused_from, 1))
         ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x = \
             sigma, eta, nt, scheme, want_div, has_x
         if H0 is None:  # nt == 0
@@ -191,6 +201,7 @@ class ShootFn(torch.autograd.Function):
         lc = g_or_zero(gC, nt, (1,)).clone()
         lx = g_or_zero(gX, nt, tuple(X.shape[1:])).clone() if has_x else None
 
+        lc_suffix = None
         for t in range(nt - 1, -1, -1):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
@@ -209,12 +220,16 @@ class ShootFn(torch.autograd.Function):
                     lc = lc + gC[t]
                 continue
             if scheme == "Euler" and not has_x:
-                # fused pass: lambda_t = lambda_{t+1} + dt VJP + the loss's own cotangent at t
-                lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lc if want_div else None, sigma, eta,
+                # fused pass: lambda_t = lambda_{t+1} + dt VJP + the loss's own cotangent at t;
+                # the cost cotangent at t is the suffix sum of gC (precomputed, no per-step op)
+                if gC is not None and lc_suffix is None:
+                    lc_suffix = torch.flip(torch.cumsum(torch.flip(gC, (0,)), 0), (0,))
+                lct = lc if gC is None else lc_suffix[t + 1]
+                lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lct if want_div else None, sigma, eta,
                                                  dt, None if gQ is None else gQ[t],
                                                  None if gP is None else gP[t])
                 if gC is not None:
-                    lc = lc + gC[t]
+                    lc = lc_suffix[t]
                 continue
             if scheme == "Euler":
                 gq, gp, gx = _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div)

@@ -1,11 +1,15 @@
 """L-BFGS wrapper with divergence fallback (semantics of diffICP/tools/optim.py:10-110).
 
-Kept on torch.optim.LBFGS (host-side optimizer logic, O(M) vector ops on the device); the
-closure's cost is the HIP shooting + its fused backward.
+The optimizer is torch.optim.LBFGS's algorithm (same control flow, memory rule, strong-Wolfe
+line search) with the inverse-Hessian product in compact form (tools/lbfgs.py CompactLBFGS:
+~10 device kernels per iteration instead of ~5 per stored pair); the closure's cost is the
+HIP shooting + its fused backward.
 """
 import math
 
 import torch
+
+from .lbfgs import CompactLBFGS
 
 
 def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
@@ -15,8 +19,8 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
     perturbation) and restart without line search; stop when the RMS parameter change is
     below tol x RMS parameter value."""
     p = [a.clone().contiguous().detach().requires_grad_(True) for a in p0]
-    optimizer = torch.optim.LBFGS(p, max_iter=20, max_eval=100, history_size=100,
-                                  line_search_fn="strong_wolfe")
+    optimizer = CompactLBFGS(p, max_iter=20, max_eval=100, history_size=100,
+                             line_search_fn="strong_wolfe")
     iter_L, best_L, best_p = [], math.inf, None
 
     def closure():
@@ -58,8 +62,8 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
                       f"current value, with relative strength {rmod}.")
             change = "None (divergent iteration step)"
             p = [a.detach().requires_grad_(True) for a in p]
-            optimizer = torch.optim.LBFGS(p, max_iter=20, max_eval=100, history_size=100,
-                                          line_search_fn=None)
+            optimizer = CompactLBFGS(p, max_iter=20, max_eval=100, history_size=100,
+                                     line_search_fn=None)
         else:
             changes = [((a - a_prev) ** 2).mean().sqrt().detach().cpu().numpy()
                        for a, a_prev in zip(p, p_prev)]

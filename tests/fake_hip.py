@@ -95,8 +95,11 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta):
     return _out(gq, q), _out(gp, q)
 
 
-def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None):
+def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=None):
     v, mG, g, _ = ode_self_fwd(q, p, sigma, eta, want_div)
+    if g_out is not None and g is not None:
+        g_out.copy_(g)
+        g = g_out
     qn, pn = q + dt * v, p + dt * mG
     if q_out is not None:
         q_out.copy_(qn)

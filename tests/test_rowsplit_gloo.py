@@ -94,7 +94,7 @@ def test_rowsplit_matches_single_process(world):
             ref = single[key]
             err = np.abs(res[key] - ref).max() / max(1e-12, np.abs(ref).max())
             assert err < tol, (world, rank, key, err)
-        assert abs(res["FE"] - single["FE"]) < 1e-5 * abs(single["FE"])
+        assert abs(res["FE"] - single["FE"]) < 5e-5 * abs(single["FE"])   # after L-BFGS (see a0)
     for rank, res in out[1:]:  # every rank holds bit-identical state
         for key in res:
             assert np.array_equal(res[key], out[0][1][key]), (rank, key)
