@@ -139,6 +139,15 @@ def decimate(x, R):                                   # point_sets.py:102-133, r
 # ---------------------------------------------------------------------------------------
 # LDDMM (diffICP/core/LDDMM.py:100-227, 286-334)
 # ---------------------------------------------------------------------------------------
+def data_distance(x, y, sigma, w=None):              # PSR_standard.py:37-58
+    Nx, Ny = x.shape[0], y.shape[0]
+    if w is None:
+        return (KBase(x, x, sigma).sum() / Nx ** 2 + KBase(y, y, sigma).sum() / Ny ** 2
+                - 2 * KBase(y, x, sigma).sum() / (Nx * Ny))
+    return (KBase(x, x, sigma).sum() / Nx ** 2 + (KRedScal(y, y, w, sigma) * w).sum()
+            - 2 * (KBase(y, x, sigma) * w).sum() / Nx)
+
+
 def KridgeSolve_torch(x, v, sigma, alpha):            # kernel.py:234-237 (dense ridge)
     Kxx = K(x, x, sigma)
     return torch.linalg.solve(Kxx + alpha * torch.eye(Kxx.shape[0], dtype=Kxx.dtype), v)

@@ -8,7 +8,7 @@ module is placed in sys.modules AFTER importing kernel/LDDMM (which guard their 
 GMM.use_keops is forced False: every computversion then resolves to the reference's own
 torch implementation.
 
-    python tests/golden/make_golden.py [--only c1|decim]
+    python tests/golden/make_golden.py [--only c1|decim|psr_std]
 """
 import importlib.machinery
 import os
@@ -313,6 +313,56 @@ def decim_cases():
     print("decim", os.path.getsize(os.path.join(HERE, "decim.npz")), "bytes")
 
 
+def psr_std_cases():
+    """PSR_standard: data_distance (PSR_standard.py:37-58) with and without
+    template weights, and a DiffPSR_std trace (2 frames, 2D, classic LDDMM lambda=2 as
+    standard_atlas.py, dense support): E at init, after Reg_opt(nmax=2), after
+    Template_opt(nmax=2) -- y0, a0, y1 recorded (float64, torch path)."""
+    import torch
+    K, L, G, P = import_reference()
+    import diffICP.core.PSR_standard as PS
+    f64 = torch.float64
+    spec64 = {"device": "cpu", "dtype": f64}
+    out = {}
+    g = torch.Generator().manual_seed(31)
+    for D in (2, 3):
+        x = torch.rand(70, D, generator=g, dtype=f64)
+        y = torch.rand(50, D, generator=g, dtype=f64)
+        w = torch.rand(50, generator=g, dtype=f64) / 50
+        DK = K.GaussKernel(0.15, D, computversion="torch", spec=spec64)
+        out[f"dd{D}/x"], out[f"dd{D}/y"], out[f"dd{D}/w"] = x.numpy(), y.numpy(), w.numpy()
+        out[f"dd{D}/L"] = np.array(float(PS.data_distance(DK, x, y)))
+        out[f"dd{D}/Lw"] = np.array(float(PS.data_distance(DK, x, y, w)))
+    t = torch.linspace(0, 2 * np.pi, 41, dtype=f64)[:-1]
+    y0 = torch.stack([0.5 + 0.3 * torch.cos(t), 0.5 + 0.2 * torch.sin(t)], 1)
+    xs = []
+    for k in range(2):
+        tk = torch.rand(60, generator=g, dtype=f64) * 2 * np.pi
+        xs.append(torch.stack([0.5 + (0.3 + 0.04 * k) * torch.cos(tk) + 0.03 * torch.sin(3 * tk),
+                               0.5 + (0.2 - 0.03 * k) * torch.sin(tk)], 1)
+                  + 0.01 * torch.randn(60, 2, generator=g, dtype=f64))
+    DK = K.GaussKernel(0.1, 2, computversion="torch", spec=spec64)
+    LM = L.LDDMMModel(sigma=0.2, D=2, lambd=2.0, version="classic", scheme="Euler", nt=10,
+                      computversion="torch", spec=spec64)
+    PSR = PS.DiffPSR_std([[xk] for xk in xs], y0, 0.05, LM, DK, dataspec=spec64, compspec=spec64)
+    PSR.printstuff = False
+    out["std/y0_init"] = y0.numpy()
+    for k in range(2):
+        out[f"std/x{k}"] = xs[k].numpy()
+    out["std/E_init"] = np.array(float(PSR.E))
+    PSR.Reg_opt(nmax=2, tol=1e-3)
+    out["std/E_reg"] = np.array(float(PSR.E))
+    for k in range(2):
+        out[f"std/a0_reg{k}"] = PSR.a0[k].detach().numpy()
+        out[f"std/y1_reg{k}"] = PSR.y1[k, 0].detach().numpy()
+    PSR.Template_opt(nmax=2, tol=1e-3)
+    out["std/E_tpl"] = np.array(float(PSR.E))
+    out["std/y0_tpl"] = PSR.y0[0].detach().numpy()
+    print("psr_std E", out["std/E_init"], out["std/E_reg"], out["std/E_tpl"])
+    np.savez_compressed(os.path.join(HERE, "psr_std.npz"), **out)
+    print("psr_std", os.path.getsize(os.path.join(HERE, "psr_std.npz")), "bytes")
+
+
 if __name__ == "__main__":
     only = sys.argv[2] if sys.argv[1:2] == ["--only"] else None
     if only is None:
@@ -321,3 +371,5 @@ if __name__ == "__main__":
         c1_trace()
     if only in (None, "decim"):
         decim_cases()
+    if only in (None, "psr_std"):
+        psr_std_cases()

@@ -242,3 +242,24 @@ def test_decim_psr_trace_golden(dev):
         fe = float(z[f"psr/it{it}/FE_reg"])
         assert abs(PS.FE - fe) < 2e-3 * abs(fe), (it, PS.FE, fe)
         assert rel_err(PS.x1[0, 0].cpu(), torch.from_numpy(z[f"psr/it{it}/x1"])) < 2e-3
+
+
+def test_psr_std_trace_gpu(dev):
+    """DiffPSR_std (PSR_standard.py:364-566) on the HIP path in float32 against the
+    reference's float64 trace: energies after init, Reg_opt(nmax=2), Template_opt(nmax=2)."""
+    import numpy as np
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR_standard import DiffPSR_std
+    from difficp_amd.tools.kernel import GaussKernel
+    z = np.load(os.path.join(GOLD, "psr_std.npz"))
+    spec = {"device": dev, "dtype": torch.float32}
+    t = lambda k: torch.from_numpy(z[k]).to(**spec)
+    DK = GaussKernel(0.1, 2, spec=spec)
+    LM = LDDMMModel(sigma=0.2, D=2, lambd=2.0, version="classic", scheme="Euler", nt=10, spec=spec)
+    P = DiffPSR_std([t("std/x0"), t("std/x1")], t("std/y0_init"), 0.05, LM, DK, dataspec=spec, compspec=spec)
+    P.printstuff = False
+    assert abs(P.E - float(z["std/E_init"])) < 1e-5 * abs(float(z["std/E_init"]))
+    P.Reg_opt(nmax=2, tol=1e-3)
+    assert abs(P.E - float(z["std/E_reg"])) < 2e-3 * abs(float(z["std/E_reg"])), (P.E, float(z["std/E_reg"]))
+    P.Template_opt(nmax=2, tol=1e-3)
+    assert abs(P.E - float(z["std/E_tpl"])) < 5e-3 * abs(float(z["std/E_tpl"])), (P.E, float(z["std/E_tpl"]))

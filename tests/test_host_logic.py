@@ -181,3 +181,35 @@ def test_exact_two_set_ridge_init(fake):
     assert rel_err(psr.a0[0], ref) < 1e-2   # CG stops at |r|^2 < n eps^2; cond(K + 1e-3 I) ~ 1e5
     workloads.psr_iteration(psr)
     assert psr.FE == psr.FE  # finite
+
+
+def _psr_std_from_golden(spec):
+    import numpy as np
+    import os
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR_standard import DiffPSR_std
+    from difficp_amd.tools.kernel import GaussKernel
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "psr_std.npz"))
+    t = lambda k: torch.from_numpy(z[k]).to(**spec)
+    DK = GaussKernel(0.1, 2, spec=spec)
+    LM = LDDMMModel(sigma=0.2, D=2, lambd=2.0, version="classic", scheme="Euler", nt=10, spec=spec)
+    P = DiffPSR_std([[t("std/x0")], [t("std/x1")]], t("std/y0_init"), 0.05, LM, DK,
+                    dataspec=spec, compspec=spec)
+    P.printstuff = False
+    return P, z
+
+
+def test_psr_std_trace_host_logic_fp64(fake):
+    """DiffPSR_std (PSR_standard.py:364-566): energy after init, Reg_opt(nmax=2) and
+    Template_opt(nmax=2) against the reference's trace (golden psr_std.npz), float64 host
+    logic with oracle-backed kernels (measured agreement ~1e-11)."""
+    spec = {"device": "cpu", "dtype": torch.float64}
+    P, z = _psr_std_from_golden(spec)
+    assert abs(P.E - float(z["std/E_init"])) < 1e-9 * abs(float(z["std/E_init"]))
+    P.Reg_opt(nmax=2, tol=1e-3)
+    assert abs(P.E - float(z["std/E_reg"])) < 1e-8 * abs(float(z["std/E_reg"])), (P.E, float(z["std/E_reg"]))
+    for k in range(2):
+        assert rel_err(P.y1[k, 0], torch.from_numpy(z[f"std/y1_reg{k}"])) < 1e-8
+    P.Template_opt(nmax=2, tol=1e-3)
+    assert abs(P.E - float(z["std/E_tpl"])) < 1e-8 * abs(float(z["std/E_tpl"])), (P.E, float(z["std/E_tpl"]))
+    assert rel_err(P.y0[0], torch.from_numpy(z["std/y0_tpl"])) < 1e-8

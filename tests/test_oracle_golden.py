@@ -140,3 +140,13 @@ def test_oracle_ridge_cg_matches_dense():
     ref = R.KridgeSolve_torch(x, v, 0.1, 0.5)
     assert 0 < k < 200
     assert float((b - ref).norm() / ref.norm()) < 1e-8
+
+
+def test_oracle_data_distance_vs_reference():
+    """data_distance (PSR_standard.py:37-58) against the reference's own values
+    (tests/golden/psr_std.npz), with and without template weights."""
+    z = np.load(os.path.join(GOLD, "psr_std.npz"))
+    for D in (2, 3):
+        x, y, w = (torch.from_numpy(z[f"dd{D}/{k}"]) for k in ("x", "y", "w"))
+        assert abs(float(R.data_distance(x, y, 0.15)) - float(z[f"dd{D}/L"])) < 1e-12
+        assert abs(float(R.data_distance(x, y, 0.15, w)) - float(z[f"dd{D}/Lw"])) < 1e-12
