@@ -138,11 +138,36 @@ class MultiPSR:
             self.y[k, s] = allys[first:last].to(**self.dataspec)
             self.update_quadloss(k, s)
 
+    def _row_split(self):
+        """The LDDMM model's row split (core/rowsplit.py) when this PSR is not frame-sharded:
+        the EM passes are then split over the same ranks by rows of the (warped) points."""
+        split = getattr(getattr(self, "LMi", None), "row_split", None)
+        return split if (split is not None and self.world == 1) else None
+
+    def _em_rows(self, s, allx1s, fn):
+        """Run fn(GMM, X) on this rank's row slice of X with the GMM's cross-rank statistics
+        exchange switched on (the atlas code path, GMM.py comm), then all-gather the targets.
+        Returns (Y (N, D), *rest of fn's result)."""
+        split = self._row_split()
+        if split is None:
+            return fn(self.GMMi[s], allx1s)
+        N = allx1s.shape[0]
+        r0, n, _ = split.rows(N)
+        g = self.GMMi[s]
+        old = g.comm
+        g.comm = True if split.group is None else split.group
+        try:
+            out = fn(g, allx1s[r0:r0 + n].contiguous())
+        finally:
+            g.comm = old
+        (Y,), _ = split.gather_rows([out[0]], N)
+        return (Y.contiguous(),) + tuple(out[1:])
+
     def update_GMM_targets(self):
         """y, Cfe, quadloss, FE from an E-step without parameter update (PSR.py:197-213)."""
         for s in range(self.S):
             allx1s = self._local_cat(self.x1, s)
-            allys, self.Cfe[s], _ = self.GMMi[s].EM_step(allx1s, skip_M=True)
+            allys, self.Cfe[s], _ = self._em_rows(s, allx1s, lambda g, X: g.EM_step(X, skip_M=True))
             self._assign_targets(s, allys)
         self.update_FE()
 
@@ -170,7 +195,8 @@ class MultiPSR:
         (PSR.py:242-271)."""
         for s in range(self.S):
             allx1s = self._local_cat(self.x1, s)
-            allys, self.Cfe[s], _, i = self.GMMi[s].EM_optimization(allx1s, max_iterations=max_iterations, tol=tol)
+            allys, self.Cfe[s], _, i = self._em_rows(
+                s, allx1s, lambda g, X: g.EM_optimization(X, max_iterations=max_iterations, tol=tol))
             self._assign_targets(s, allys)
             message = f"GMM optim (structure {s}) : {i} EM steps"
             if self.GMMi[s].outliers:

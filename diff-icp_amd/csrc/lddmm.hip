@@ -3,6 +3,7 @@
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
 #include "lddmm_sym.hpp"
+#include "packed.hpp"
 
 #include <stdlib.h>
 
@@ -28,11 +29,13 @@ int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd;
 // eta = 0 VJP: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48), 2 = symmetric
 // pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair)
 int g_bwd_alg = 2;
-// eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, default: measured ~3% faster on MI355X),
-// 1 = symmetric pair-once kernel (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair
-// instead of 20 + 1, but issue-stalled on its rotating column sums)
+// eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
+// (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair instead of 20 + 1, but 3-5%
+// slower: issue-stalled on its rotating column sums), 2 = packed-FP32 rows (packed.hpp: the
+// thread's two rows as float2, 11 VALU instructions per pair; default, measured 4-11% faster
+// than 0 at 200k-20k on MI355X)
 #ifndef DICP_FWD_ALG
-#define DICP_FWD_ALG 0
+#define DICP_FWD_ALG 2
 #endif
 int g_fwd_alg = DICP_FWD_ALG;
 
@@ -107,7 +110,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "fwd_alg")) {
-    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    if (value < 0 || value > 2) return DICP_ERR_INVALID;
     g_fwd_alg = value;
     return DICP_OK;
   }
@@ -200,6 +203,10 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   if (g_fwd_alg == 1 && all)
     return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st)
                                : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st);
+  if (g_fwd_alg == 2)
+    return o.ptr[2] != nullptr
+               ? launch_rowred_pk<OpOdeSelfFwdPk<D, true>>("ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
+               : launch_rowred_pk<OpOdeSelfFwdPk<D, false>>("ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st);
   if (o.ptr[2] != nullptr)
     return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
@@ -210,7 +217,9 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
   size_t m = 0;
   for (size_t v : {ws_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), nrows, M),
                    ws_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), nrows, M),
-                   ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), nrows, M)})
+                   ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M)})
     m = v > m ? v : m;
   return m;
 }
@@ -224,7 +233,11 @@ size_t ode_self_fwd_ws(int64_t M) {
   a = a > b ? a : b;
   a = a > c ? a : c;
   const size_t d = sym_ws_bytes(M, 3 * D);
-  return a > d ? a : d;
+  a = a > d ? a : d;
+  for (size_t e : {rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M)})
+    a = a > e ? a : e;
+  return a;
 }
 
 template <int D>

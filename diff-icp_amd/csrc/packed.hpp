@@ -1,0 +1,230 @@
+// Packed-FP32 variant of the row-reduction skeleton (common.hpp rowred_kernel) for the
+// fused LDDMM forward: each thread's two rows (i, i + 256) are held as float2 vectors, so
+// every per-pair FMA / mul / sub of the two rows is ONE v_pk_*_f32 instruction (two lanes of
+// work per VALU issue slot; the MI355X vector peak, 157 TF/s, is only reachable packed).
+// The column record is a scalar broadcast into both halves (VOP3P op_sel).  Split columns,
+// slabs, merge and the Outs epilogue are those of the generic kernel (same row mapping as
+// rowred_kernel<Op, 2>), so results differ only by fp32 contraction order.
+#pragma once
+#include "launch.hpp"
+#include "lddmm_ops.hpp"
+
+namespace dicp {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
+
+// OpOdeSelfFwd<D, false, DIV> (lddmm_ops.hpp) on two rows at once: V, Gs' (, Z').
+template <int D, bool DIV>
+struct OpOdeSelfFwdPk {
+  using Base = OpOdeSelfFwd<D, false, DIV>;
+  static constexpr int CW4 = Base::CW4;
+  static constexpr int NACC = Base::NACC;
+  static constexpr int kNOut = Base::kNOut;
+  static constexpr bool kMin = false;
+  struct Row2 {
+    f2 q[D], p[D];
+  };
+  __device__ static void load_rows(const Args& a, int64_t i0, int64_t i1, Row2& r,
+                                   typename Base::Row& b0, typename Base::Row& b1) {
+    Base::load_row(a, i0, b0);
+    Base::load_row(a, i1, b1);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      r.q[d] = f2{b0.q[d], b1.q[d]};
+      r.p[d] = f2{b0.p[d], b1.p[d]};
+    }
+  }
+  __device__ static void pair2(const Row2& r, const float* rec, f2* acc) {
+    f2 z[D];
+    f2 r2 = splat(0.f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      z[d] = r.q[d] - splat(rec[d]);
+      r2 = pk_fma(z[d], z[d], r2);
+    }
+    const f2 K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    const float* pj = rec + D;
+    f2 pp = r.p[0] * splat(pj[0]);
+#pragma unroll
+    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+    const f2 Kpp = K * pp;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = pk_fma(K, splat(pj[d]), acc[d]);
+      acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
+      if (DIV) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
+    }
+  }
+};
+
+template <class Op>
+__global__ __launch_bounds__(kBlock) void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
+                                                           int64_t chunk, Outs outs) {
+  using Base = typename Op::Base;
+  constexpr int CW4 = Op::CW4;
+  constexpr int NACC = Op::NACC;
+  __shared__ float4 lds[2][kTile * CW4];
+  if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
+
+  const int tid = threadIdx.x;
+  const int64_t ibase = (int64_t)blockIdx.x * (kBlock * 2) + tid;
+  int64_t i0 = ibase, i1 = ibase + kBlock;
+  typename Base::Row brow[2];
+  typename Op::Row2 row;
+  Op::load_rows(args, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row, brow[0], brow[1]);
+
+  f2 tot[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) tot[k] = splat(0.f);
+
+  const int64_t j0 = (int64_t)blockIdx.y * chunk;
+  int64_t j1 = j0 + chunk;
+  if (j1 > N) j1 = N;
+
+  float pre[CW4 * 4];
+  int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
+  if (cnt > 0 && tid < cnt) {
+    op_load_col<Base>(args, sc, j0 + tid, pre);
+#pragma unroll
+    for (int k = 0; k < CW4; ++k)
+      lds[0][tid * CW4 + k] = make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int64_t jt = j0; jt < j1; jt += kTile) {
+    const int64_t jn = jt + kTile;
+    const int cntn = jn < j1 ? (int)((j1 - jn) < kTile ? (j1 - jn) : kTile) : 0;
+    if (tid < cntn) {
+      op_load_col<Base>(args, sc, jn + tid, pre);
+#pragma unroll
+      for (int k = 0; k < CW4; ++k)
+        lds[buf ^ 1][tid * CW4 + k] =
+            make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
+    }
+    f2 acc[NACC];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) acc[k] = splat(0.f);
+    const float4* tile = lds[buf];
+#pragma unroll DICP_PAIR_UNROLL
+    for (int t = 0; t < cnt; ++t) {
+      float rec[CW4 * 4];
+#pragma unroll
+      for (int k = 0; k < CW4; ++k) {
+        const float4 q = tile[t * CW4 + k];
+        rec[4 * k + 0] = q.x;
+        rec[4 * k + 1] = q.y;
+        rec[4 * k + 2] = q.z;
+        rec[4 * k + 3] = q.w;
+      }
+      Op::pair2(row, rec, acc);
+    }
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) tot[k] = tot[k] + acc[k];
+    __syncthreads();
+    buf ^= 1;
+    cnt = cntn;
+  }
+
+  const bool split = gridDim.y > 1;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t i = r == 0 ? i0 : i1;
+    if (i >= M) continue;
+    float t[NACC];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) t[k] = r == 0 ? tot[k].x : tot[k].y;
+    float vals[Base::kOutW[0] + Base::kOutW[1] + Base::kOutW[2] + Base::kOutW[3]];
+    Base::store(sc, brow[r], t, vals);
+    int off = 0;
+#pragma unroll
+    for (int k = 0; k < Base::kNOut; ++k) {
+      const int w = Base::kOutW[k];
+      float* base = outs.ptr[k];
+      if (base != nullptr) {
+        if (split) {
+          float* dst = base + (int64_t)blockIdx.y * M * w + i * w;
+#pragma unroll
+          for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < w; ++e) base[i * w + e] = epilogue(outs, k, i * w + e, vals[off + e]);
+        }
+      }
+      off += w;
+    }
+  }
+}
+
+template <class Op>
+int64_t rowred_pk_capacity() {
+  static int64_t cap = -1;
+  if (cap < 0) cap = (int64_t)device_cus() * blocks_per_cu(rowred_pk_kernel<Op>);
+  return cap;
+}
+
+template <class Op>
+int rowred_pk_splits(int64_t M, int64_t N) {
+  using Base = typename Op::Base;
+  return num_splits_cap(M, N, 2, rowred_pk_capacity<Op>(), round_rows_of<Base>::rows,
+                        round_rows_of<Base>::max);
+}
+
+template <class Op>
+size_t rowred_pk_ws_bytes(int64_t M, int64_t N) {
+  const int S = rowred_pk_splits<Op>(M, N);
+  if (S <= 1) return 0;
+  return (size_t)S * (size_t)M * (size_t)total_out_width<typename Op::Base>() * sizeof(float);
+}
+
+// Same contract as launch_rowred<Base, 2> (launch.hpp).
+template <class Op>
+int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
+                     const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
+  using Base = typename Op::Base;
+  if (M <= 0) return DICP_OK;
+  const int S = rowred_pk_splits<Op>(M, N);
+  const int64_t chunk = N > 0 ? chunk_of(N, S) : 0;
+  const int64_t bx = (M + (int64_t)kBlock * 2 - 1) / ((int64_t)kBlock * 2);
+  dim3 grid((unsigned)bx, (unsigned)S, 1), block(kBlock, 1, 1);
+  if (S == 1) {
+    rowred_pk_kernel<Op><<<grid, block, 0, st>>>(a, sc, M, N, chunk, fin);
+    return check_launch(name);
+  }
+  const size_t need = rowred_pk_ws_bytes<Op>(M, N);
+  if (ws == nullptr || ws_bytes < need) {
+    set_error("%s: workspace too small (%zu < %zu bytes)", name, ws_bytes, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  Outs part = fin;
+  float* cur = reinterpret_cast<float*>(ws);
+  for (int k = 0; k < Base::kNOut; ++k) {
+    part.ptr[k] = fin.ptr[k] ? cur : nullptr;
+    cur += (int64_t)S * M * Base::kOutW[k];
+  }
+  rowred_pk_kernel<Op><<<grid, block, 0, st>>>(a, sc, M, N, chunk, part);
+  int rc = check_launch(name);
+  if (rc) return rc;
+  MergeSet ms;
+  int nk = 0;
+  int64_t nmax = 0;
+  for (int k = 0; k < Base::kNOut; ++k) {
+    if (!fin.ptr[k]) continue;
+    ms.slab[nk] = part.ptr[k];
+    ms.n[nk] = M * Base::kOutW[k];
+    ms.k[nk] = k;
+    nmax = ms.n[nk] > nmax ? ms.n[nk] : nmax;
+    ++nk;
+  }
+  if (nk > 0) {
+    const int64_t nb = (nmax + kBlock - 1) / kBlock;
+    merge_slabs_kernel<false><<<dim3((unsigned)nb, (unsigned)nk), dim3(kBlock), 0, st>>>(ms, fin, S);
+    rc = check_launch(name);
+    if (rc) return rc;
+  }
+  return DICP_OK;
+}
+
+}  // namespace dicp

@@ -246,7 +246,10 @@ def test_decim_psr_trace_golden(dev):
 
 def test_psr_std_trace_gpu(dev):
     """DiffPSR_std (PSR_standard.py:364-566) on the HIP path in float32 against the
-    reference's float64 trace: energies after init, Reg_opt(nmax=2), Template_opt(nmax=2)."""
+    reference's float64 trace: energies after init, Reg_opt(nmax=2), Template_opt(nmax=2).
+    Tolerance = 2 x the float32 oracle's own deviation (SURVEY 8c criterion): the data term is
+    a small difference of large kernel sums, and the oracle-backed host logic in float32
+    deviates from the float64 trace by 1.49e-3 (E_reg) and 1.83e-3 (E_tpl)."""
     import numpy as np
     from difficp_amd.core.LDDMM import LDDMMModel
     from difficp_amd.core.PSR_standard import DiffPSR_std
@@ -260,6 +263,6 @@ def test_psr_std_trace_gpu(dev):
     P.printstuff = False
     assert abs(P.E - float(z["std/E_init"])) < 1e-5 * abs(float(z["std/E_init"]))
     P.Reg_opt(nmax=2, tol=1e-3)
-    assert abs(P.E - float(z["std/E_reg"])) < 2e-3 * abs(float(z["std/E_reg"])), (P.E, float(z["std/E_reg"]))
+    assert abs(P.E - float(z["std/E_reg"])) < 3.0e-3 * abs(float(z["std/E_reg"])), (P.E, float(z["std/E_reg"]))
     P.Template_opt(nmax=2, tol=1e-3)
-    assert abs(P.E - float(z["std/E_tpl"])) < 5e-3 * abs(float(z["std/E_tpl"])), (P.E, float(z["std/E_tpl"]))
+    assert abs(P.E - float(z["std/E_tpl"])) < 3.7e-3 * abs(float(z["std/E_tpl"])), (P.E, float(z["std/E_tpl"]))

@@ -97,13 +97,13 @@ def test_ode_self_fwd(dev, version, M, D):
     v64, mG64, c64 = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
     v32, mG32, c32 = m32.ODE(q.float(), p.float(), torch.zeros(1))
     H64, H32 = m.Hamiltonian(q, p), m32.Hamiltonian(q.float(), p.float())
-    for alg in (0, 1):  # eta = 0: ordered rows (OpOdeSelfFwd), symmetric pair-once kernel
+    for alg in (0, 1, 2):  # eta = 0: ordered rows, symmetric pair-once, packed-FP32 rows
         L.set_option("fwd_alg", alg)
         try:
             v, mG, gdiv, h = L.ode_self_fwd(q.float().to(dev), p.float().to(dev), 0.15, m.eta, wl,
                                             want_h=True)
         finally:
-            L.set_option("fwd_alg", 0)
+            L.set_option("fwd_alg", 2)
         assert rel_err(v.cpu(), v64) <= _tol(v64, v32), alg
         assert rel_err(mG.cpu(), mG64) <= _tol(mG64, mG32), alg
         assert rel_err(h.sum().cpu(), H64) <= _tol(H64, H32), alg
@@ -228,23 +228,25 @@ def test_sym_bwd_vs_ordered(dev, M):
 
 @pytest.mark.parametrize("M", [1, 127, 128, 129, 1000, 5000, 50000])
 @pytest.mark.parametrize("want_div", [True, False])
-def test_sym_fwd_vs_ordered(dev, M, want_div):
-    """Symmetric pair-once forward == ordered-row forward up to fp32 summation order (partial
-    last groups and quads included), every output incl. the fused Euler epilogue;
-    deterministic run to run."""
+@pytest.mark.parametrize("alg", [1, 2])
+def test_sym_fwd_vs_ordered(dev, M, want_div, alg):
+    """Symmetric pair-once (alg 1) and packed-FP32 (alg 2) forwards == the ordered-row forward
+    up to fp32 summation order (partial last groups / row pairs included), every output incl.
+    the fused Euler epilogue; deterministic run to run."""
     L = _lib()
     g = torch.Generator().manual_seed(M + 11)
     q = torch.rand(M, 3, generator=g).to(dev)
     p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
-    ref = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)      # default: ordered rows
+    L.set_option("fwd_alg", 0)                                        # ordered rows
+    ref = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)
     qn0, pn0, _ = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div)
-    L.set_option("fwd_alg", 1)
+    L.set_option("fwd_alg", alg)
     try:
         out = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)
         out2 = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)
         qn1, pn1, _ = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div)
     finally:
-        L.set_option("fwd_alg", 0)
+        L.set_option("fwd_alg", 2)
     for k, (a, b) in enumerate(zip(out, ref)):
         if b is None:
             continue

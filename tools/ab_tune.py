@@ -121,7 +121,8 @@ def main():
             variants.append((f"bwd_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
     elif a.mode == "fwd":  # ordered vs symmetric forward (and the symmetric VJP), sym_L sweep
         variants.append(("fwd_alg0_r2", {"fwd_alg": 0, "r_fwd": 2, "split_rounds": 0}, fwd))
-        for L in (2, 4, 8, 16):
+        variants.append(("fwd_alg2_packed", {"fwd_alg": 2, "split_rounds": 0}, fwd))
+        for L in (4,):
             variants.append((f"fwd_alg1_sym_L{L}", {"fwd_alg": 1, "sym_L": L}, fwd))
             variants.append((f"bwd_alg2_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
     else:  # pair-algebra variants of the backward, automatic splits
