@@ -29,6 +29,11 @@ int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd;
 // eta = 0 VJP: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48), 2 = symmetric
 // pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair)
 int g_bwd_alg = 2;
+// eta != 0 VJP: 0 = ordered OpOdeSelfBwdEta, 1 = symmetric pair-once SymBwdEta (lddmm_sym.hpp)
+#ifndef DICP_BWD_ETA_ALG
+#define DICP_BWD_ETA_ALG 1
+#endif
+int g_bwd_eta_alg = DICP_BWD_ETA_ALG;
 // eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
 // (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair instead of 20 + 1, but 3-5%
 // slower: issue-stalled on its rotating column sums), 2 = packed-FP32 rows (packed.hpp: the
@@ -112,6 +117,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
   if (!strcmp(name, "fwd_alg")) {
     if (value < 0 || value > 2) return DICP_ERR_INVALID;
     g_fwd_alg = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "bwd_eta_alg")) {
+    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    g_bwd_eta_alg = value;
     return DICP_OK;
   }
   if (!strcmp(name, "bwd_alg")) {
@@ -248,6 +258,7 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   if (eta != 0.0) {
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
+    if (g_bwd_eta_alg == 1) return launch_sym_bwd_eta<D>(a, sc, M, o, ws, wsb, st);
     return launch_r<OpOdeSelfBwdEta<D>>(r_bwd(), "ode_self_bwd_eta", a, sc, M, M, o, ws, wsb, st);
   }
   Scal sc = make_scal(sigma, 0.0);
@@ -583,7 +594,7 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
       size_t c = D == 2 ? ws_r<OpOdeSelfBwd2<2>>(r_bwd(), M, M) : ws_r<OpOdeSelfBwd2<3>>(r_bwd(), M, M);
       a = a > b ? a : b;
       a = a > c ? a : c;
-      const size_t d = sym_ws_bytes(M, 2 * D);
+      const size_t d = sym_ws_bytes(M, 2 * D);  // SymBwd and SymBwdEta: W = 2D
       return a > d ? a : d;
     }
     case DICP_WS_ODE_EXT_FWD: return D == 2 ? ode_ext_fwd_ws<2>(N, M) : ode_ext_fwd_ws<3>(N, M);

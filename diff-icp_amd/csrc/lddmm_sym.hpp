@@ -271,6 +271,119 @@ struct SymFwd {
   }
 };
 
+// Symmetric (pair-once) VJP with gradcomponent (eta != 0, the "logdet" model, e.g. the
+// exact ICP_two_set model): the pair algebra of OpOdeSelfBwdEta (lddmm_ops.hpp).  Under
+// (m, j) -> (j, m): z, da, db, dp flip sign; r2, pp, ap, zb, zp, za, bp, Phi and the
+// coefficients cz_p, cz_q, cdb are symmetric.  Hence per unordered pair
+//   gp_m += K a_j + K s zb p_j + T,   gp_j += K a_m + K s zb p_m - T,  T = K (cz_p z - es db)
+//   gq_m += G,                         gq_j -= G,   G = K (es da + cdb db + (es2 zb - gs) dp + cz_q z)
+// Accumulators: [gp (D), gq (D)] unscaled (merge with s = alpha = 1).
+// Padding points sit at kFarEta = 1e4 (not 1e12): the eta algebra multiplies up to ~|z|^4 s^3
+// before the factor K = 0 is applied, which must stay finite (0 * inf = NaN); K = exp2(nc r2)
+// underflows to 0 at r2 ~ 3e8 for any sigma < ~1e3.
+constexpr float kFarEta = 1.0e4f;
+template <int D>
+struct SymBwdEta {
+  static constexpr int kMaxWaves = 8;
+  static constexpr int CW = cw4(4 * D);
+  static constexpr int kUsed = 4 * D;
+  static constexpr int W = 2 * D;
+  struct Prm {
+    float nc, s, es, es2, e2s2, gs, gam;
+  };
+  __device__ static Prm params(const Args&, const Scal& sc) {
+    const float es = sc.eta * sc.s, es2 = es * sc.s;
+    return Prm{sc.nc, sc.s, es, es2, sc.eta * es2, sc.aux0 * sc.s, sc.aux0};
+  }
+  struct Row {
+    float q[D], p[D], a[D], b[D];
+  };
+  __device__ static void load_row(const Args& a, const Scal&, int64_t i, bool valid, Row& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      r.q[d] = valid ? a.r0[i * D + d] : kFarEta;
+      r.p[d] = valid ? a.r1[i * D + d] : 0.f;
+      r.a[d] = valid ? a.r2[i * D + d] : 0.f;
+      r.b[d] = valid ? a.r3[i * D + d] : 0.f;
+    }
+  }
+  __device__ static void load_col(const Args& a, const Scal&, int64_t j, bool valid, float* rec) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      rec[d] = valid ? a.c0[j * D + d] : kFarEta;
+      rec[D + d] = valid ? a.c1[j * D + d] : 0.f;
+      rec[2 * D + d] = valid ? a.c2[j * D + d] : 0.f;
+      rec[3 * D + d] = valid ? a.c3[j * D + d] : 0.f;
+    }
+#pragma unroll
+    for (int k = 4 * D; k < 4 * CW; ++k) rec[k] = 0.f;
+  }
+  struct Shared {
+    float z[D], db[D], da[D], dp[D];
+    float K, szbK, czp, es_db_c;  // K, K s zb
+    float cdb, cdp, czq;
+  };
+  __device__ static void shared_terms(const Prm& P, const Row& r, const float* rec, Shared& t) {
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+    float r2 = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      t.z[d] = r.q[d] - rec[d];
+      r2 = fmaf(t.z[d], t.z[d], r2);
+      t.da[d] = r.a[d] - aj[d];
+      t.db[d] = r.b[d] - bj[d];
+      t.dp[d] = r.p[d] - pj[d];
+    }
+    t.K = fast_exp2(P.nc * r2);
+    const float pp = dot<D>(r.p, pj);
+    const float ap = dot<D>(r.a, pj) + dot<D>(aj, r.p);
+    const float zb = dot<D>(t.z, t.db), zp = dot<D>(t.z, t.dp), za = dot<D>(t.z, t.da);
+    const float bp = dot<D>(t.db, t.dp);
+    const float sr2 = P.s * r2;
+    const float Phi = ap + P.es * za + P.s * pp * zb + P.es * (P.s * zp * zb - bp) -
+                      P.e2s2 * zb * (sr2 - (float)(D + 2)) - P.gs * zp +
+                      2.f * P.gam * P.es * (sr2 - (float)D);
+    t.czp = P.s * zb * P.es - P.gs;
+    t.czq = -2.f * P.e2s2 * P.s * zb + 4.f * P.gam * P.es2 - P.s * Phi;
+    t.cdb = P.s * pp + P.es2 * zp - P.e2s2 * (sr2 - (float)(D + 2));
+    t.cdp = P.es2 * zb - P.gs;
+    t.szbK = P.s * zb * t.K;
+  }
+  // ordered pair (m, j), row side only (diag blocks, self pair included)
+  __device__ static void pair_row(const Prm& P, const Row& r, const float* rec, float* acc) {
+    Shared t;
+    shared_terms(P, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float Tv = fmaf(t.czp, t.z[d], -P.es * t.db[d]);
+      acc[d] = fmaf(t.K, aj[d] + Tv, fmaf(t.szbK, pj[d], acc[d]));
+      const float G = fmaf(P.es, t.da[d], fmaf(t.cdb, t.db[d], fmaf(t.cdp, t.dp[d], t.czq * t.z[d])));
+      acc[D + d] = fmaf(t.K, G, acc[D + d]);
+    }
+  }
+  template <bool FIRST>
+  __device__ static void pair_sym(const Prm& P, const Row& r, const float* rec, float* acc, float* ct) {
+    Shared t;
+    shared_terms(P, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float Tv = fmaf(t.czp, t.z[d], -P.es * t.db[d]);
+      const float G = t.K * fmaf(P.es, t.da[d], fmaf(t.cdb, t.db[d], fmaf(t.cdp, t.dp[d], t.czq * t.z[d])));
+      acc[d] = fmaf(t.K, aj[d] + Tv, fmaf(t.szbK, pj[d], acc[d]));
+      acc[D + d] += G;
+      const float cgp = fmaf(t.K, r.a[d] - Tv, t.szbK * r.p[d]);
+      ct[d] = FIRST ? cgp : ct[d] + cgp;
+      ct[D + d] = FIRST ? -G : ct[D + d] - G;
+    }
+  }
+};
+
 __device__ __forceinline__ float rol1(float x) {
   // wave_rol:1 -- lane l receives lane (l + 1) mod 64
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x134, 0xF, 0xF, false));
@@ -567,7 +680,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxW
 // Pair-subset mode (row-split over ranks): only the quads Q = qoff (mod qstride) ran, so a
 // row of quad Q_T sums its column slots Q <= Q_T of those quads and, if Q_T is one of them,
 // its row slots; (qoff, qstride) = (0, 1) is every slot in slot order.
-template <int D>
+template <int D, bool kPart>
 __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
                                                         int64_t slot_stride, int64_t M, int nG,
                                                         int L, float s, float alpha, Outs o,
@@ -578,12 +691,18 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
   const int64_t row = e / W;
   const int c = (int)(e - row * W);
   const int T = (int)(row / kSymG);
-  const int QT = T / kSymQ;
   const int ns = sym_nslots(T, nG, L);
-  float acc = 0.f;
-  for (int q = qoff; q <= QT; q += qstride) acc += slab[(int64_t)q * slot_stride + e];
-  if (QT >= qoff && (QT - qoff) % qstride == 0)
-    for (int t = QT + 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
+  float acc;
+  if constexpr (!kPart) {
+    acc = slab[e];
+    for (int t = 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
+  } else {
+    const int QT = T / kSymQ;
+    acc = 0.f;
+    for (int q = qoff; q <= QT; q += qstride) acc += slab[(int64_t)q * slot_stride + e];
+    if (QT >= qoff && (QT - qoff) % qstride == 0)
+      for (int t = QT + 1; t < ns; ++t) acc += slab[(int64_t)t * slot_stride + e];
+  }
   if (c < D) {
     const int64_t idx = row * D + c;
     o.ptr[1][idx] = epilogue(o, 1, idx, alpha * acc);
@@ -660,6 +779,33 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
 }
 
 template <int D>
+int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws,
+                       size_t wsb, hipStream_t st) {
+  using S = SymBwdEta<D>;
+  if (M <= 0) return DICP_OK;
+  const SymGeom g = sym_geom(M);
+  const size_t need = sym_ws_bytes(M, S::W);
+  if (ws == nullptr || wsb < need) {
+    set_error("ode_self_bwd(sym eta): workspace too small (%zu < %zu bytes)", wsb, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  if (o.ptr[0] == nullptr || o.ptr[1] == nullptr) {
+    set_error("ode_self_bwd(sym eta): both outputs are required");
+    return DICP_ERR_INVALID;
+  }
+  float* slab = reinterpret_cast<float*>(ws);
+  const int64_t stride = M * S::W;
+  sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
+                                                                              slab, stride);
+  int rc = check_launch("ode_self_bwd(sym eta)");
+  if (rc) return rc;
+  const int64_t n = M * S::W;
+  sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+      slab, stride, M, g.nG, g.L, 1.f, 1.f, o, 0, 1);
+  return check_launch("ode_self_bwd(sym eta merge)");
+}
+
+template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
                    hipStream_t st, int part = 0, int nparts = 1) {
   if (M <= 0) return DICP_OK;
@@ -683,8 +829,12 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     if (rc) return rc;
   }
   const int64_t n = M * 2 * D;
-  sym_merge_kernel<D><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-      slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts);
+  if (nparts > 1)
+    sym_merge_kernel<D, true><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts);
+  else
+    sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1);
   return check_launch("ode_self_bwd(sym merge)");
 }
 

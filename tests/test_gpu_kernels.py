@@ -255,3 +255,26 @@ def test_sym_fwd_vs_ordered(dev, M, want_div, alg):
         if a is not None:
             assert torch.equal(a, b)
     assert rel_err(qn1, qn0) < 1e-7 and rel_err(pn1, pn0) < 2e-6
+
+
+@pytest.mark.parametrize("M", [1, 128, 129, 1000, 5000, 50000])
+def test_sym_bwd_eta_vs_ordered(dev, M):
+    """Symmetric pair-once eta != 0 VJP (SymBwdEta) == the ordered OpOdeSelfBwdEta up to fp32
+    summation order, incl. partial last groups; deterministic run to run."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 5)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    a = torch.randn(M, 3, generator=g).to(dev)
+    b = torch.randn(M, 3, generator=g).to(dev)
+    gd = torch.full((1,), -0.4, device=dev)
+    L.set_option("bwd_eta_alg", 0)
+    try:
+        gq0, gp0 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3)
+    finally:
+        L.set_option("bwd_eta_alg", 1)
+    gq1, gp1 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3)
+    gq2, gp2 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3)
+    assert torch.isfinite(gq1).all() and torch.isfinite(gp1).all()
+    assert rel_err(gq1, gq0) < 5e-6 and rel_err(gp1, gp0) < 5e-6, (rel_err(gq1, gq0), rel_err(gp1, gp0))
+    assert torch.equal(gq1, gq2) and torch.equal(gp1, gp2)

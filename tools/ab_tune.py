@@ -91,7 +91,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL"])
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL", "eta"])
     ap.add_argument("--Ms", default="20000,50000,200000", help="row counts for --mode rounds")
     a = ap.parse_args()
     if a.mode == "splits":
@@ -116,6 +116,11 @@ def main():
             for r in (1, 2):
                 variants.append((f"fwd_r{r}_s{sr}", {"r_fwd": r, "split_rounds": sr}, fwd))
                 variants.append((f"bwd_r{r}_s{sr}", {"r_bwd": r, "split_rounds": sr}, bwd))
+    elif a.mode == "eta":  # eta != 0 VJP: ordered vs symmetric pair-once
+        bwde = lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 1e-3)
+        variants.append(("bwd_eta_ordered", {"bwd_eta_alg": 0}, bwde))
+        variants.append(("bwd_eta_sym", {"bwd_eta_alg": 1}, bwde))
+        variants.append(("bwd_eta0_sym", {"bwd_eta_alg": 1}, bwd))
     elif a.mode == "symL":  # symmetric VJP column groups per workgroup (0 = automatic)
         for L in (0, 1, 2, 4):
             variants.append((f"bwd_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
