@@ -236,6 +236,7 @@ class DiffPSR(MultiPSR):
         self.support_scheme, self.rho = None, None
         self.q0 = self.allx0
         self.a0 = [None] * self.K
+        self.concurrent_frames = None   # Reg_opt host threads / HIP streams (None = automatic)
         self.initialize_a0()
 
     def initialize_a0(self, **v2p_args):
@@ -310,18 +311,48 @@ class DiffPSR(MultiPSR):
             return ((x - y) ** 2 / (2 * sig2[:, None])).sum()
         return dataloss_func
 
+    def _optimize_frame(self, k, nmax, tol):
+        if self.support_scheme is None:
+            return self.LMi.Optimize(self.QuadLossFunctor(k), self.q0[k], self.a0[k], tol=tol, nmax=nmax)
+        return self.LMi.Optimize(self.QuadLossFunctor(k), self.q0[k], self.a0[k], self.allx0[k],
+                                 tol=tol, nmax=nmax)
+
+    def _optimize_frames(self, nmax, tol):
+        """{k: Optimize(...)} for the local frames.  With `concurrent_frames` > 1 (default on a
+        HIP device: up to 4) the frames' independent L-BFGS runs are driven by that many host
+        threads, each on its own HIP stream, so one frame's host-side work (L-BFGS logic,
+        launches, .item() syncs) overlaps the others' kernels; every frame's computation is
+        unchanged, so the results are bitwise those of the sequential loop (PSR.py:528)."""
+        frames = list(self.frames)
+        nconc = getattr(self, "concurrent_frames", None)
+        if nconc is None:
+            nconc = 4 if str(self.compspec.get("device", "cpu")).startswith("cuda") else 1
+        nconc = min(int(nconc), len(frames))
+        if nconc <= 1 or self.LMi.row_split is not None:
+            return {k: self._optimize_frame(k, nmax, tol) for k in frames}
+        from concurrent.futures import ThreadPoolExecutor
+        main = torch.cuda.current_stream()
+        streams = [torch.cuda.Stream() for _ in range(nconc)]
+        for st in streams:
+            st.wait_stream(main)        # inputs (q0, a0, targets) were produced on `main`
+
+        def work(i_k):
+            i, k = i_k
+            st = streams[i % nconc]
+            with torch.cuda.stream(st):
+                out = self._optimize_frame(k, nmax, tol)
+            st.synchronize()            # results are consumed on `main` afterwards
+            return k, out
+
+        with ThreadPoolExecutor(max_workers=nconc) as ex:
+            return dict(ex.map(work, list(enumerate(frames))))
+
     def Reg_opt(self, nmax=10, tol=1e-3):
         """Per-frame LDDMM optimisation (PSR.py:521-569), local frames only when sharded."""
+        results = self._optimize_frames(nmax, tol)
         for k in self.frames:
-            if self.support_scheme is None:
-                self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
-                    self.LMi.Optimize(self.QuadLossFunctor(k), self.q0[k], self.a0[k], tol=tol, nmax=nmax)
-                allx1k = self.shoot[k][-1][0]
-            else:
-                self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
-                    self.LMi.Optimize(self.QuadLossFunctor(k), self.q0[k], self.a0[k],
-                                      self.allx0[k], tol=tol, nmax=nmax)
-                allx1k = self.shoot[k][-1][-1]
+            self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = results[k]
+            allx1k = self.shoot[k][-1][0] if self.support_scheme is None else self.shoot[k][-1][-1]
             last = 0
             for s in range(self.S):
                 first, last = last, last + int(self.N[k, s])

@@ -137,3 +137,20 @@ def test_kernel_autograd(dev, D):
         gg = torch.autograd.grad((outg * _f(wt, dev)).sum(), [insg[i] for i in which])
         for a, b_ in zip(gg, grads64):
             assert rel_err(a.cpu(), b_) < 2e-5, (name, rel_err(a.cpu(), b_))
+
+
+def test_concurrent_frames_bitwise_equal_sequential(dev):
+    """Reg_opt with the frames driven concurrently (host threads, one HIP stream each) gives
+    bitwise the same momenta, trajectories and free energy as the sequential frame loop
+    (PSR.py:528), since every frame's computation is unchanged and deterministic."""
+    from difficp_amd import workloads
+    out = []
+    for conc in (1, 4):
+        psr = workloads.build_atlas(4, 1500, 32, dev, seed=3)
+        psr.concurrent_frames = conc
+        workloads.psr_iteration(psr, max_repeat_GMM=3, tol=1e-6)
+        out.append((psr.FE, [a.detach().cpu().clone() for a in psr.a0],
+                    [psr.x1[k, 0].detach().cpu().clone() for k in range(4)]))
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1] + out[0][2], out[1][1] + out[1][2]):
+        assert torch.equal(a, b)
