@@ -278,6 +278,8 @@ template <int D>
 int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const float* gmG,
                         const float* gdiv, int64_t M, double sigma, double eta, int part,
                         int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
+  if (nparts == 1)  // the whole VJP: exactly the single-device kernel
+    return ode_self_bwd_d<D>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, wsb, st);
   if (eta == 0.0 && g_bwd_alg == 2) {
     Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
     Scal sc = make_scal(sigma, 0.0);
