@@ -8,7 +8,7 @@ module is placed in sys.modules AFTER importing kernel/LDDMM (which guard their 
 GMM.use_keops is forced False: every computversion then resolves to the reference's own
 torch implementation.
 
-    python tests/golden/make_golden.py [--only c1|decim|psr_std]
+    python tests/golden/make_golden.py [--only c1|decim|psr_std|chui]
 """
 import importlib.machinery
 import os
@@ -363,6 +363,42 @@ def psr_std_cases():
     print("psr_std", os.path.getsize(os.path.join(HERE, "psr_std.npz")), "bytes")
 
 
+def chui_case():
+    """SURVEY 8c fixture "one Chui dataset (ex3) two-set trace": the reference's own data file
+    (diffICP/examples/chui-data/demodata_ex3.mat, read as data), DiffPSR with the ICP_two_set
+    defaults (ICP_two_set.py:140-207: GMM on xB, sigma 0.1 optimised, mu / w fixed; LDDMM
+    sigma 0.2, hybrid (withlogdet, gradcomponent False), Euler nt=10, grid support rho=1;
+    lambda fixed at 1e2 since "auto" needs the affine calibration); 4 iterations of
+    GMM_opt(10, tol 1e-3) + Reg_opt(nmax=1, tol 1e-3) (ICP_two_set.py:254-282), float64."""
+    import scipy.io
+    import torch
+    K, L, G, P = import_reference()
+    f64 = torch.float64
+    spec64 = {"device": "cpu", "dtype": f64}
+    yo = scipy.io.loadmat(os.path.join(REF, "diffICP/examples/chui-data/demodata_ex3.mat"))
+    xA = torch.tensor(yo["x3"], dtype=f64).contiguous()
+    xB = torch.tensor(yo["y3"], dtype=f64).contiguous()
+    GM = G.GaussianMixtureUnif(xB, sigma=0.1, computversion="torch", spec=spec64)
+    GM.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
+    LM = L.LDDMMModel(sigma=0.2, D=2, lambd=1e2, withlogdet=True, gradcomponent=False,
+                      computversion="torch", scheme="Euler", nt=10, spec=spec64)
+    PSR = P.DiffPSR([[xA]], GM, LM, dataspec=spec64, compspec=spec64)
+    PSR.printstuff = False
+    PSR.set_support_scheme("grid", rho=1.0)
+    out = {"xA": xA.numpy(), "xB": xB.numpy(), "q0": PSR.q0[0].numpy(), "FE_init": np.array(float(PSR.FE))}
+    for it in range(4):
+        PSR.GMM_opt(max_iterations=10, tol=1e-3)
+        out[f"it{it}/FE_gmm"] = np.array(float(PSR.FE))
+        out[f"it{it}/sigma"] = np.array(float(PSR.GMMi[0].sigma))
+        PSR.Reg_opt(tol=1e-3, nmax=1)
+        out[f"it{it}/FE_reg"] = np.array(float(PSR.FE))
+        out[f"it{it}/x1"] = PSR.x1[0, 0].numpy()
+        out[f"it{it}/a0"] = PSR.a0[0].detach().numpy()
+        print("chui it", it, float(PSR.FE), float(PSR.GMMi[0].sigma))
+    np.savez_compressed(os.path.join(HERE, "chui_ex3.npz"), **out)
+    print("chui", os.path.getsize(os.path.join(HERE, "chui_ex3.npz")), "bytes")
+
+
 if __name__ == "__main__":
     only = sys.argv[2] if sys.argv[1:2] == ["--only"] else None
     if only is None:
@@ -373,3 +409,5 @@ if __name__ == "__main__":
         decim_cases()
     if only in (None, "psr_std"):
         psr_std_cases()
+    if only in (None, "chui"):
+        chui_case()

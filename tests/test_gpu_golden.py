@@ -266,3 +266,24 @@ def test_psr_std_trace_gpu(dev):
     assert abs(P.E - float(z["std/E_reg"])) < 3.0e-3 * abs(float(z["std/E_reg"])), (P.E, float(z["std/E_reg"]))
     P.Template_opt(nmax=2, tol=1e-3)
     assert abs(P.E - float(z["std/E_tpl"])) < 3.7e-3 * abs(float(z["std/E_tpl"])), (P.E, float(z["std/E_tpl"]))
+
+
+def test_chui_ex3_trace_gpu(dev):
+    """SURVEY 8c fixture: the reference's Chui ex3 two-set trace (ICP_two_set defaults, grid
+    support, hybrid model, 4 iterations) on the HIP path in float32.  Tolerances = 2 x the
+    float32 oracle's own deviation from the float64 trace (measured: FE <= 1.06e-3, sigma
+    <= 1.45e-3, x1 <= 2.23e-3 relative over the 4 iterations)."""
+    import chui_case
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            assert rel_err(PS.q0[0].cpu(), torch.from_numpy(z["q0"])) < 1e-6
+            assert abs(PS.FE - float(z["FE_init"])) < 1e-4 * abs(float(z["FE_init"]))
+            return
+        fe = float(z[f"it{it}/FE_{stage}"])
+        assert abs(PS.FE - fe) < 2.2e-3 * abs(fe), (stage, it, PS.FE, fe)
+        if stage == "gmm":
+            assert abs(PS.GMMi[0].sigma - float(z[f"it{it}/sigma"])) < 3e-3 * float(z[f"it{it}/sigma"])
+        else:
+            assert rel_err(PS.x1[0, 0].cpu(), torch.from_numpy(z[f"it{it}/x1"])) < 4.5e-3, (it,)
+    chui_case.run_chui(spec(dev), iters=4, check=check)

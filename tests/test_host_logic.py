@@ -226,3 +226,43 @@ def test_psr_std_fp32_oracle_deviation(fake):
     P.Template_opt(nmax=2, tol=1e-3)
     e_tpl = abs(P.E - float(z["std/E_tpl"])) / abs(float(z["std/E_tpl"]))
     assert e_reg < 1.5e-3 and e_tpl < 1.85e-3, (e_reg, e_tpl)
+
+
+def test_chui_ex3_trace_host_logic_fp64(fake):
+    """The reference's Chui ex3 two-set trace (ICP_two_set defaults, grid support, hybrid
+    model) replayed in float64 with oracle-backed kernels."""
+    import chui_case
+    spec = {"device": "cpu", "dtype": torch.float64}
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            assert rel_err(PS.q0[0], torch.from_numpy(z["q0"])) < 1e-12
+            assert abs(PS.FE - float(z["FE_init"])) < 1e-9 * abs(float(z["FE_init"]))
+            return
+        fe = float(z[f"it{it}/FE_{stage}"])
+        assert abs(PS.FE - fe) < 1e-6 * abs(fe), (stage, it, PS.FE, fe)
+        if stage == "gmm":
+            assert abs(PS.GMMi[0].sigma - float(z[f"it{it}/sigma"])) < 1e-6 * float(z[f"it{it}/sigma"])
+        else:
+            assert rel_err(PS.x1[0, 0], torch.from_numpy(z[f"it{it}/x1"])) < 1e-6
+    chui_case.run_chui(spec, iters=4, check=check)
+
+
+def test_chui_fp32_oracle_deviation(fake):
+    """Pins the float32 deviation that sets test_gpu_golden.py::test_chui_ex3_trace_gpu's
+    tolerances (2 x these)."""
+    import chui_case
+    worst = {"fe": 0.0, "sigma": 0.0, "x1": 0.0}
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            return
+        fe = float(z[f"it{it}/FE_{stage}"])
+        worst["fe"] = max(worst["fe"], abs(PS.FE - fe) / abs(fe))
+        if stage == "gmm":
+            worst["sigma"] = max(worst["sigma"], abs(PS.GMMi[0].sigma - float(z[f"it{it}/sigma"]))
+                                 / float(z[f"it{it}/sigma"]))
+        else:
+            worst["x1"] = max(worst["x1"], rel_err(PS.x1[0, 0], torch.from_numpy(z[f"it{it}/x1"])))
+    chui_case.run_chui({"device": "cpu", "dtype": torch.float32}, iters=4, check=check)
+    assert worst["fe"] < 1.1e-3 and worst["sigma"] < 1.5e-3 and worst["x1"] < 2.25e-3, worst
