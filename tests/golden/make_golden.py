@@ -363,6 +363,40 @@ def psr_std_cases():
     print("psr_std", os.path.getsize(os.path.join(HERE, "psr_std.npz")), "bytes")
 
 
+def reductions_large():
+    """The (M, N) = (1000, 700) per-operator fixtures of SURVEY 8c (D = 3 / sigma 0.05 and
+    D = 2 / sigma 1.0), same layout as reductions.npz."""
+    import torch
+    K, L, G, P = import_reference()
+    f64 = torch.float64
+    red = {}
+    for (M, N, D, sig) in [(1000, 700, 3, 0.05), (1000, 700, 2, 1.0)]:
+        key = f"M{M}_N{N}_D{D}_s{sig}"
+        g = torch.Generator().manual_seed(M * 7 + N + D)
+        x = torch.rand(M, D, generator=g, dtype=f64)
+        y = torch.rand(N, D, generator=g, dtype=f64)
+        b = torch.randn(N, D, generator=g, dtype=f64)
+        c = torch.randn(M, D, generator=g, dtype=f64)
+        d = torch.randn(N, generator=g, dtype=f64)
+        dm = torch.randn(M, D, generator=g, dtype=f64)
+        GK = K.GaussKernel(sig, D, computversion="torch", spec={"device": "cpu", "dtype": f64})
+        for nm, t in dict(x=x, y=y, b=b, c=c, d=d, dm=dm).items():
+            red[f"{key}/in_{nm}"] = t.numpy()
+        red[f"{key}/sigma"] = np.array(sig)
+        red[f"{key}/KBase"] = GK.KBase(x, y).numpy()
+        red[f"{key}/KRedScal"] = GK.KRedScal(x, y, d).numpy()
+        red[f"{key}/KRed"] = GK.KRed(x, y, b).numpy()
+        red[f"{key}/GradKRed"] = GK.GradKRed(x, y).numpy()
+        red[f"{key}/GradKRed_rev"] = GK.GradKRed_rev(x, y, dm).numpy()
+        red[f"{key}/DDKRed"] = GK.DDKRed(x, y, b).numpy()
+        red[f"{key}/GenDKRed"] = GK.GenDKRed(x, y, b, c).numpy()
+        red[f"{key}/HessKRed"] = GK.HessKRed(x, y, b, c).numpy()
+        red[f"{key}/LapKRed"] = GK.LapKRed(x, y).numpy()
+        red[f"{key}/GradLapKRed"] = GK.GradLapKRed(x, y).numpy()
+    np.savez_compressed(os.path.join(HERE, "reductions_large.npz"), **red)
+    print("reductions_large", os.path.getsize(os.path.join(HERE, "reductions_large.npz")), "bytes")
+
+
 def chui_case():
     """SURVEY 8c fixture "one Chui dataset (ex3) two-set trace": the reference's own data file
     (diffICP/examples/chui-data/demodata_ex3.mat, read as data), DiffPSR with the ICP_two_set
@@ -411,3 +445,5 @@ if __name__ == "__main__":
         psr_std_cases()
     if only in (None, "chui"):
         chui_case()
+    if only in (None, "red_large"):
+        reductions_large()

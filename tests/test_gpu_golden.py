@@ -32,9 +32,10 @@ def spec(dev):
     return {"device": dev, "dtype": torch.float32}
 
 
-def test_reductions_golden(dev):
+@pytest.mark.parametrize("fname", ["reductions", "reductions_large"])
+def test_reductions_golden(dev, fname):
     from difficp_amd.tools.kernel import GaussKernel
-    z = load("reductions")
+    z = load(fname)
     for key in keys(z, "/KRed"):
         x, y, b, c, d, dm = (G(z, f"{key}/in_{n}", dev) for n in ("x", "y", "b", "c", "d", "dm"))
         s = float(z[f"{key}/sigma"])

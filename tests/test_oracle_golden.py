@@ -24,8 +24,9 @@ def keys(z, suffix):
     return sorted({k.split("/")[0] for k in z.files if k.endswith(suffix)})
 
 
-def test_reductions_oracle_vs_reference():
-    z = load("reductions")
+@pytest.mark.parametrize("fname", ["reductions", "reductions_large"])
+def test_reductions_oracle_vs_reference(fname):
+    z = load(fname)
     for key in keys(z, "/KRed"):
         g = lambda n: T(z[f"{key}/{n}"])
         x, y, b, c, d, dm = (g("in_" + n) for n in ("x", "y", "b", "c", "d", "dm"))
