@@ -17,12 +17,19 @@ compact representation (Byrd, Nocedal & Schnabel 1994, eq. 2.6; H0 = gamma I):
 with S, Y the (m, n) histories kept in preallocated device buffers, R = triu(S^T Y),
 D = diag(S^T Y).  Per iteration: one stacked GEMV [S; Y] v, two m x m triangular solves
 (float64) and one GEMV back; the m x m products are updated incrementally (two GEMVs per new
-pair).  Results equal torch's two-loop up to floating-point rounding.
+pair).  Results equal torch's two-loop up to floating-point rounding.  The "GEMVs" are torch
+elementwise products + reductions, not BLAS calls: rocBLAS allows atomics by default, and the
+row-split multi-GPU mode needs bitwise-identical iterates on every rank.
 """
 from __future__ import annotations
 
 import torch
 from torch.optim.lbfgs import _strong_wolfe
+
+
+def _rowdots(A, v):
+    """A @ v as a deterministic elementwise product + row reduction."""
+    return (A * v[None, :]).sum(1)
 
 
 class CompactLBFGS(torch.optim.LBFGS):
@@ -52,8 +59,8 @@ class CompactLBFGS(torch.optim.LBFGS):
         S[m].copy_(s)
         Y[m].copy_(y)
         # new column of S^T Y / Y^T Y and new row s_m^T Y: two stacked GEMVs
-        a = torch.cat([S[:m + 1], Y[:m + 1]], 0) @ y            # [S^T y; Y^T y]
-        b = Y[:m + 1] @ s                                          # y_j . s_m
+        a = _rowdots(torch.cat([S[:m + 1], Y[:m + 1]], 0), y)    # [S^T y; Y^T y]
+        b = _rowdots(Y[:m + 1], s)                                 # y_j . s_m
         SY[:m + 1, m] = a[:m + 1].double()
         SY[m, :m + 1] = b.double()
         YY[:m + 1, m] = a[m + 1:].double()
@@ -68,15 +75,16 @@ class CompactLBFGS(torch.optim.LBFGS):
             return v * gamma
         S, Y = st["S"][:m], st["Y"][:m]
         SY, YY = st["SY"][:m, :m], st["YY"][:m, :m]
-        ab = (torch.cat([S, Y], 0) @ v).double()
+        SY_ = torch.cat([S, Y], 0)
+        ab = _rowdots(SY_, v).double()
         a, b = ab[:m], ab[m:]
         g = gamma if isinstance(gamma, float) else gamma.double()
         R = torch.triu(SY)
         u = torch.linalg.solve_triangular(R, a[:, None], upper=True)[:, 0]
-        w = torch.diagonal(SY) * u + g * (YY @ u) - g * b
+        w = torch.diagonal(SY) * u + g * _rowdots(YY, u) - g * b
         t = torch.linalg.solve_triangular(R.t(), w[:, None], upper=False)[:, 0]
         coef = torch.cat([t, -g * u]).to(v.dtype)
-        return v * gamma + torch.cat([S, Y], 0).t() @ coef
+        return v * gamma + (SY_ * coef[:, None]).sum(0)
 
     # ------------------------------------------------------------------------------
     @torch.no_grad()
