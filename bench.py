@@ -41,6 +41,8 @@ METRIC = "PSR iterations/sec + kernel-sum HBM GB/s, 100k-pt 3D, 1/2/4/8 MI355X"
 WORKLOADS = {
     "two_set_50k": dict(kind="two_set", N=50000),
     "two_set_200k": dict(kind="two_set", N=200000),
+    # the point count BASELINE.json's metric string names ("100k-pt 3D")
+    "two_set_100k": dict(kind="two_set", N=100000),
     # SURVEY C2': the exact ICP_two_set model (gradcomponent=True, eta = 1/lambda), a0 from
     # the device ridge CG (v2p version "ridge_keops", alpha 1e-3, PSR.py:402)
     "two_set_50k_exact": dict(kind="two_set", N=50000, version="logdet",
@@ -163,8 +165,10 @@ def _main(out):
         split = world > 1 and not args.replicas
         if split:
             psr.LMi.set_row_split()
-        cfg = {"workload": f"two-set 3D {wl['N']} vs {wl['N']} (BASELINE configs[1]" +
-               (")" if wl["N"] == 50000 else "/[2])") + (" exact ICP_two_set model" if version == "logdet" else ""),
+        src = {50000: "BASELINE configs[1]", 200000: "BASELINE configs[2]",
+               100000: "BASELINE metric's 100k-pt 3D"}.get(wl["N"], "two-set")
+        cfg = {"workload": f"two-set 3D {wl['N']} vs {wl['N']} ({src})" +
+               (" exact ICP_two_set model" if version == "logdet" else ""),
                "points_per_set": wl["N"], "lddmm": f"{version} sigma=0.1 lambda=1e3 Euler nt=10 dense",
                "gmm": "mu=xB fixed, sigma optimised", "max_repeat_GMM": 10, "tol": 1e-3,
                "parallelism": (f"row-split x{world} (RCCL all-gather / all-reduce per ODE step)" if split
@@ -246,7 +250,11 @@ def _main(out):
             flops_per_launch = d["flops"] / d["launches"]
             achieved = flops_per_launch / avg_s / 1e12
             traffic = load_traffic(dom)
-            roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+            # compute-bound: priced against the dense FP32 peak, 157.3 TF/s on MI355X, which is
+            # both the f32 MFMA rate and the packed-VALU rate (MI355X_MICROARCH.md); the pair
+            # kernels run on the VALU (3-wide dot products + exp: no contraction for MFMA)
+            roof = {"bound": "mfma", "compute_unit": "VALU (fp32; dense fp32 peak = f32 MFMA peak)",
+                    "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                     "traffic": traffic, "kernel": dom, "launches": d["launches"],
                     "avg_launch_ms": round(d["ms"] / d["launches"], 4),
