@@ -4,6 +4,7 @@
 #include "lddmm_ops.hpp"
 #include "lddmm_sym.hpp"
 #include "packed.hpp"
+#include "lddmm_sym_pk.hpp"
 
 #include <stdlib.h>
 
@@ -27,8 +28,9 @@ int g_r_fwd = -1, g_r_bwd = -1;
 int r_fwd() { if (g_r_fwd < 0) g_r_fwd = env_r("DICP_R_FWD", 2); return g_r_fwd; }
 int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd; }
 // eta = 0 VJP: 0 = OpOdeSelfBwd (55 VALU/pair), 1 = OpOdeSelfBwd2 (48), 2 = symmetric
-// pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair)
-int g_bwd_alg = 2;
+// pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair), 3 = the same pair-once
+// decomposition with the lane's two rows packed as float2 (lddmm_sym_pk.hpp, v_pk_*_f32; default: 5-7% faster on MI355X at 50k-100k)
+int g_bwd_alg = 3;
 // eta != 0 VJP: 0 = ordered OpOdeSelfBwdEta, 1 = symmetric pair-once SymBwdEta (lddmm_sym.hpp)
 #ifndef DICP_BWD_ETA_ALG
 #define DICP_BWD_ETA_ALG 1
@@ -125,7 +127,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "bwd_alg")) {
-    if (value < 0 || value > 2) return DICP_ERR_INVALID;
+    if (value < 0 || value > 3) return DICP_ERR_INVALID;
     g_bwd_alg = value;
     return DICP_OK;
   }
@@ -264,7 +266,7 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
-  if (g_bwd_alg == 2) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st);
+  if (g_bwd_alg >= 2) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, g_bwd_alg == 3);
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
@@ -280,12 +282,12 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
                         int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
   if (nparts == 1)  // the whole VJP: exactly the single-device kernel
     return ode_self_bwd_d<D>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, wsb, st);
-  if (eta == 0.0 && g_bwd_alg == 2) {
+  if (eta == 0.0 && g_bwd_alg >= 2) {
     Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
     Scal sc = make_scal(sigma, 0.0);
     scale_coords(a, sc, sigma);
     sc.dev0 = gdiv;
-    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts);
+    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts, g_bwd_alg == 3);
   }
   const int64_t per = (M + nparts - 1) / nparts;
   const int64_t r0 = per * part < M ? per * part : M;

@@ -805,9 +805,14 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
   return check_launch("ode_self_bwd(sym eta merge)");
 }
 
+// packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp)
+template <int D>
+__global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
+                                  int64_t slot_stride, int qoff, int qstride);
+
 template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
-                   hipStream_t st, int part = 0, int nparts = 1) {
+                   hipStream_t st, int part = 0, int nparts = 1, bool pk = false) {
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M, nparts);
   const size_t need = sym_ws_bytes(M, 2 * D, nparts);
@@ -823,8 +828,12 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   const int64_t stride = M * 2 * D;
   const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
   if (nq_own > 0) {
-    sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
-        a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    if (pk)
+      sym_bwd_pk_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    else
+      sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
     int rc = check_launch("ode_self_bwd(sym)");
     if (rc) return rc;
   }

@@ -1,0 +1,219 @@
+// Packed-FP32 variant of the symmetric pair-once VJP (lddmm_sym.hpp sym_bwd_kernel, eta = 0):
+// the two rows a lane owns are held as float2 vectors, so the pair algebra of SymBwd<D> runs
+// as v_pk_*_f32 instructions over both rows (the column record is broadcast into both halves);
+// the column-side contributions of the two rows are added once per step (one scalar add per
+// accumulator) before the DPP rotation.  Work decomposition, slots and merge are those of
+// sym_bwd_kernel, so results differ only by fp32 contraction order.
+#pragma once
+#include "lddmm_sym.hpp"
+#include "packed.hpp"
+
+namespace dicp {
+
+template <int D>
+struct SymBwdPk {
+  using S = SymBwd<D>;
+  struct Row2 {
+    f2 q[D], p[D], b[D], ia_a[D], gp[D];
+  };
+  __device__ static void pack(const typename S::Row& r0, const typename S::Row& r1, Row2& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      r.q[d] = f2{r0.q[d], r1.q[d]};
+      r.p[d] = f2{r0.p[d], r1.p[d]};
+      r.b[d] = f2{r0.b[d], r1.b[d]};
+      r.ia_a[d] = f2{r0.ia_a[d], r1.ia_a[d]};
+      r.gp[d] = f2{r0.gp[d], r1.gp[d]};
+    }
+  }
+  struct Shared {
+    f2 z[D], u[D];
+    f2 K, w, cKzb;
+  };
+  __device__ static void shared_terms(float c, const Row2& r, const float* rec, Shared& t) {
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+    const float* gpj = rec + 4 * D;
+    f2 r2 = splat(0.f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      t.z[d] = r.q[d] - splat(rec[d]);
+      r2 = pk_fma(t.z[d], t.z[d], r2);
+    }
+    t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    f2 pp = r.p[0] * splat(pj[0]);
+#pragma unroll
+    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+    f2 db[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      db[d] = r.b[d] - splat(bj[d]);
+      t.u[d] = pk_fma(-pp, db[d], r.gp[d] - splat(gpj[d]));
+    }
+    f2 zu = t.z[0] * t.u[0], zb = t.z[0] * db[0];
+    f2 iap = pk_fma(r.ia_a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+#pragma unroll
+    for (int d = 1; d < D; ++d) {
+      zu = pk_fma(t.z[d], t.u[d], zu);
+      zb = pk_fma(t.z[d], db[d], zb);
+      iap = pk_fma(r.ia_a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), iap));
+    }
+    t.w = pk_fma(splat(kS2), zu, -iap);
+    t.cKzb = (splat(c) * zb) * t.K;
+  }
+  // ordered pairs (i, j) of both rows, row side only (diag blocks)
+  __device__ static void pair_row(float gt, float c, const Row2& r, const float* rec, f2* acc) {
+    Shared t;
+    shared_terms(c, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
+      acc[D + d] = pk_fma(t.K, pk_fma(t.w, t.z[d], -t.u[d]), acc[D + d]);
+    }
+  }
+  // unordered pairs {i, j} of both rows: row side into acc, the column's total (both rows)
+  // into ct (scalars)
+  __device__ static void pair_sym(float gt, float c, const Row2& r, const float* rec, f2* acc, float* ct) {
+    Shared t;
+    shared_terms(c, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const f2 e = pk_fma(t.w, t.z[d], -t.u[d]);
+      const f2 Ke = t.K * e;
+      acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
+      acc[D + d] = acc[D + d] + Ke;
+      const f2 tt = pk_fma(splat(gt), t.z[d], r.ia_a[d]);
+      const f2 cg = pk_fma(t.cKzb, r.p[d], t.K * tt);
+      ct[d] = cg.x + cg.y;
+      ct[D + d] = -(Ke.x + Ke.y);
+    }
+  }
+};
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void sym_bwd_pk_kernel(
+    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
+    int qstride) {
+  using S = SymBwd<D>;
+  using P = SymBwdPk<D>;
+  constexpr int CW = S::CW, W = S::W;
+  __shared__ float4 planes[2][CW][kSymG];
+  __shared__ float colacc[kSymQ][kSymG][W];
+  if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
+  const float cs = sc.aux1 / a.scale;    // s1 / alpha
+  const float gt = sc.aux0 * cs;         // gam s1 / alpha
+
+  const int Q = qoff + qstride * (int)blockIdx.y, kc = blockIdx.x;
+  const int B0 = kSymQ * Q + kc * L;
+  if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
+  const int B1 = min(B0 + L, nG);
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int A = kSymQ * Q + wv;
+
+  typename P::Row2 row;
+  int64_t ri[2];
+  bool rv[2];
+  {
+    typename S::Row r2[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      ri[r] = (int64_t)A * kSymG + r * 64 + l;
+      rv[r] = A < nG && ri[r] < M;
+      S::load_row(a, sc, rv[r] ? ri[r] : 0, rv[r], r2[r]);
+    }
+    P::pack(r2[0], r2[1], row);
+  }
+  f2 racc[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) racc[k] = splat(0.f);
+
+  auto stage = [&](int B, int buf) {
+    if (tid < kSymG) {
+      const int64_t j = (int64_t)B * kSymG + tid;
+      float rec[4 * CW];
+      S::load_col(a, sc, j < M ? j : 0, j < M, rec);
+#pragma unroll
+      for (int m = 0; m < CW; ++m)
+        planes[buf][m][tid] = make_float4(rec[4 * m], rec[4 * m + 1], rec[4 * m + 2], rec[4 * m + 3]);
+    }
+  };
+
+  int buf = 0;
+  stage(B0, 0);
+  __syncthreads();
+  for (int B = B0; B < B1; ++B) {
+    if (B + 1 < B1) stage(B + 1, buf ^ 1);
+    const bool sym = A < B;          // wave-uniform
+    const bool diag = A == B;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      float cacc[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+      if (sym) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW];
+#pragma unroll
+          for (int m = 0; m < CW; ++m) {
+            const float4 v = planes[buf][m][col];
+            rec[4 * m] = v.x;
+            rec[4 * m + 1] = v.y;
+            rec[4 * m + 2] = v.z;
+            rec[4 * m + 3] = v.w;
+          }
+          float ct[W];
+          P::pair_sym(gt, cs, row, rec, racc, ct);
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+      } else if (diag) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW];
+#pragma unroll
+          for (int m = 0; m < CW; ++m) {
+            const float4 v = planes[buf][m][col];
+            rec[4 * m] = v.x;
+            rec[4 * m + 1] = v.y;
+            rec[4 * m + 2] = v.z;
+            rec[4 * m + 3] = v.w;
+          }
+          P::pair_row(gt, cs, row, rec, racc);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) colacc[wv][h * 64 + l][k] = cacc[k];
+    }
+    __syncthreads();
+    if (tid < kSymG) {
+      const int64_t j = (int64_t)B * kSymG + tid;
+      if (j < M) {
+        float* dst = slab + (int64_t)Q * slot_stride + j * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+          dst[k] = ((colacc[0][tid][k] + colacc[1][tid][k]) + colacc[2][tid][k]) + colacc[3][tid][k];
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    if (!rv[r]) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = r == 0 ? racc[k].x : racc[k].y;
+  }
+}
+
+}  // namespace dicp

@@ -28,8 +28,10 @@ from torch.optim.lbfgs import _strong_wolfe
 
 
 def _rowdots(A, v):
-    """A @ v as a deterministic elementwise product + row reduction."""
-    return (A * v[None, :]).sum(1)
+    """A @ v as a deterministic elementwise product + row reduction, accumulated in float64
+    (the m x m algebra is float64 already; an fp32 sum over n ~ 1e5-1e6 entries would make the
+    fp32 trajectory depend on the reduction order)."""
+    return (A * v[None, :]).sum(1, dtype=torch.float64)
 
 
 class CompactLBFGS(torch.optim.LBFGS):

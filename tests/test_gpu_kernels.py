@@ -11,6 +11,8 @@ import torch
 from conftest import rel_err
 from oracle import torch_ref as R
 
+BWD_ALG_DEFAULT = 3  # lddmm.hip g_bwd_alg: symmetric pair-once VJP, packed-FP32 rows
+
 pytestmark = pytest.mark.gpu
 
 
@@ -126,12 +128,12 @@ def test_ode_self_bwd(dev, M, D, withlogdet, gradcomp):
     Lf = (a * v).sum() + (bm * mG).sum() + (gam * c).sum()
     gq64, gp64 = torch.autograd.grad(Lf, (q, p))
     f = lambda t: t.detach().float().to(dev)
-    for alg in (0, 1, 2):  # eta = 0 variants: pair algebras (lddmm_ops.hpp), symmetric kernel
+    for alg in (0, 1, 2, 3):  # eta = 0: pair algebras (lddmm_ops.hpp), symmetric kernel (+ packed)
         L.set_option("bwd_alg", alg)
         try:
             gq, gp = L.ode_self_bwd(f(q), f(p), f(a), f(bm), f(gam) if withlogdet else None, 0.15, m.eta)
         finally:
-            L.set_option("bwd_alg", 2)
+            L.set_option("bwd_alg", BWD_ALG_DEFAULT)
         assert rel_err(gq.cpu(), gq64) < 2e-5, (alg, rel_err(gq.cpu(), gq64))
         assert rel_err(gp.cpu(), gp64) < 2e-5, (alg, rel_err(gp.cpu(), gp64))
 
@@ -218,12 +220,17 @@ def test_sym_bwd_vs_ordered(dev, M):
     L.set_option("bwd_alg", 1)
     try:
         gq1, gp1 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+        L.set_option("bwd_alg", 2)  # scalar rows
+        gq2, gp2 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+        gq3, gp3 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
     finally:
-        L.set_option("bwd_alg", 2)
-    gq2, gp2 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
-    gq3, gp3 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+        L.set_option("bwd_alg", BWD_ALG_DEFAULT)
     assert rel_err(gq2, gq1) < 2e-6 and rel_err(gp2, gp1) < 2e-6
     assert torch.equal(gq2, gq3) and torch.equal(gp2, gp3)
+    gq4, gp4 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)  # default: packed-FP32 rows
+    gq5, gp5 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0)
+    assert rel_err(gq4, gq1) < 2e-6 and rel_err(gp4, gp1) < 2e-6
+    assert torch.equal(gq4, gq5) and torch.equal(gp4, gp5)
 
 
 @pytest.mark.parametrize("M", [1, 127, 128, 129, 1000, 5000, 50000])

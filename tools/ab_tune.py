@@ -91,7 +91,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL", "eta"])
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL", "eta", "pk"])
     ap.add_argument("--Ms", default="20000,50000,200000", help="row counts for --mode rounds")
     a = ap.parse_args()
     if a.mode == "splits":
@@ -121,6 +121,10 @@ def main():
         variants.append(("bwd_eta_ordered", {"bwd_eta_alg": 0}, bwde))
         variants.append(("bwd_eta_sym", {"bwd_eta_alg": 1}, bwde))
         variants.append(("bwd_eta0_sym", {"bwd_eta_alg": 1}, bwd))
+    elif a.mode == "pk":  # symmetric VJP: scalar rows vs packed-FP32 rows (lddmm_sym_pk.hpp)
+        for L in (0, 2, 4):
+            variants.append((f"bwd_alg2_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
+            variants.append((f"bwd_alg3_pk_L{L}", {"bwd_alg": 3, "sym_L": L}, bwd))
     elif a.mode == "symL":  # symmetric VJP column groups per workgroup (0 = automatic)
         for L in (0, 1, 2, 4):
             variants.append((f"bwd_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
