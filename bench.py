@@ -1,12 +1,13 @@
 """Headline benchmark: diff-ICP PSR iterations/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload two_set_50k|two_set_200k|atlas_c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload two_set_100k|two_set_50k|two_set_200k|atlas_c4|c5]
     (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
 
 A "step" is one diff-ICP iteration on the workload -- GMM_opt(max_repeat_GMM=10, tol=1e-3)
 + Reg_opt(nmax=1, tol=1e-3), the loop body of ICP_two_set.py:254-282 / ICP_atlas.py:269-298 --
-with every point set resident in HBM.  Default workload (BASELINE.json configs[1]):
-two-point-set 3D match, 50k vs 50k synthetic points, hybrid LDDMM (sigma 0.1, lambda 1e3,
+with every point set resident in HBM.  Default workload (the point count BASELINE.json's
+metric names, "100k-pt 3D"; configs[1] is two_set_50k):
+two-point-set 3D match, 100k vs 100k synthetic points, hybrid LDDMM (sigma 0.1, lambda 1e3,
 Euler nt=10, dense support), GMM on xB with sigma optimised.  The atlas workloads shard
 frames over ranks with an RCCL exchange of the GMM sufficient statistics.
 
@@ -121,7 +122,7 @@ def _main(out):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="two_set_50k", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="two_set_100k", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip live per-kernel events")
     ap.add_argument("--concurrent-frames", type=int, default=None,

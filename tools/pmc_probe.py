@@ -1,4 +1,4 @@
-"""Launch each hot kernel a few times at the bench's sizes (C2: 50k support points, 50k x 50k
+"""Launch each hot kernel a few times at the bench's sizes (100k support points, 100k x 100k
 E-step) for rocprofv3 PMC passes, e.g.
 
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o fetch --output-format csv -- python tools/pmc_probe.py
@@ -15,7 +15,7 @@ from difficp_amd import _lib  # noqa: E402
 
 
 def main():
-    M = int(os.environ.get("PMC_M", "50000"))
+    M = int(os.environ.get("PMC_M", "100000"))
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     q = torch.rand(M, 3, device=dev)
