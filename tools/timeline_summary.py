@@ -8,7 +8,7 @@ import argparse
 import csv
 import json
 
-HOT = ("sym_bwd_kernel", "OpOdeSelf", "lse_rowred", "OpGmm", "sym_merge", "merge_slabs",
+HOT = ("sym_bwd_kernel", "sym_bwd_pk_kernel", "rowred_pk_kernel", "lse_finalize", "OpOdeSelf", "lse_rowred", "OpGmm", "sym_merge", "merge_slabs",
        "sym_kernel", "OpOdeExt", "rowred_kernel")
 
 
