@@ -95,8 +95,14 @@ struct SymBwdPk {
   }
 };
 
+#ifndef DICP_SYMBWD_PK_WMIN
+#define DICP_SYMBWD_PK_WMIN 1
+#endif
+#ifndef DICP_SYMBWD_PK_UNROLL
+#define DICP_SYMBWD_PK_UNROLL 2
+#endif
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void sym_bwd_pk_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
   using S = SymBwd<D>;
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
 #pragma unroll
       for (int k = 0; k < W; ++k) cacc[k] = 0.f;
       if (sym) {
-#pragma unroll 2
+#pragma unroll DICP_SYMBWD_PK_UNROLL
         for (int k2 = 0; k2 < 64; ++k2) {
           const int col = h * 64 + ((l + k2) & 63);
           float rec[4 * CW];
