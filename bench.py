@@ -59,8 +59,9 @@ def log(msg):
 
 def cpu_baseline(pair_counts, M_work, budget_s=15.0):
     """Time the oracle's C restatement (OpenMP) of the dominant pair kernels on this host on a
-    bounded sample -- repeated ODE-forward / VJP / E-step evaluations at the workload's own
-    M x M size -- then extrapolate to one iteration from the live pair counts."""
+    bounded sample -- repeated ODE-forward / VJP / E-step evaluations at M x M pairs (the
+    workload's size, capped at 50k so one evaluation stays ~1 s) -- then extrapolate to one
+    iteration from the live pair counts (the C kernels' pair rate is flat in M)."""
     from oracle import c_ref
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.manual_seed(0)
@@ -90,7 +91,7 @@ def cpu_baseline(pair_counts, M_work, budget_s=15.0):
     secs = sum(v / rates[kind_of.get(k, "fwd")] for k, v in pair_counts.items())
     return {"value": 1.0 / secs, "unit": "PSR iterations/sec", "cores": threads, "kind": "port",
             "sample": (f"oracle/difficp_ref.c (OpenMP, {threads} threads): {reps} x (ODE fwd + VJP + "
-                       f"E-step) at the workload's {M}x{M} pairs ({time.perf_counter() - t_start:.1f} s), rates fwd {rates['fwd'] / 1e9:.3f} / bwd {rates['bwd'] / 1e9:.3f} / "
+                       f"E-step) at {M}x{M} pairs ({time.perf_counter() - t_start:.1f} s), rates fwd {rates['fwd'] / 1e9:.3f} / bwd {rates['bwd'] / 1e9:.3f} / "
                        f"EM {rates['em'] / 1e9:.3f} Gpair/s, extrapolated to the live pair counts of one "
                        "iteration")}
 
