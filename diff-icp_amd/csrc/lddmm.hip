@@ -31,9 +31,10 @@ int r_bwd() { if (g_r_bwd < 0) g_r_bwd = env_r("DICP_R_BWD", 1); return g_r_bwd;
 // pair-once kernel (lddmm_sym.hpp, ~32 VALU per ordered pair), 3 = the same pair-once
 // decomposition with the lane's two rows packed as float2 (lddmm_sym_pk.hpp, v_pk_*_f32; default: 5-7% faster on MI355X at 50k-100k)
 int g_bwd_alg = 3;
-// eta != 0 VJP: 0 = ordered OpOdeSelfBwdEta, 1 = symmetric pair-once SymBwdEta (lddmm_sym.hpp)
+// eta != 0 VJP: 0 = ordered OpOdeSelfBwdEta, 1 = symmetric pair-once SymBwdEta (lddmm_sym.hpp),
+// 2 = the same with packed-FP32 rows (lddmm_sym_pk.hpp SymBwdEtaPk)
 #ifndef DICP_BWD_ETA_ALG
-#define DICP_BWD_ETA_ALG 1
+#define DICP_BWD_ETA_ALG 2
 #endif
 int g_bwd_eta_alg = DICP_BWD_ETA_ALG;
 // eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
@@ -122,7 +123,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "bwd_eta_alg")) {
-    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    if (value < 0 || value > 2) return DICP_ERR_INVALID;
     g_bwd_eta_alg = value;
     return DICP_OK;
   }
@@ -211,7 +212,9 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
   if (eta != 0.0)
-    return launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
+    return g_fwd_alg == 2
+               ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, true>>("ode_self_fwd_eta(pk)", a, sc, nrows, M, o, ws, wsb, st)
+               : launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
   if (g_fwd_alg == 1 && all)
     return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st)
                                : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st);
@@ -231,7 +234,8 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
                    ws_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), nrows, M),
                    ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M)})
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, M)})
     m = v > m ? v : m;
   return m;
 }
@@ -247,7 +251,8 @@ size_t ode_self_fwd_ws(int64_t M) {
   const size_t d = sym_ws_bytes(M, 3 * D);
   a = a > d ? a : d;
   for (size_t e : {rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M)})
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(M, M)})
     a = a > e ? a : e;
   return a;
 }
@@ -260,7 +265,7 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   if (eta != 0.0) {
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
-    if (g_bwd_eta_alg == 1) return launch_sym_bwd_eta<D>(a, sc, M, o, ws, wsb, st);
+    if (g_bwd_eta_alg >= 1) return launch_sym_bwd_eta<D>(a, sc, M, o, ws, wsb, st, g_bwd_eta_alg == 2);
     return launch_r<OpOdeSelfBwdEta<D>>(r_bwd(), "ode_self_bwd_eta", a, sc, M, M, o, ws, wsb, st);
   }
   Scal sc = make_scal(sigma, 0.0);

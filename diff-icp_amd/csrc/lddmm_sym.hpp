@@ -778,9 +778,14 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   return check_launch("ode_self_fwd(sym merge)");
 }
 
+// packed-FP32 rows of the eta != 0 VJP (lddmm_sym_pk.hpp)
+template <int D>
+__global__ void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
+                                      int64_t slot_stride);
+
 template <int D>
 int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws,
-                       size_t wsb, hipStream_t st) {
+                       size_t wsb, hipStream_t st, bool pk = false) {
   using S = SymBwdEta<D>;
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M);
@@ -795,8 +800,12 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
   }
   float* slab = reinterpret_cast<float*>(ws);
   const int64_t stride = M * S::W;
-  sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
-                                                                              slab, stride);
+  if (pk)
+    sym_bwd_eta_pk_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
+        a, sc, M, g.nG, g.L, slab, stride);
+  else
+    sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
+                                                                                slab, stride);
   int rc = check_launch("ode_self_bwd(sym eta)");
   if (rc) return rc;
   const int64_t n = M * S::W;

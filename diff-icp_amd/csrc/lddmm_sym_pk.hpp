@@ -13,6 +13,14 @@ namespace dicp {
 template <int D>
 struct SymBwdPk {
   using S = SymBwd<D>;
+  static constexpr int kMaxWaves = 4;
+  struct Prm {
+    float gt, c;  // gam s1 / alpha, s1 / alpha (SymBwd::Prm)
+  };
+  __device__ static Prm params(const Args& a, const Scal& sc) {
+    const float cs = sc.aux1 / a.scale;
+    return Prm{sc.aux0 * cs, cs};
+  }
   struct Row2 {
     f2 q[D], p[D], b[D], ia_a[D], gp[D];
   };
@@ -63,9 +71,10 @@ struct SymBwdPk {
     t.cKzb = (splat(c) * zb) * t.K;
   }
   // ordered pairs (i, j) of both rows, row side only (diag blocks)
-  __device__ static void pair_row(float gt, float c, const Row2& r, const float* rec, f2* acc) {
+  __device__ static void pair_row(const Prm& prm, const Row2& r, const float* rec, f2* acc) {
+    const float gt = prm.gt;
     Shared t;
-    shared_terms(c, r, rec, t);
+    shared_terms(prm.c, r, rec, t);
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
 #pragma unroll
@@ -76,9 +85,10 @@ struct SymBwdPk {
   }
   // unordered pairs {i, j} of both rows: row side into acc, the column's total (both rows)
   // into ct (scalars)
-  __device__ static void pair_sym(float gt, float c, const Row2& r, const float* rec, f2* acc, float* ct) {
+  __device__ static void pair_sym(const Prm& prm, const Row2& r, const float* rec, f2* acc, float* ct) {
+    const float gt = prm.gt;
     Shared t;
-    shared_terms(c, r, rec, t);
+    shared_terms(prm.c, r, rec, t);
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
 #pragma unroll
@@ -98,21 +108,25 @@ struct SymBwdPk {
 #ifndef DICP_SYMBWD_PK_WMIN
 #define DICP_SYMBWD_PK_WMIN 1
 #endif
+#ifndef DICP_SYMBWD_PK_PREFETCH
+#define DICP_SYMBWD_PK_PREFETCH 0
+#endif
 #ifndef DICP_SYMBWD_PK_UNROLL
 #define DICP_SYMBWD_PK_UNROLL 2
 #endif
-template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
-    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
-    int qstride) {
-  using S = SymBwd<D>;
-  using P = SymBwdPk<D>;
+// The kernel body, shared by the eta = 0 (SymBwdPk) and eta != 0 (SymBwdEtaPk) VJPs.  P supplies
+// S (the scalar struct: CW, W, kUsed, Row, load_row, load_col), Row2 / pack, Prm / params and
+// the packed pair_sym / pair_row.
+template <class P>
+__device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, int L,
+                                            float* __restrict__ slab, int64_t slot_stride, int qoff,
+                                            int qstride) {
+  using S = typename P::S;
   constexpr int CW = S::CW, W = S::W;
   __shared__ float4 planes[2][CW][kSymG];
   __shared__ float colacc[kSymQ][kSymG][W];
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
-  const float cs = sc.aux1 / a.scale;    // s1 / alpha
-  const float gt = sc.aux0 * cs;         // gam s1 / alpha
+  const typename P::Prm prm = P::params(a, sc);
 
   const int Q = qoff + qstride * (int)blockIdx.y, kc = blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
@@ -150,6 +164,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD
   };
 
   int buf = 0;
+  // read a column record: only the S::kUsed live floats (as sym_kernel's ldrec)
+  auto ldrec = [&](int col, float* rec) {
+    constexpr int kLast = S::kUsed - 4 * (CW - 1);  // live floats of the last plane (1..4)
+#pragma unroll
+    for (int m = 0; m < CW; ++m) {
+      const float* src = reinterpret_cast<const float*>(&planes[buf][m][col]);
+      if (m < CW - 1 || kLast == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = v.z, rec[4 * m + 3] = v.w;
+      } else if (kLast == 3) {
+        const float3 v = *reinterpret_cast<const float3*>(src);
+        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = v.z, rec[4 * m + 3] = 0.f;
+      } else if (kLast == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = rec[4 * m + 3] = 0.f;
+      } else {
+        rec[4 * m] = src[0], rec[4 * m + 1] = rec[4 * m + 2] = rec[4 * m + 3] = 0.f;
+      }
+    }
+  };
   stage(B0, 0);
   __syncthreads();
   for (int B = B0; B < B1; ++B) {
@@ -162,23 +196,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD
 #pragma unroll
       for (int k = 0; k < W; ++k) cacc[k] = 0.f;
       if (sym) {
+#if DICP_SYMBWD_PK_PREFETCH
+        // register double-buffer of the column record (as sym_kernel): step k2 + 1's LDS
+        // reads are issued before step k2's algebra, so their latency is not exposed
+        float rec[4 * CW];
+        ldrec(h * 64 + (l & 63), rec);
+#pragma unroll DICP_SYMBWD_PK_UNROLL
+        for (int k2 = 0; k2 < 64; ++k2) {
+          float nxt[4 * CW];
+          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          ldrec(h * 64 + ((l + k2 + 1) & 63), nxt);  // k2 = 63 wraps to column l: harmless
+          __builtin_amdgcn_sched_barrier(0);
+          float ct[W];
+          P::pair_sym(prm, row, rec, racc, ct);
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+#pragma unroll
+          for (int k = 0; k < 4 * CW; ++k) rec[k] = nxt[k];
+        }
+#else
 #pragma unroll DICP_SYMBWD_PK_UNROLL
         for (int k2 = 0; k2 < 64; ++k2) {
           const int col = h * 64 + ((l + k2) & 63);
           float rec[4 * CW];
-#pragma unroll
-          for (int m = 0; m < CW; ++m) {
-            const float4 v = planes[buf][m][col];
-            rec[4 * m] = v.x;
-            rec[4 * m + 1] = v.y;
-            rec[4 * m + 2] = v.z;
-            rec[4 * m + 3] = v.w;
-          }
+          ldrec(col, rec);
           float ct[W];
-          P::pair_sym(gt, cs, row, rec, racc, ct);
+          P::pair_sym(prm, row, rec, racc, ct);
 #pragma unroll
           for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
         }
+#endif
 #pragma unroll
         for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
       } else if (diag) {
@@ -194,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD
             rec[4 * m + 2] = v.z;
             rec[4 * m + 3] = v.w;
           }
-          P::pair_row(gt, cs, row, rec, racc);
+          P::pair_row(prm, row, rec, racc);
         }
       }
 #pragma unroll
@@ -220,6 +267,113 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD
 #pragma unroll
     for (int k = 0; k < W; ++k) dst[k] = r == 0 ? racc[k].x : racc[k].y;
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
+    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
+    int qstride) {
+  sym_pk_body<SymBwdPk<D>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+}
+
+// Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /
+// gradcomponent model): the same per-pair algebra on float2 rows, column side summed over the
+// lane's two rows before the rotation (the scalar kernel's ct = cgp(row 0) + cgp(row 1)).
+template <int D>
+struct SymBwdEtaPk {
+  using S = SymBwdEta<D>;
+  using Prm = typename S::Prm;
+  __device__ static Prm params(const Args& a, const Scal& sc) { return S::params(a, sc); }
+  struct Row2 {
+    f2 q[D], p[D], a[D], b[D];
+  };
+  __device__ static void pack(const typename S::Row& r0, const typename S::Row& r1, Row2& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      r.q[d] = f2{r0.q[d], r1.q[d]};
+      r.p[d] = f2{r0.p[d], r1.p[d]};
+      r.a[d] = f2{r0.a[d], r1.a[d]};
+      r.b[d] = f2{r0.b[d], r1.b[d]};
+    }
+  }
+  struct Shared {
+    f2 z[D], db[D], da[D], dp[D];
+    f2 K, szbK, czp, cdb, cdp, czq;
+  };
+  __device__ static void shared_terms(const Prm& P, const Row2& r, const float* rec, Shared& t) {
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+    const float* bj = rec + 3 * D;
+    f2 r2 = splat(0.f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      t.z[d] = r.q[d] - splat(rec[d]);
+      r2 = pk_fma(t.z[d], t.z[d], r2);
+      t.da[d] = r.a[d] - splat(aj[d]);
+      t.db[d] = r.b[d] - splat(bj[d]);
+      t.dp[d] = r.p[d] - splat(pj[d]);
+    }
+    t.K = f2{fast_exp2(P.nc * r2.x), fast_exp2(P.nc * r2.y)};
+    f2 pp = r.p[0] * splat(pj[0]);
+    f2 ap = pk_fma(r.a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+    f2 zb = t.z[0] * t.db[0], zp = t.z[0] * t.dp[0], za = t.z[0] * t.da[0], bp = t.db[0] * t.dp[0];
+#pragma unroll
+    for (int d = 1; d < D; ++d) {
+      pp = pk_fma(r.p[d], splat(pj[d]), pp);
+      ap = pk_fma(r.a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), ap));
+      zb = pk_fma(t.z[d], t.db[d], zb);
+      zp = pk_fma(t.z[d], t.dp[d], zp);
+      za = pk_fma(t.z[d], t.da[d], za);
+      bp = pk_fma(t.db[d], t.dp[d], bp);
+    }
+    const f2 sr2 = splat(P.s) * r2;
+    const f2 sr2D2 = sr2 - splat((float)(D + 2));
+    const f2 Phi = ap + splat(P.es) * za + splat(P.s) * pp * zb +
+                   splat(P.es) * (splat(P.s) * zp * zb - bp) - splat(P.e2s2) * zb * sr2D2 -
+                   splat(P.gs) * zp + splat(2.f * P.gam * P.es) * (sr2 - splat((float)D));
+    t.czp = splat(P.s) * zb * splat(P.es) - splat(P.gs);
+    t.czq = splat(-2.f * P.e2s2 * P.s) * zb + splat(4.f * P.gam * P.es2) - splat(P.s) * Phi;
+    t.cdb = splat(P.s) * pp + splat(P.es2) * zp - splat(P.e2s2) * sr2D2;
+    t.cdp = splat(P.es2) * zb - splat(P.gs);
+    t.szbK = splat(P.s) * zb * t.K;
+  }
+  // ordered pairs of both rows, row side only (diag blocks)
+  __device__ static void pair_row(const Prm& P, const Row2& r, const float* rec, f2* acc) {
+    Shared t;
+    shared_terms(P, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const f2 Tv = pk_fma(t.czp, t.z[d], splat(-P.es) * t.db[d]);
+      acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, pk_fma(t.szbK, splat(pj[d]), acc[d]));
+      const f2 G = pk_fma(splat(P.es), t.da[d], pk_fma(t.cdb, t.db[d], pk_fma(t.cdp, t.dp[d], t.czq * t.z[d])));
+      acc[D + d] = pk_fma(t.K, G, acc[D + d]);
+    }
+  }
+  // unordered pairs of both rows: row side into acc, the column's total (both rows) into ct
+  __device__ static void pair_sym(const Prm& P, const Row2& r, const float* rec, f2* acc, float* ct) {
+    Shared t;
+    shared_terms(P, r, rec, t);
+    const float* pj = rec + D;
+    const float* aj = rec + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const f2 Tv = pk_fma(t.czp, t.z[d], splat(-P.es) * t.db[d]);
+      const f2 G = t.K * pk_fma(splat(P.es), t.da[d], pk_fma(t.cdb, t.db[d], pk_fma(t.cdp, t.dp[d], t.czq * t.z[d])));
+      acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, pk_fma(t.szbK, splat(pj[d]), acc[d]));
+      acc[D + d] = acc[D + d] + G;
+      const f2 cgp = pk_fma(t.K, r.a[d] - Tv, t.szbK * r.p[d]);
+      ct[d] = cgp.x + cgp.y;
+      ct[D + d] = -G.x - G.y;
+    }
+  }
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+                                                             float* __restrict__ slab, int64_t slot_stride) {
+  sym_pk_body<SymBwdEtaPk<D>>(a, sc, M, nG, L, slab, slot_stride, 0, 1);
 }
 
 }  // namespace dicp

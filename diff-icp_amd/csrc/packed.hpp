@@ -16,10 +16,11 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
 
-// OpOdeSelfFwd<D, false, DIV> (lddmm_ops.hpp) on two rows at once: V, Gs' (, Z').
-template <int D, bool DIV>
+// OpOdeSelfFwd<D, ETA, DIV> (lddmm_ops.hpp) on two rows at once: V, Gs' (, Z'), and for
+// eta != 0 (ETA, which implies Z') the Hs, GL' and L sums of the logdet / gradcomponent model.
+template <int D, bool DIV, bool ETA = false>
 struct OpOdeSelfFwdPk {
-  using Base = OpOdeSelfFwd<D, false, DIV>;
+  using Base = OpOdeSelfFwd<D, ETA, DIV || ETA>;
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = Base::NACC;
   static constexpr int kNOut = Base::kNOut;
@@ -55,7 +56,24 @@ struct OpOdeSelfFwdPk {
     for (int d = 0; d < D; ++d) {
       acc[d] = pk_fma(K, splat(pj[d]), acc[d]);
       acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
-      if (DIV) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
+      if (DIV || ETA) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
+    }
+    if (ETA) {  // OpOdeSelfFwd::pair, eta != 0 terms
+      f2 u[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) u[d] = r.p[d] - splat(pj[d]);
+      f2 zu = z[0] * u[0];
+#pragma unroll
+      for (int d = 1; d < D; ++d) zu = pk_fma(z[d], u[d], zu);
+      const f2 szu = splat(kS2) * zu;
+      const f2 sr2 = splat(kS2) * r2;
+      const f2 KGL = K * (sr2 - splat((float)(D + 2)));
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        acc[3 * D + d] = pk_fma(K, pk_fma(szu, z[d], -u[d]), acc[3 * D + d]);  // Hs
+        acc[4 * D + d] = pk_fma(KGL, z[d], acc[4 * D + d]);                     // GL'
+      }
+      acc[5 * D] = pk_fma(K, sr2 - splat((float)D), acc[5 * D]);  // L
     }
   }
 };

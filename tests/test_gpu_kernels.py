@@ -12,6 +12,7 @@ from conftest import rel_err
 from oracle import torch_ref as R
 
 BWD_ALG_DEFAULT = 3  # lddmm.hip g_bwd_alg: symmetric pair-once VJP, packed-FP32 rows
+BWD_ETA_ALG_DEFAULT = 2  # lddmm.hip g_bwd_eta_alg (DICP_BWD_ETA_ALG)
 
 pytestmark = pytest.mark.gpu
 
@@ -275,13 +276,16 @@ def test_sym_bwd_eta_vs_ordered(dev, M):
     a = torch.randn(M, 3, generator=g).to(dev)
     b = torch.randn(M, 3, generator=g).to(dev)
     gd = torch.full((1,), -0.4, device=dev)
-    L.set_option("bwd_eta_alg", 0)
+    res = {}
     try:
-        gq0, gp0 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3)
+        for alg in (0, 1, 2):  # ordered, symmetric scalar rows, symmetric packed-FP32 rows
+            L.set_option("bwd_eta_alg", alg)
+            res[alg] = [L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3) for _ in range(2 if alg else 1)]
     finally:
-        L.set_option("bwd_eta_alg", 1)
-    gq1, gp1 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3)
-    gq2, gp2 = L.ode_self_bwd(q, p, a, b, gd, 0.1, 1e-3)
-    assert torch.isfinite(gq1).all() and torch.isfinite(gp1).all()
-    assert rel_err(gq1, gq0) < 5e-6 and rel_err(gp1, gp0) < 5e-6, (rel_err(gq1, gq0), rel_err(gp1, gp0))
-    assert torch.equal(gq1, gq2) and torch.equal(gp1, gp2)
+        L.set_option("bwd_eta_alg", BWD_ETA_ALG_DEFAULT)
+    gq0, gp0 = res[0][0]
+    for alg in (1, 2):
+        (gq1, gp1), (gq2, gp2) = res[alg]
+        assert torch.isfinite(gq1).all() and torch.isfinite(gp1).all()
+        assert rel_err(gq1, gq0) < 5e-6 and rel_err(gp1, gp0) < 5e-6, (alg, rel_err(gq1, gq0), rel_err(gp1, gp0))
+        assert torch.equal(gq1, gq2) and torch.equal(gp1, gp2)

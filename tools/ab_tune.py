@@ -91,7 +91,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=50000)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL", "eta", "pk"])
+    ap.add_argument("--mode", default="rsplit", choices=["rsplit", "alg", "rounds", "splits", "fwd", "symL", "eta", "pk", "fwdeta"])
     ap.add_argument("--Ms", default="20000,50000,200000", help="row counts for --mode rounds")
     a = ap.parse_args()
     if a.mode == "splits":
@@ -120,7 +120,12 @@ def main():
         bwde = lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 1e-3)
         variants.append(("bwd_eta_ordered", {"bwd_eta_alg": 0}, bwde))
         variants.append(("bwd_eta_sym", {"bwd_eta_alg": 1}, bwde))
+        variants.append(("bwd_eta_sym_pk", {"bwd_eta_alg": 2}, bwde))
         variants.append(("bwd_eta0_sym", {"bwd_eta_alg": 1}, bwd))
+    elif a.mode == "fwdeta":  # eta != 0 forward: scalar ordered rows vs packed-FP32 rows
+        fwde = lambda: _lib.ode_self_fwd(q, p, 0.1, 1e-3, True)
+        variants.append(("fwd_eta_alg0_scalar", {"fwd_alg": 0}, fwde))
+        variants.append(("fwd_eta_alg2_packed", {"fwd_alg": 2}, fwde))
     elif a.mode == "pk":  # symmetric VJP: scalar rows vs packed-FP32 rows (lddmm_sym_pk.hpp)
         for L in (0, 2, 4):
             variants.append((f"bwd_alg2_sym_L{L}", {"bwd_alg": 2, "sym_L": L}, bwd))
