@@ -241,8 +241,15 @@ const char* dicp_last_error(void);
 const char* dicp_version(void);
 /* 1 if D is compiled in. */
 int dicp_supports_dim(int D);
-/* Tuning knobs for measurements: "r_fwd" / "r_bwd" = rows per thread {1,2,4} of the fused
- * ODE forward / backward passes (defaults from env DICP_R_FWD / DICP_R_BWD or built-in). */
+/* Tuning / A-B knobs (process-wide; results of every setting agree to fp32 summation order):
+ *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
+ *                  rows (default; for eta != 0: 2 packed, otherwise ordered scalar rows)
+ *   "bwd_alg"      eta = 0 VJP: 0 / 1 ordered pair algebras, 2 symmetric pair-once, 3 symmetric
+ *                  with packed-FP32 rows (default)
+ *   "bwd_eta_alg"  eta != 0 VJP: 0 ordered, 1 symmetric, 2 symmetric packed-FP32 (default)
+ *   "r_fwd" / "r_bwd"  rows per thread {1,2,4} of the ordered passes (env DICP_R_FWD / DICP_R_BWD)
+ *   "split_rounds", "force_splits", "sym_L"  column-split / symmetric-chunk geometry (0 = auto)
+ * Returns DICP_ERR_INVALID for an unknown name or an out-of-range value. */
 int dicp_set_option(const char* name, int value);
 /* Number of column splits the library will use for an M x N pass (diagnostics/bench). */
 int dicp_num_splits(int kind, int64_t M, int64_t N);
