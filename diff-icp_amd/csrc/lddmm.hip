@@ -278,7 +278,7 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
 }
 
 // Pair subset `part` of `nparts` of the VJP (row-split over ranks; the sum over parts is
-// the full VJP): eta = 0 symmetric kernel -> the quads Q = part (mod nparts), written to all
+// the full VJP): symmetric kernels (eta = 0, and eta != 0 packed) -> the quads Q = part (mod nparts), written to all
 // rows; otherwise (ordered kernels) the row slice [part * ceil(M/nparts), ...) against all
 // columns, other rows zero.  Outputs plain (no epilogue).
 template <int D>
@@ -293,6 +293,12 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
     scale_coords(a, sc, sigma);
     sc.dev0 = gdiv;
     return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts, g_bwd_alg == 3);
+  }
+  if (eta != 0.0 && g_bwd_eta_alg == 2) {  // symmetric packed eta VJP: quads Q = part (mod nparts)
+    Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
+    Scal sc = make_scal(sigma, eta);
+    sc.dev0 = gdiv;
+    return launch_sym_bwd_eta<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, true, part, nparts);
   }
   const int64_t per = (M + nparts - 1) / nparts;
   const int64_t r0 = per * part < M ? per * part : M;

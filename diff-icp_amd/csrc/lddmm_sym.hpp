@@ -781,15 +781,19 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
 // packed-FP32 rows of the eta != 0 VJP (lddmm_sym_pk.hpp)
 template <int D>
 __global__ void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
-                                      int64_t slot_stride);
+                                      int64_t slot_stride, int qoff, int qstride);
 
 template <int D>
 int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws,
-                       size_t wsb, hipStream_t st, bool pk = false) {
+                       size_t wsb, hipStream_t st, bool pk = false, int part = 0, int nparts = 1) {
   using S = SymBwdEta<D>;
   if (M <= 0) return DICP_OK;
-  const SymGeom g = sym_geom(M);
-  const size_t need = sym_ws_bytes(M, S::W);
+  if (nparts > 1 && !pk) {
+    set_error("ode_self_bwd(sym eta): pair-subset parts need the packed kernel (bwd_eta_alg 2)");
+    return DICP_ERR_INVALID;
+  }
+  const SymGeom g = sym_geom(M, nparts);
+  const size_t need = sym_ws_bytes(M, S::W, nparts);
   if (ws == nullptr || wsb < need) {
     set_error("ode_self_bwd(sym eta): workspace too small (%zu < %zu bytes)", wsb, need);
     return DICP_ERR_WORKSPACE;
@@ -800,17 +804,24 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
   }
   float* slab = reinterpret_cast<float*>(ws);
   const int64_t stride = M * S::W;
-  if (pk)
-    sym_bwd_eta_pk_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
-        a, sc, M, g.nG, g.L, slab, stride);
-  else
-    sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
-                                                                                slab, stride);
-  int rc = check_launch("ode_self_bwd(sym eta)");
-  if (rc) return rc;
+  const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
+  if (nq_own > 0) {
+    if (pk)
+      sym_bwd_eta_pk_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    else
+      sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
+                                                                                  slab, stride);
+    int rc = check_launch("ode_self_bwd(sym eta)");
+    if (rc) return rc;
+  }
   const int64_t n = M * S::W;
-  sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-      slab, stride, M, g.nG, g.L, 1.f, 1.f, o, 0, 1);
+  if (nparts > 1)
+    sym_merge_kernel<D, true><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+        slab, stride, M, g.nG, g.L, 1.f, 1.f, o, part, nparts);
+  else
+    sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+        slab, stride, M, g.nG, g.L, 1.f, 1.f, o, 0, 1);
   return check_launch("ode_self_bwd(sym eta merge)");
 }
 

@@ -372,8 +372,9 @@ struct SymBwdEtaPk {
 
 template <int D>
 __global__ __launch_bounds__(256) void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,
-                                                             float* __restrict__ slab, int64_t slot_stride) {
-  sym_pk_body<SymBwdEtaPk<D>>(a, sc, M, nG, L, slab, slot_stride, 0, 1);
+                                                             float* __restrict__ slab, int64_t slot_stride,
+                                                             int qoff, int qstride) {
+  sym_pk_body<SymBwdEtaPk<D>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 }  // namespace dicp
