@@ -251,7 +251,9 @@ def _main(out):
             avg_s = d["ms"] / d["launches"] * 1e-3
             flops_per_launch = d["flops"] / d["launches"]
             achieved = flops_per_launch / avg_s / 1e12
-            traffic = load_traffic(dom)
+            # committed PMC summary: whole-size single-device launches of the default workload
+            # (tools/pmc_probe.py); not the pair-subset launches of a row split
+            traffic = load_traffic(dom) if world == 1 and wl.get("N") == 100000 else None
             # compute-bound: priced against the dense FP32 peak, 157.3 TF/s on MI355X, which is
             # both the f32 MFMA rate and the packed-VALU rate (MI355X_MICROARCH.md); the pair
             # kernels run on the VALU (3-wide dot products + exp: no contraction for MFMA)
@@ -271,9 +273,10 @@ def _main(out):
                                    else "the timed iterations",
                     "note": "pair kernels are fp32 VALU/exp-bound (O(N) bytes, O(N^2) work): "
                             "compute roofline, HBM bytes reported as alg_hbm_GBps/traffic; traffic "
-                            "(rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, profiles/pmc_traffic.json) is "
-                            "dominated by the per-column-split partial slabs (S x M x outputs x 4 B) "
-                            "that the deterministic merge reads back"}
+                            "(rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch, the gfx950 correction of "
+                            "MI355X_MICROARCH.md; profiles/pmc_traffic.json; default workload at N=1 only) "
+                            "is dominated by the deterministic partial slots (written once, read once "
+                            "by the merge), ~2% of HBM bandwidth over the launch"}
         base = None
         if not args.no_cpu_baseline and world == 1 and pair_counts:
             try:

@@ -2,9 +2,9 @@
 
 gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE = TCC_EA0_RDREQ x 64 B reads
 exactly 1/2 of the bytes of a wide (16 B/lane) coalesced streaming read; for other access
-widths it is uncalibrated.  Our pair kernels read their inputs with 4-B and 16-B loads, so
-we report both the raw value and the x2-corrected upper estimate, and use the raw
-FETCH_SIZE + WRITE_SIZE (KB x 1024) as `hbm_bytes_per_launch` (a lower bound).
+widths it is uncalibrated.  `hbm_bytes_per_launch` applies the guide's gfx950 correction
+(2 x FETCH_SIZE + WRITE_SIZE, KB x 1024); the raw sum is kept as `hbm_bytes_per_launch_raw`
+(our kernels also use 4-B loads, for which the factor is uncalibrated: the two bracket it).
 
     python tools/pmc_traffic.py <dir with *_counter_collection.csv>
 """
@@ -42,8 +42,8 @@ def main():
         fetch = sum(c.get("FETCH_SIZE", [0])) / max(1, len(c.get("FETCH_SIZE", [1])))
         write = sum(c.get("WRITE_SIZE", [0])) / max(1, len(c.get("WRITE_SIZE", [1])))
         out[k] = {"fetch_kb_per_launch": fetch, "write_kb_per_launch": write,
-                  "hbm_bytes_per_launch": (fetch + write) * 1024,
-                  "hbm_bytes_per_launch_fetch_x2": (2 * fetch + write) * 1024,
+                  "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+                  "hbm_bytes_per_launch_raw": (fetch + write) * 1024,
                   "launches": len(c.get("FETCH_SIZE", c.get("WRITE_SIZE", [])))}
     json.dump(out, sys.stdout, indent=1)
     print()
