@@ -107,6 +107,18 @@ def load_traffic(kernel_name):
         return None
 
 
+def load_issue(kernel_name):
+    """Effective clock under load and VALU issue occupancy from the committed SQ/GRBM pass
+    (tools/pmc_issue.py -> profiles/pmc_issue.json), if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_issue.json")
+    try:
+        with open(path) as f:
+            d = json.load(f).get(kernel_name, {})
+        return d.get("eff_clock_GHz"), d.get("valu_issue_busy_per_simd")
+    except Exception:
+        return None, None
+
+
 def main():
     # the driver parses ONE JSON line from stdout: everything else (e.g. the reference's
     # "GMM optimization - reached maximum number of iterations" message) goes to stderr
@@ -277,6 +289,13 @@ def _main(out):
                             "MI355X_MICROARCH.md; profiles/pmc_traffic.json; default workload at N=1 only) "
                             "is dominated by the deterministic partial slots (written once, read once "
                             "by the merge), ~2% of HBM bandwidth over the launch"}
+            clk, busy = load_issue(dom) if traffic is not None else (None, None)
+            if clk:
+                # the 157.3 TF/s peak assumes the 2.4 GHz peak clock; under this load the chip
+                # runs at the DVFS clock GRBM_GUI_ACTIVE reports (profiles/pmc_issue.json)
+                roof["pmc_eff_clock_GHz"] = round(clk, 3)
+                roof["pmc_valu_issue_busy"] = round(busy, 3) if busy else None
+                roof["frac_at_eff_clock"] = round(achieved / (FP32_PEAK_TFLOPS * clk / 2.4), 4)
         base = None
         if not args.no_cpu_baseline and world == 1 and pair_counts:
             try:
