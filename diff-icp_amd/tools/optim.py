@@ -27,12 +27,16 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
         nonlocal best_L, best_p
         optimizer.zero_grad()
         L = lossfunc(*p)
+        # backward is queued BEFORE the host reads the loss (optim.py:41-47 reads it first): the
+        # gradient does not depend on the read and p is not modified by backward, so results are
+        # unchanged, but the host no longer drains the stream between the forward shooting and
+        # its adjoint -- the backward's host-side setup overlaps the forward's kernels
+        L.backward()
         Ld = L.detach().item()
         iter_L.append(Ld)
         if Ld < best_L:
             best_L = Ld
             best_p = [a.clone().detach() for a in p]
-        L.backward()
         return L
 
     i, keepOn, L = 0, True, math.inf
