@@ -277,6 +277,10 @@ def _main(out):
                     "pairs_per_launch": d["pairs"] / d["launches"],
                     "flops_per_pair": _lib.FLOPS_PER_PAIR.get(dom),
                     "flops_source": "SURVEY.md 8(d) per-unit figure x ordered pairs (M^2)",
+                    "exec_flops_per_pair": _lib.EXEC_FLOPS_PER_PAIR.get(dom, _lib.FLOPS_PER_PAIR.get(dom)),
+                    "frac_executed": round(achieved / FP32_PEAK_TFLOPS *
+                                           _lib.EXEC_FLOPS_PER_PAIR.get(dom, _lib.FLOPS_PER_PAIR.get(dom))
+                                           / _lib.FLOPS_PER_PAIR.get(dom), 4),
                     "alg_bytes_per_launch": d["bytes"] / d["launches"],
                     "alg_hbm_GBps": round(d["bytes"] / d["launches"] / avg_s / 1e9, 3),
                     "share_of_step_time": round(d["ms"] / prof_iters * 1e-3 / (elapsed / args.steps), 3),

@@ -152,6 +152,11 @@ FLOPS_PER_PAIR = {
     "ode_ext_fwd": 22, "ode_ext_bwd": (36 + 49) / 2, "gmm_estep": 37, "gmm_mstep": 31,
     "gmm_targets": 32, "ridge_cg": 15,
 }
+# Executed fp32 arithmetic per ordered pair where it differs from the algorithmic figure
+# (FMA = 2 flop, from the hot loop's instruction counts, tools/isa_loop_stats.py): the
+# symmetric pair-once VJP evaluates each unordered pair once.  bench.py reports the fraction
+# of the peak on both counts (roofline.frac = algorithmic, roofline.frac_executed).
+EXEC_FLOPS_PER_PAIR = {"ode_self_bwd": 53}
 
 
 class KernelProfile:
@@ -424,6 +429,13 @@ def gmm_mstep(X, T2, mu, w2, sigma: float):
     N, D = X.shape
     C = mu.shape[0]
     colstats = torch.empty((C, D + 1), device=X.device, dtype=torch.float32)
+    if N == 0:
+        # neutral statistics of an empty shard (a rank that owns no points in a sharded
+        # atlas): log-weight -inf, mean 0; the cross-rank combine in GMM.EM_step gives them
+        # weight exp(-inf) = 0
+        colstats[:, 0] = float("-inf")
+        colstats[:, 1:] = 0.0
+        return colstats
     ws, nb = _workspace(WS_GMM_MSTEP, N, C, D, X.device)
     rc = _launch("gmm_mstep", N * C, 4 * (N * (D + 1) + 2 * C * (D + 1)),
                  lambda: lib().dicp_gmm_mstep_f32(_ptr(X), _ptr(T2), N, _ptr(mu), _ptr(w2), C, D, float(sigma),

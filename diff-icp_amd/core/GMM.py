@@ -122,8 +122,12 @@ class GaussianMixtureUnif(torch.nn.Module):
         """Outlier reference volume = bounding-box volume of X (GMM.py:163-171); global
         bounding box across ranks when sharded."""
         if self.outliers is not None:
-            lo = X.min(dim=0)[0]
-            hi = X.max(dim=0)[0]
+            if X.shape[0] == 0:     # empty shard: neutral bounds for the cross-rank min / max
+                lo = torch.full((X.shape[1],), float("inf"), dtype=X.dtype, device=X.device)
+                hi = torch.full((X.shape[1],), float("-inf"), dtype=X.dtype, device=X.device)
+            else:
+                lo = X.min(dim=0)[0]
+                hi = X.max(dim=0)[0]
             if _comm_active(self.comm):
                 lo = _gather_rows(lo, self.comm).min(0)[0]
                 hi = _gather_rows(hi, self.comm).max(0)[0]

@@ -66,12 +66,16 @@ class LDDMMModel:
         self.try_trajcost_optim = False
         self.row_split = None
 
-    def set_row_split(self, group=None, enable=True):
+    def set_row_split(self, group=None, enable=True, exact_reduce=None, verify=None):
         """Split every dense Euler shooting of this model over the ranks of a torch.distributed
         group (extension; core/rowsplit.py): all ranks must make the same
-        calls (the host logic runs replicated).  enable=False restores single-device shooting."""
+        calls (the host logic runs replicated).  enable=False restores single-device shooting.
+        exact_reduce / verify: see RowSplit (rank-ordered VJP sums / cross-rank bit checks).
+        The L-BFGS divergence fallback draws from a generator seeded identically on every rank
+        (tools/optim.py), so the replicated iterates stay in lockstep whatever each rank's
+        global RNG state is."""
         from .rowsplit import RowSplit
-        self.row_split = RowSplit(group) if enable else None
+        self.row_split = RowSplit(group, exact_reduce=exact_reduce, verify=verify) if enable else None
 
     def set_integration_scheme(self, scheme: str):
         self.scheme = scheme

@@ -98,7 +98,10 @@ class MultiPSR:
                 allx0s = torch.cat(tuple(self.x0[:, s]), dim=0)
                 mean, std = allx0s.mean(dim=0), allx0s.std()
             else:
-                loc = torch.cat(tuple(self.x0[k, s] for k in self.frames), dim=0).double()
+                parts = tuple(self.x0[k, s] for k in self.frames)
+                # a rank may own no frames (K < world): it contributes zero sums
+                loc = (torch.cat(parts, dim=0) if parts else
+                       torch.empty((0, self.D), **self.dataspec)).double()
                 n = _sum_ranks(float(loc.shape[0]), self.comm).item()
                 s1 = _gather_rows(loc.sum(0).to(**self.compspec).double(), self.comm).sum(0)
                 s2 = _sum_ranks((loc ** 2).sum().to(self.compspec["device"]), self.comm)
@@ -330,22 +333,31 @@ class DiffPSR(MultiPSR):
         nconc = min(int(nconc), len(frames))
         if nconc <= 1 or self.LMi.row_split is not None:
             return {k: self._optimize_frame(k, nmax, tol) for k in frames}
+        import threading
         from concurrent.futures import ThreadPoolExecutor
         main = torch.cuda.current_stream()
         streams = [torch.cuda.Stream() for _ in range(nconc)]
         for st in streams:
             st.wait_stream(main)        # inputs (q0, a0, targets) were produced on `main`
+        # one stream per worker THREAD (not per frame index): a thread that finishes early
+        # and picks up the next frame keeps its own stream, so two frames driven by two
+        # threads never share (and serialise on) one stream
+        local = threading.local()
+        lock = threading.Lock()
+        free = list(streams)
 
-        def work(i_k):
-            i, k = i_k
-            st = streams[i % nconc]
+        def work(k):
+            st = getattr(local, "stream", None)
+            if st is None:
+                with lock:
+                    st = local.stream = free.pop()
             with torch.cuda.stream(st):
                 out = self._optimize_frame(k, nmax, tol)
             st.synchronize()            # results are consumed on `main` afterwards
             return k, out
 
         with ThreadPoolExecutor(max_workers=nconc) as ex:
-            return dict(ex.map(work, list(enumerate(frames))))
+            return dict(ex.map(work, frames))
 
     def Reg_opt(self, nmax=10, tol=1e-3):
         """Per-frame LDDMM optimisation (PSR.py:521-569), local frames only when sharded."""

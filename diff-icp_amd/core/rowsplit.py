@@ -11,9 +11,10 @@ and per ODE evaluation
     Q = r mod W, dicp_lddmm_ode_self_bwd_part_f32) for all rows, then ONE all-reduce sums the
     parts (M x 2D floats).
 Every collective returns bitwise-identical data on all ranks (all-gather is exact; an
-all-reduce reduces each element once and broadcasts it), and the divergence partials are
-combined in rank order, so every rank runs the same L-BFGS iterates and takes the same
-decisions -- the host logic above (LBFGS, EM, PSR) runs replicated, unchanged.
+all-reduce reduces each element once and broadcasts it -- `exact_reduce` replaces it by an
+all-gather + rank-ordered sum, `verify` checks it), and the scalar partials (divergence,
+Hamiltonian) are combined in rank order, so every rank runs the same L-BFGS iterates and
+takes the same decisions -- the host logic above (LBFGS, EM, PSR) runs replicated, unchanged.
 """
 from __future__ import annotations
 
@@ -25,11 +26,23 @@ class RowSplit:
     """Rank / world of a torch.distributed process group (RCCL over xGMI on the GPU box,
     gloo in the CPU tests) and the two collectives the split shooting needs."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, exact_reduce=None, verify=None):
+        """exact_reduce: sum the per-step VJP parts by all-gather + rank-ordered sum instead of
+        an all-reduce (bitwise identical on every rank by construction, W x the bytes; default
+        from DICP_ROWSPLIT_EXACT, off).  verify: after every all-reduce, all-gather a float64
+        checksum of the result and raise if the ranks disagree (one host sync per call; default
+        from DICP_ROWSPLIT_VERIFY, off) -- the check that the replicated L-BFGS cannot diverge
+        because a collective returned different bits on different ranks."""
+        import os
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self._gather_base = dist.get_backend(group) != "gloo"
+        env = os.environ.get
+        self.exact_reduce = bool(int(env("DICP_ROWSPLIT_EXACT", "0"))) if exact_reduce is None \
+            else bool(exact_reduce)
+        self.verify = bool(int(env("DICP_ROWSPLIT_VERIFY", "0"))) if verify is None else bool(verify)
+        self.verified_calls = 0
 
     def rows(self, M: int):
         """(row0, nrows, per): this rank's row slice; per = ceil(M / W) (padded chunk)."""
@@ -47,9 +60,41 @@ class RowSplit:
             dist.all_gather(list(out.chunk(self.world)), local, group=self.group)
         return out
 
+    def sum_ordered(self, t: torch.Tensor) -> torch.Tensor:
+        """Cross-rank sum as all-gather + a sum in rank order: the same bits on every rank
+        whatever algorithm the backend picks (used for the small (H0, div) scalars and, with
+        exact_reduce, for the VJP parts)."""
+        allb = self.all_gather(t.reshape(-1).contiguous()).view(self.world, -1)
+        s = allb[0].clone()
+        for r in range(1, self.world):
+            s = s + allb[r]
+        return s.view(t.shape)
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        """In-place cross-rank sum of t.  An RCCL all-reduce (ring or tree) reduces each element
+        once and broadcasts it, so every rank receives the same bits; exact_reduce makes that
+        hold by construction, verify checks it."""
+        if self.exact_reduce:
+            t.copy_(self.sum_ordered(t))
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        if self.verify:
+            self.check_identical(t)
         return t
+
+    def check_identical(self, t: torch.Tensor) -> None:
+        """Raise if t is not bitwise the same on every rank (float64 checksum of the values
+        and of their bit patterns, all-gathered)."""
+        flat = t.reshape(-1)
+        bits = flat.contiguous().view(torch.int32).to(torch.float64) if flat.dtype == torch.float32 \
+            else flat.to(torch.float64)
+        w = torch.arange(1, flat.numel() + 1, device=flat.device, dtype=torch.float64)
+        cs = torch.stack([(bits * w).sum(), flat.to(torch.float64).sum()])
+        allc = self.all_gather(cs).view(self.world, 2).cpu()
+        if not bool((allc == allc[0]).all()):
+            raise RuntimeError(f"row split: a collective returned different data on different "
+                               f"ranks (checksums {allc.tolist()}): the replicated L-BFGS would diverge")
+        self.verified_calls += 1
 
     # -------------------------------------------------------------------------------
     def gather_rows(self, parts, M: int, scalar=None):

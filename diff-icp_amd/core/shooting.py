@@ -89,7 +89,7 @@ class ShootFn(torch.autograd.Function):
                                                                  want_h=True)
                     loc = torch.stack([h_l.sum(), g_l.sum() if g_l is not None else h_l.sum() * 0])
                     (v0, mG0), _ = split.gather_rows([v_l, mG_l], M)
-                    sums = split.all_reduce_(loc)   # (H0, div): identical on every rank
+                    sums = split.sum_ordered(loc)   # (H0, div): rank-ordered, same bits everywhere
                     H0 = sums[0]
                     torch.add(q, v0, alpha=dt, out=Q[t + 1])
                     torch.add(p, mG0, alpha=dt, out=P[t + 1])

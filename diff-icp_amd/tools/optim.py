@@ -12,12 +12,21 @@ import torch
 from .lbfgs import CompactLBFGS
 
 
-def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
+FALLBACK_SEED = 0x5EED
+
+
+def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator=None):
     """Returns (best_p list, best_L, nsteps, change) exactly as optim.py:10-110:
     L-BFGS(max_iter=20, max_eval=100, history_size=100, strong_wolfe) steps; on NaN /
     increase / > errthresh fall back to the best parameters seen (or a 1% random
     perturbation) and restart without line search; stop when the RMS parameter change is
-    below tol x RMS parameter value."""
+    below tol x RMS parameter value.
+
+    The perturbation (optim.py:85 draws it from torch's global RNG) is drawn from `generator`,
+    by default a dedicated one seeded with FALLBACK_SEED at the first fallback of this call:
+    the result then does not depend on the global RNG state, ranks of a row split (which must
+    stay in lockstep) draw the same numbers, and concurrent frames (one host thread each)
+    do not race on a shared generator."""
     p = [a.clone().contiguous().detach().requires_grad_(True) for a in p0]
     optimizer = CompactLBFGS(p, max_iter=20, max_eval=100, history_size=100,
                              line_search_fn="strong_wolfe")
@@ -59,7 +68,11 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8):
                 print("L-BFGS optimization. Found an intermediate 'best_p' value for this iteration.")
             else:
                 rmod = 0.01
-                p = [a + rmod * a.std() * torch.randn(a.shape, dtype=a.dtype, device=a.device)
+                if generator is None:
+                    generator = torch.Generator(device=best_p[0].device)
+                    generator.manual_seed(FALLBACK_SEED)
+                p = [a + rmod * a.std() * torch.randn(a.shape, dtype=a.dtype, device=a.device,
+                                                      generator=generator)
                      for a in best_p]
                 L = lossfunc(*p)
                 print("L-BFGS optimization. Trying a random perturbation of parameter from its "

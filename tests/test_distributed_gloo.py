@@ -1,8 +1,9 @@
-"""World-size-2 (gloo, CPU) test of the frame-sharded atlas path: each rank owns half of the
-frames, Reg_opt is rank-local, GMM_opt exchanges the per-component sufficient statistics.
-Kernels are replaced by the oracle-backed executable spec (tests/fake_hip.py), so this
-checks the sharding / exchange logic; results must equal the single-process run on all
-frames."""
+"""Multi-rank (gloo, CPU) tests of the frame-sharded atlas path: each rank owns the frames
+k = rank mod W, Reg_opt is rank-local, GMM_opt exchanges the per-component sufficient
+statistics.  Kernels are replaced by the oracle-backed executable spec (tests/fake_hip.py),
+so this checks the sharding / exchange logic; results must equal the single-process run on
+all frames.  Cases: world 2 / 4 frames, and world 3 / 2 frames with outliers and a
+reinitialize_GMM (rank 2 owns no frame and must still join every collective)."""
 import os
 import socket
 import sys
@@ -23,16 +24,16 @@ def _free_port():
     return port
 
 
-def _frames():
+def _frames(K=4):
     g = torch.Generator().manual_seed(5)
     out = []
-    for k in range(4):
+    for k in range(K):
         base = torch.rand(50, 2, generator=g)
         out.append(base + 0.03 * torch.sin(6.28 * base[:, [1, 0]]) * (1 + 0.5 * k))
     return out
 
 
-def _run(world, rank, comm):
+def _run(world, rank, comm, K=4, outliers=False):
     sys.path.insert(0, HERE)
     sys.path.insert(0, ROOT)
     import fake_hip
@@ -41,13 +42,16 @@ def _run(world, rank, comm):
     from difficp_amd.core.LDDMM import LDDMMModel
     from difficp_amd.core.PSR import DiffPSR
     spec = {"device": "cpu", "dtype": torch.float32}
-    frames = _frames()
+    frames = _frames(K)
     g = torch.Generator().manual_seed(9)
     mu0 = torch.rand(6, 2, generator=g)
-    GM = GaussianMixtureUnif(mu0, sigma=0.1, spec=spec)
+    GM = GaussianMixtureUnif(mu0, sigma=0.1, use_outliers=outliers, spec=spec)
     LM = LDDMMModel(sigma=0.25, D=2, lambd=100.0, version="hybrid", scheme="Euler", nt=5, spec=spec)
     P = DiffPSR(frames, GM, LM, dataspec=spec, compspec=spec, comm=comm)
     P.printstuff = False
+    if outliers:
+        torch.manual_seed(11)          # reinitialize_GMM draws on rank 0 and broadcasts
+        P.reinitialize_GMM()
     res = {"FE0": P.FE}
     P.GMM_opt(max_iterations=5, tol=1e-6)
     res["FE_gmm"] = P.FE
@@ -61,36 +65,37 @@ def _run(world, rank, comm):
     return res
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, K, outliers):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     import torch.distributed as dist
     torch.set_num_threads(1)  # no OpenMP oversubscription across the worker processes
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _run(world, rank, True)
+        res = _run(world, rank, True, K, outliers)
         q.put((rank, {k: (v if not isinstance(v, torch.Tensor) else v.numpy()) for k, v in res.items()
                       if k != "x1"}, {k: v.numpy() for k, v in res["x1"].items()}))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_atlas_matches_single_process():
+@pytest.mark.parametrize("world,K,outliers", [(2, 4, False), (3, 2, True)])
+def test_sharded_atlas_matches_single_process(world, K, outliers):
     import numpy as np
-    single = _run(1, 0, None)
+    single = _run(1, 0, None, K, outliers)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, K, outliers)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=300) for _ in range(2)]
+    out = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
     for rank, res, x1 in out:
-        assert res["frames"] == [k for k in range(4) if k % 2 == rank]
+        assert res["frames"] == [k for k in range(K) if k % world == rank]
         for key in ("FE0", "FE_gmm", "FE_reg"):
             assert abs(res[key] - single[key]) < 1e-4 * abs(single[key]), (rank, key, res[key], single[key])
         assert abs(res["sigma"] - single["sigma"]) < 1e-5 * single["sigma"]
@@ -98,6 +103,7 @@ def test_sharded_atlas_matches_single_process():
         assert np.abs(res["w"] - single["w"].numpy()).max() < 1e-4
         for k, v in x1.items():
             assert np.abs(v - single["x1"][k].numpy()).max() < 1e-4, (rank, k)
-    # both ranks hold bit-identical GMM parameters
-    assert np.array_equal(out[0][1]["mu"], out[1][1]["mu"])
-    assert out[0][1]["sigma"] == out[1][1]["sigma"]
+    # all ranks hold bit-identical GMM parameters
+    for r in range(1, world):
+        assert np.array_equal(out[0][1]["mu"], out[r][1]["mu"])
+        assert out[0][1]["sigma"] == out[r][1]["sigma"]

@@ -92,6 +92,25 @@ def test_em_step(dev, opt, N, C, D, outl):
             assert abs(G.outliers["eta0"] - st["outliers"]["eta0"]) < 1e-4
 
 
+def test_em_step_empty_shard(dev):
+    """A rank that owns no points (sharded atlas with fewer frames than ranks): the HIP passes
+    return neutral statistics (M-step log-weight -inf, mean 0) instead of failing, so the
+    rank can join the cross-rank exchange."""
+    from difficp_amd import _lib
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    mu = torch.rand(7, 3, device=dev)
+    X = torch.empty((0, 3), device=dev)
+    w2 = torch.zeros(7, device=dev)
+    cs = _lib.gmm_mstep(X, torch.empty(0, device=dev), mu, w2, 0.1)
+    assert cs.shape == (7, 4)
+    assert bool(torch.isneginf(cs[:, 0]).all()) and bool((cs[:, 1:] == 0).all())
+    G = GaussianMixtureUnif(mu, sigma=0.1, use_outliers=True, spec={"device": dev, "dtype": torch.float32})
+    G.set_vol0(X)        # neutral bounds, no exception (vol0 is only meaningful once gathered)
+    G.outliers["vol0"] = 1.0
+    Y, Cfe, FE = G.EM_step(X, skip_M=True)
+    assert Y.shape == (0, 3)
+
+
 def test_em_skip_M_and_loglik(dev):
     from difficp_amd.core.GMM import GaussianMixtureUnif
     g = torch.Generator().manual_seed(5)

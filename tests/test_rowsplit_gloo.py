@@ -23,7 +23,7 @@ def _free_port():
     return port
 
 
-def _run(split):
+def _run(split, mode=None):
     sys.path.insert(0, HERE)
     sys.path.insert(0, ROOT)
     import fake_hip
@@ -40,7 +40,7 @@ def _run(split):
     tgt = q0 + 0.02 * torch.randn(M, 3, generator=g)
     LM = LDDMMModel(sigma=0.2, D=3, lambd=100.0, version="hybrid", scheme="Euler", nt=5, spec=spec)
     if split:
-        LM.set_row_split()
+        LM.set_row_split(exact_reduce=mode == "exact", verify=mode == "verify")
     p = p0.clone().requires_grad_(True)
     sh = LM.Shoot(q0, p)
     L = LM.trajloss(sh) + ((sh[-1][0] - tgt) ** 2).sum()
@@ -52,34 +52,36 @@ def _run(split):
     # 2. one diff-ICP iteration of a small two-set match (GMM_opt + Reg_opt(nmax=1))
     psr = workloads.build_two_set(120, torch.device("cpu"), seed=2, nt=5)
     if split:
-        psr.LMi.set_row_split()
+        psr.LMi.set_row_split(exact_reduce=mode == "exact", verify=mode == "verify")
     workloads.psr_iteration(psr, max_repeat_GMM=3, tol=1e-6)
+    if split and mode == "verify":   # every VJP all-reduce was checked bitwise across ranks
+        res["verified"] = torch.tensor(float(LM.row_split.verified_calls + psr.LMi.row_split.verified_calls))
     res["FE"] = torch.tensor(float(psr.FE))
     res["a0"] = psr.a0[0].detach().clone()
     return res
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     import torch.distributed as dist
     torch.set_num_threads(1)  # W processes on a few cores: no OpenMP oversubscription
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _run(True)
+        res = _run(True, mode)
         q.put((rank, {k: v.numpy() for k, v in res.items()}))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_rowsplit_matches_single_process(world):
+@pytest.mark.parametrize("world,mode", [(2, "exact"), (3, "verify")])
+def test_rowsplit_matches_single_process(world, mode):
     import numpy as np
     single = {k: v.numpy() for k, v in _run(False).items()}
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(world)]
@@ -88,6 +90,8 @@ def test_rowsplit_matches_single_process(world):
         assert p.exitcode == 0
     out.sort(key=lambda t: t[0])
     for rank, res in out:
+        if mode == "verify":
+            assert float(res.pop("verified")) > 0
         # a0 comes out of L-BFGS, which amplifies the fp32 rounding of a different summation
         # order of the gradient (sum of per-rank parts)
         for key, tol in (("q1", 2e-5), ("cost1", 2e-5), ("L", 2e-5), ("grad", 2e-5), ("a0", 5e-3)):
