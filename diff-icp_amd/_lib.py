@@ -51,6 +51,10 @@ _SIGNATURES = {
                                          _P, _SZ, _P],
     "dicp_lddmm_euler_step_rows_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P,
                                        _P, _SZ, _P],
+    "dicp_lddmm_ode_self_fwd_ord_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
+                                        _P, _SZ, _P],
+    "dicp_lddmm_euler_step_ord_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P, _P,
+                                      _P, _SZ, _P],
     "dicp_lddmm_ode_self_bwd_part_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _INT, _INT, _P,
                                          _P, _P, _SZ, _P],
     "dicp_kernel_ridge_cg_f32": [_P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _INT, _INT, _P, _SZ, _P],
@@ -136,6 +140,16 @@ def _ptr(t):
 
 def _stream(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _order(order, n: int, device):
+    """Optional row visit order (int32 permutation of n rows, on the device) or None."""
+    if order is None:
+        return None
+    if (not isinstance(order, torch.Tensor) or order.dtype != torch.int32 or order.numel() != n
+            or order.device != device):
+        raise ValueError(f"row order must be an int32 device tensor of {n} row indices")
+    return order.contiguous()
 
 
 # ---------------------------------------------------------------------------------------
@@ -260,11 +274,14 @@ def radius_count(x, y, R: float):
 # ---------------------------------------------------------------------------------------
 # Fused LDDMM ODE
 # ---------------------------------------------------------------------------------------
-def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = False):
+def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = False, order=None):
+    """(v, mG, g rows, h rows) of the fused ODE (dicp_lddmm_ode_self_fwd_ord_f32); order: optional
+    int32 row visit order (spatial grouping for the matrix-core forward, see spatial_order)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
+    order = _order(order, M, dev)
     v = torch.empty_like(q)
     mG = torch.empty_like(q)
     g = torch.empty(M, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
@@ -273,20 +290,22 @@ def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = 
         return v, mG, g, h
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, dev)
     rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), M * M, 4 * M * (4 * D + 2),
-                 lambda: lib().dicp_lddmm_ode_self_fwd_f32(_ptr(q), _ptr(p), M, D, float(sigma), float(eta),
-                                           _ptr(v), _ptr(mG), _ptr(g), _ptr(h), _ptr(ws), nb,
-                                           _stream(dev)))
+                 lambda: lib().dicp_lddmm_ode_self_fwd_ord_f32(_ptr(q), _ptr(p), M, 0, M, D, float(sigma),
+                                                               float(eta), _ptr(order), _ptr(v), _ptr(mG),
+                                                               _ptr(g), _ptr(h), _ptr(ws), nb, _stream(dev)))
     _check_rc(rc, "ode_self_fwd")
     return v, mG, g, h
 
 
 def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=None, p_out=None,
-               g_out=None):
-    """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_f32);
-    q_out / p_out / g_out: optional contiguous destinations (must not overlap q, p)."""
+               g_out=None, order=None):
+    """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_ord_f32);
+    q_out / p_out / g_out: optional contiguous destinations (must not overlap q, p); order:
+    optional int32 row visit order (see ode_self_fwd)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
+    order = _order(order, M, q.device)
     qn = torch.empty_like(q) if q_out is None else q_out
     pn = torch.empty_like(q) if p_out is None else p_out
     for t, name in ((qn, "q_out"), (pn, "p_out")):
@@ -301,9 +320,9 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
         return qn, pn, g
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, q.device)
     rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), M * M, 4 * M * (4 * D + 1),
-                 lambda: lib().dicp_lddmm_euler_step_f32(_ptr(q), _ptr(p), M, D, float(sigma), float(eta),
-                                                         float(dt), _ptr(qn), _ptr(pn), _ptr(g), _ptr(ws),
-                                                         nb, _stream(q.device)))
+                 lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, 0, M, D, float(sigma),
+                                                             float(eta), float(dt), _ptr(order), _ptr(qn),
+                                                             _ptr(pn), _ptr(g), _ptr(ws), nb, _stream(q.device)))
     _check_rc(rc, "euler_step")
     return qn, pn, g
 
@@ -513,13 +532,15 @@ def kernel_ridge_cg(x, v, sigma: float, alpha: float, eps: float = 1e-6, maxiter
 # Row-split of one frame over ranks (core/rowsplit.py)
 # ---------------------------------------------------------------------------------------
 def ode_self_fwd_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, want_div: bool,
-                      want_h: bool = False):
+                      want_h: bool = False, order=None):
     """Rows [row0, row0 + nrows) of ode_self_fwd against all columns
-    (dicp_lddmm_ode_self_fwd_rows_f32).  Returns (v, mG, g, h) for the slice."""
+    (dicp_lddmm_ode_self_fwd_ord_f32).  Returns (v, mG, g, h) for the slice; order: optional
+    int32 visit order of the slice's rows (indices into the slice)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
+    order = _order(order, nrows, dev)
     v = torch.empty((nrows, D), device=dev, dtype=torch.float32)
     mG = torch.empty_like(v)
     g = torch.empty(nrows, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
@@ -528,21 +549,24 @@ def ode_self_fwd_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, wan
         return v, mG, g, h
     ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
     rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), nrows * M, 4 * (nrows * (2 * D + 2) + 2 * M * D),
-                 lambda: lib().dicp_lddmm_ode_self_fwd_rows_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
-                                                                float(sigma), float(eta), _ptr(v), _ptr(mG),
-                                                                _ptr(g), _ptr(h), _ptr(ws), nb, _stream(dev)))
+                 lambda: lib().dicp_lddmm_ode_self_fwd_ord_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                                                               float(sigma), float(eta), _ptr(order), _ptr(v),
+                                                               _ptr(mG), _ptr(g), _ptr(h), _ptr(ws), nb,
+                                                               _stream(dev)))
     _check_rc(rc, "ode_self_fwd_rows")
     return v, mG, g, h
 
 
 def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: float,
-                    want_div: bool, q_out=None, p_out=None):
-    """Rows [row0, row0 + nrows) of euler_step (dicp_lddmm_euler_step_rows_f32):
-    (q + dt v, p + dt mG, g) for the slice; q_out / p_out: optional contiguous (nrows, D)."""
+                    want_div: bool, q_out=None, p_out=None, order=None):
+    """Rows [row0, row0 + nrows) of euler_step (dicp_lddmm_euler_step_ord_f32):
+    (q + dt v, p + dt mG, g) for the slice; q_out / p_out: optional contiguous (nrows, D);
+    order: optional int32 visit order of the slice's rows."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
+    order = _order(order, nrows, dev)
     qn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if q_out is None else q_out
     pn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if p_out is None else p_out
     for t, name in ((qn, "q_out"), (pn, "p_out")):
@@ -553,9 +577,10 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
         return qn, pn, g
     ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
     rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), nrows * M, 4 * (nrows * (4 * D + 1) + 2 * M * D),
-                 lambda: lib().dicp_lddmm_euler_step_rows_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
-                                                              float(sigma), float(eta), float(dt), _ptr(qn),
-                                                              _ptr(pn), _ptr(g), _ptr(ws), nb, _stream(dev)))
+                 lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                                                             float(sigma), float(eta), float(dt), _ptr(order),
+                                                             _ptr(qn), _ptr(pn), _ptr(g), _ptr(ws), nb,
+                                                             _stream(dev)))
     _check_rc(rc, "euler_step_rows")
     return qn, pn, g
 

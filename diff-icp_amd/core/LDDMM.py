@@ -18,7 +18,7 @@ from ..tools.integrators import EulerIntegrator, RalstonIntegrator
 from ..tools.kernel import GaussKernel, SVDpow
 from ..tools.optim import LBFGS_optimization
 from ..tools.spec import defspec, getspec
-from .shooting import HamiltonianFn, OdeExtFn, OdeFn, ShootFn
+from .shooting import HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootFn
 
 
 class Shoot(list):
@@ -65,6 +65,11 @@ class LDDMMModel:
         self.set_integration_scheme(scheme)
         self.try_trajcost_optim = False
         self.row_split = None
+        # spatial visit order of the support rows for the fused forward passes (shooting.py
+        # spatial_order), memoised per q0 (the support points are fixed over an L-BFGS run);
+        # only the matrix-core forward (library option fwd_alg 3) uses it: set
+        # `row_orders = RowOrderCache()` together with that option
+        self.row_orders = None
 
     def set_row_split(self, group=None, enable=True, exact_reduce=None, verify=None):
         """Split every dense Euler shooting of this model over the ranks of a torch.distributed
@@ -88,6 +93,8 @@ class LDDMMModel:
 
     def __setstate__(self, state):
         self.__dict__.update(state)
+        if self.__dict__.get("row_orders") is not None:
+            self.row_orders = RowOrderCache()
         self.Kernel = GaussKernel(self.Kernel.sigma, self.Kernel.D, self.Kernel.computversion,
                                   spec=defspec)
 
@@ -190,7 +197,7 @@ class LDDMMModel:
         outs = ShootFn.apply(q0.contiguous(), p0.contiguous(),
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
                              float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet),
-                             self.row_split)
+                             self.row_split, getattr(self, "row_orders", None))
         if x0 is None:
             Q, P, C, H0 = outs
             return Shoot(Q, P, C, None, H0)

@@ -14,21 +14,89 @@ integrator (up to fp32 rounding); the trajectory (nt+1 states) stays resident in
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 
 from .. import _lib
 
 
-def _f_self(q, p, sigma, eta, want_div, want_h=False):
+def spatial_order(x: torch.Tensor) -> torch.Tensor:
+    """Morton (Z-order) visit order of the rows of x (N, D), as an int32 permutation on x's
+    device: rows that are close in space get close positions, so the workgroups of the
+    matrix-core forward (csrc/mfma_fwd.hpp) hold compact groups of rows and the fp32 error of
+    its centred channel split stays at the ordered-pair kernels' level whatever the cloud's
+    extent.  10 (3D) / 16 (2D) bits per coordinate over the bounding box; a stable sort, so
+    the order (hence every result) is deterministic."""
+    N, D = x.shape
+    bits = 10 if D == 3 else 16
+    xd = x.detach()
+    lo = xd.amin(0)
+    ext = (xd.amax(0) - lo).clamp_min(1e-30)
+    c = ((xd - lo) * ((2 ** bits - 1) / ext)).to(torch.int64).clamp_(0, 2 ** bits - 1)
+    if D == 3:   # spread 10 bits to every third bit
+        c = (c | (c << 16)) & 0x030000FF
+        c = (c | (c << 8)) & 0x0300F00F
+        c = (c | (c << 4)) & 0x030C30C3
+        c = (c | (c << 2)) & 0x09249249
+    else:        # spread 16 bits to every second bit
+        c = (c | (c << 8)) & 0x00FF00FF
+        c = (c | (c << 4)) & 0x0F0F0F0F
+        c = (c | (c << 2)) & 0x33333333
+        c = (c | (c << 1)) & 0x55555555
+    code = (c << torch.arange(D, device=x.device, dtype=torch.int64)).sum(1)   # disjoint bits
+    return torch.argsort(code, stable=True).to(torch.int32)
+
+
+class RowOrderCache:
+    """spatial_order of the support points, memoised per tensor (q0 is fixed over an L-BFGS
+    run: every closure reuses the order).  Keyed on (storage pointer, version counter, shape):
+    a stale hit after a free / re-allocation still returns a valid permutation of the same
+    length, so results stay correct (only the grouping could be less compact)."""
+
+    def __init__(self, maxsize=32):
+        self._d = {}
+        self._lock = threading.Lock()
+        self.maxsize = maxsize
+
+    # a cache: copies and pickles start empty
+    def __getstate__(self):
+        return {"maxsize": self.maxsize}
+
+    def __setstate__(self, state):
+        self.__init__(state.get("maxsize", 32))
+
+    def __deepcopy__(self, memo):
+        return RowOrderCache(self.maxsize)
+
+    def get(self, x: torch.Tensor, row0: int = 0, n: int = None):
+        n = x.shape[0] - row0 if n is None else n
+        key = (x.data_ptr(), x._version, tuple(x.shape), str(x.device), row0, n)
+        with self._lock:
+            o = self._d.get(key)
+        if o is None:
+            o = spatial_order(x[row0:row0 + n])
+            with self._lock:
+                if len(self._d) >= self.maxsize:
+                    self._d.pop(next(iter(self._d)))
+                self._d[key] = o
+        return o
+
+
+# rows per workgroup of the matrix-core forward: at or below it the order cannot matter
+_ORDER_MIN_ROWS = 256
+
+
+def _f_self(q, p, sigma, eta, want_div, want_h=False, order=None):
     """ODE right-hand side at the support points: (v, mG, div[1]) [+ per-row h]."""
-    v, mG, g, h = _lib.ode_self_fwd(q, p, sigma, eta, want_div, want_h=want_h)
+    v, mG, g, h = _lib.ode_self_fwd(q, p, sigma, eta, want_div, want_h=want_h, order=order)
     div = g.sum().reshape(1) if want_div else None
     return (v, mG, div, h) if want_h else (v, mG, div)
 
 
-def _f_ext(q, p, x, sigma, eta, want_div, want_h=False):
+def _f_ext(q, p, x, sigma, eta, want_div, want_h=False, order=None):
     """ODE with external points: (vq, mGq, div over x [1], vx) [+ per-row h]."""
-    v, mG, _, h = _lib.ode_self_fwd(q, p, sigma, eta, False, want_h=want_h)
+    v, mG, _, h = _lib.ode_self_fwd(q, p, sigma, eta, False, want_h=want_h, order=order)
     vx, gx = _lib.ode_ext_fwd(x, q, p, sigma, eta, want_div)
     div = gx.sum().reshape(1) if want_div else None
     return (v, mG, div, vx, h) if want_h else (v, mG, div, vx)
@@ -56,7 +124,9 @@ class ShootFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None):
+    def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None, orders=None):
+        """orders: optional RowOrderCache; the forward passes then visit the support rows in
+        the spatial order of q0 (kept for every step: the flow moves neighbours together)."""
         ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
         # row-split over ranks (core/rowsplit.py): dense Euler shooting only; other schemes
@@ -77,6 +147,14 @@ class ShootFn(torch.autograd.Function):
             X[0].copy_(x0)
         mids = []  # Ralston intermediate states (needed by the adjoint)
         H0 = v0 = mG0 = None
+        order = order_l = None
+        if orders is not None and eta == 0:
+            if split is not None:
+                r0_, n_, _ = split.rows(M)
+                if n_ > _ORDER_MIN_ROWS:
+                    order_l = orders.get(q0, r0_, n_)
+            elif M > _ORDER_MIN_ROWS:
+                order = orders.get(q0)
         Gd, fused_from = None, None  # fused Euler steps: per-step divergence rows, first step
         for t in range(nt):
             q, p = Q[t], P[t]
@@ -86,7 +164,7 @@ class ShootFn(torch.autograd.Function):
                 r0, n, _ = split.rows(M)
                 if first:
                     v_l, mG_l, g_l, h_l = _lib.ode_self_fwd_rows(q, p, r0, n, sigma, eta, want_div,
-                                                                 want_h=True)
+                                                                 want_h=True, order=order_l)
                     loc = torch.stack([h_l.sum(), g_l.sum() if g_l is not None else h_l.sum() * 0])
                     (v0, mG0), _ = split.gather_rows([v_l, mG_l], M)
                     sums = split.sum_ordered(loc)   # (H0, div): rank-ordered, same bits everywhere
@@ -95,7 +173,8 @@ class ShootFn(torch.autograd.Function):
                     torch.add(p, mG0, alpha=dt, out=P[t + 1])
                     div = sums[1:2]
                 else:
-                    qn_l, pn_l, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div)
+                    qn_l, pn_l, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div,
+                                                           order=order_l)
                     gs = g_l.sum().reshape(1) if g_l is not None else None
                     (qn, pn), div = split.gather_rows([qn_l, pn_l], M, scalar=gs)
                     Q[t + 1].copy_(qn)
@@ -111,14 +190,14 @@ class ShootFn(torch.autograd.Function):
                 if Gd is None:
                     Gd = torch.empty((nt, M), device=dev, dtype=q0.dtype) if want_div else False
                 _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1],
-                                g_out=Gd[t] if want_div else None)
+                                g_out=Gd[t] if want_div else None, order=order)
                 fused_from = t if fused_from is None else fused_from
                 continue
             if has_x:
-                out = _f_ext(q, p, x, sigma, eta, want_div, want_h=first)
+                out = _f_ext(q, p, x, sigma, eta, want_div, want_h=first, order=order)
                 v, mG, div, vx = out[:4]
             else:
-                out = _f_self(q, p, sigma, eta, want_div, want_h=first)
+                out = _f_self(q, p, sigma, eta, want_div, want_h=first, order=order)
                 v, mG, div = out[:3]
                 vx = None
             if first:
@@ -138,9 +217,9 @@ class ShootFn(torch.autograd.Function):
                 pi = torch.add(p, mG, alpha=a)
                 xi = torch.add(x, vx, alpha=a) if has_x else None
                 if has_x:
-                    v2, mG2, div2, vx2 = _f_ext(qi, pi, xi, sigma, eta, want_div)
+                    v2, mG2, div2, vx2 = _f_ext(qi, pi, xi, sigma, eta, want_div, order=order)
                 else:
-                    v2, mG2, div2 = _f_self(qi, pi, sigma, eta, want_div)
+                    v2, mG2, div2 = _f_self(qi, pi, sigma, eta, want_div, order=order)
                     vx2 = None
                 Q[t + 1].copy_(q + (0.25 * dt) * (v + 3.0 * v2))
                 P[t + 1].copy_(p + (0.25 * dt) * (mG + 3.0 * mG2))
@@ -266,7 +345,7 @@ class ShootFn(torch.autograd.Function):
         if gH is not None:
             lq = lq - gH * mG0
             lp = lp + gH * v0
-        return lq, lp, (lx if has_x else None), None, None, None, None, None, None
+        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None
 
 
 class HamiltonianFn(torch.autograd.Function):

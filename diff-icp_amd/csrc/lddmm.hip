@@ -5,6 +5,7 @@
 #include "lddmm_sym.hpp"
 #include "packed.hpp"
 #include "lddmm_sym_pk.hpp"
+#include "mfma_fwd.hpp"
 
 #include <stdlib.h>
 
@@ -40,12 +41,21 @@ int g_bwd_eta_alg = DICP_BWD_ETA_ALG;
 // eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
 // (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair instead of 20 + 1, but 3-5%
 // slower: issue-stalled on its rotating column sums), 2 = packed-FP32 rows (packed.hpp: the
-// thread's two rows as float2, 11 VALU instructions per pair; default, measured 4-11% faster
-// than 0 at 200k-20k on MI355X)
+// thread's two rows as float2, 11 VALU instructions per pair; measured 4-11% faster
+// than 0 at 200k-20k on MI355X), 3 = the column contraction on the matrix cores
+// (mfma_fwd.hpp: VALU evaluates K, one v_mfma_f32_16x16x4_f32 per 64 pairs sums 16 channels;
+// eta = 0 only, eta != 0 keeps 2), 4 = the symmetric pair-once kernel with packed-FP32 rows
+// (lddmm_sym_pk.hpp SymFwdPk; all rows only, row slices take 2)
 #ifndef DICP_FWD_ALG
 #define DICP_FWD_ALG 2
 #endif
 int g_fwd_alg = DICP_FWD_ALG;
+#ifndef DICP_MFMA_RMAX_X100
+#define DICP_MFMA_RMAX_X100 300
+#endif
+struct MfmaRmaxInit {
+  MfmaRmaxInit() { if (mfma_rmax_x100() < 0) mfma_rmax_x100() = DICP_MFMA_RMAX_X100; }
+} g_mfma_rmax_init;
 
 template <class Op>
 int launch_r(int R, const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
@@ -118,8 +128,13 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "fwd_alg")) {
-    if (value < 0 || value > 2) return DICP_ERR_INVALID;
+    if (value < 0 || value > 4) return DICP_ERR_INVALID;
     g_fwd_alg = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "mfma_rmax_x100")) {  // >= 100000: always the MFMA branch, 0: never
+    if (value < 0) return DICP_ERR_INVALID;
+    mfma_rmax_x100() = value;
     return DICP_OK;
   }
   if (!strcmp(name, "bwd_eta_alg")) {
@@ -202,23 +217,30 @@ namespace {
 
 // rows [row0, row0 + nrows) of the pass against all M columns (row-split over ranks);
 // nrows < 0: all rows.  Output pointers in `o` address the row slice.
+// order: optional nrows int32 row indices (a permutation of the slice's rows) that groups
+// spatially close rows into the same workgroup -- used by the matrix-core forward, whose
+// fp32 error grows with the spread of a workgroup's rows (mfma_fwd.hpp); ignored otherwise.
 template <int D>
 int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, double eta,
                    const Outs& o, void* ws, size_t wsb, hipStream_t st, int64_t row0 = 0,
-                   int64_t nrows = -1) {
-  const bool all = nrows < 0;
-  if (all) nrows = M;
+                   int64_t nrows = -1, const int* order = nullptr) {
+  if (nrows < 0) nrows = M;
+  const bool all = row0 == 0 && nrows == M;
   Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
   if (eta != 0.0)
-    return g_fwd_alg == 2
+    return g_fwd_alg >= 2
                ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, true>>("ode_self_fwd_eta(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
-  if (g_fwd_alg == 1 && all)
-    return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st)
-                               : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st);
-  if (g_fwd_alg == 2)
+  if ((g_fwd_alg == 1 || g_fwd_alg == 4) && all)
+    return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st, g_fwd_alg == 4)
+                               : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st, g_fwd_alg == 4);
+  if (g_fwd_alg == 3)
+    return o.ptr[2] != nullptr
+               ? launch_mfma_fwd<D, true>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order)
+               : launch_mfma_fwd<D, false>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order);
+  if (g_fwd_alg == 2 || g_fwd_alg == 4)
     return o.ptr[2] != nullptr
                ? launch_rowred_pk<OpOdeSelfFwdPk<D, true>>("ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_rowred_pk<OpOdeSelfFwdPk<D, false>>("ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st);
@@ -235,7 +257,8 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
                    ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, M)})
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, M),
+                   mfma_fwd_ws_bytes<D, true>(nrows, M), mfma_fwd_ws_bytes<D, false>(nrows, M)})
     m = v > m ? v : m;
   return m;
 }
@@ -252,7 +275,8 @@ size_t ode_self_fwd_ws(int64_t M) {
   a = a > d ? a : d;
   for (size_t e : {rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(M, M)})
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(M, M),
+                   mfma_fwd_ws_bytes<D, true>(M, M), mfma_fwd_ws_bytes<D, false>(M, M)})
     a = a > e ? a : e;
   return a;
 }
@@ -563,6 +587,51 @@ extern "C" int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, in
     case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows);
     case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows);
     default: set_error("euler_step_rows: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+// Ordered forms (rows [row0, row0 + nrows) visited in row_order, or NULL = natural order):
+// the general entry points behind the four above.
+extern "C" int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, int64_t M,
+                                               int64_t row0, int64_t nrows, int D, double sigma,
+                                               double eta, const int32_t* row_order, float* v,
+                                               float* mG, float* g, float* h, void* ws,
+                                               size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
+      (nrows > 0 && (!q || !p || !v || !mG)) || !(sigma > 0)) {
+    set_error("dicp_lddmm_ode_self_fwd_ord_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  if (nrows == 0) return DICP_OK;
+  switch (D) {
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, make_outs(v, mG, g, h), ws, ws_bytes, st, row0, nrows, row_order);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, make_outs(v, mG, g, h), ws, ws_bytes, st, row0, nrows, row_order);
+    default: set_error("ode_self_fwd_ord: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int64_t M,
+                                             int64_t row0, int64_t nrows, int D, double sigma,
+                                             double eta, double dt, const int32_t* row_order,
+                                             float* q_next, float* p_next, float* g, void* ws,
+                                             size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
+      (nrows > 0 && (!q || !p || !q_next || !p_next)) || !(sigma > 0) ||
+      (nrows > 0 && (q_next == q || q_next == p || p_next == q || p_next == p))) {
+    set_error("dicp_lddmm_euler_step_ord_f32: invalid arguments (outputs must not alias inputs)");
+    return DICP_ERR_INVALID;
+  }
+  if (nrows == 0) return DICP_OK;
+  Outs o = make_outs(q_next, p_next, g, nullptr);
+  o.base[0] = q + row0 * D;
+  o.base[1] = p + row0 * D;
+  o.alpha[0] = o.alpha[1] = (float)dt;
+  switch (D) {
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows, row_order);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows, row_order);
+    default: set_error("euler_step_ord: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
 

@@ -771,9 +771,14 @@ __global__ __launch_bounds__(256) void sym_fwd_merge_kernel(const float* __restr
   if (o.ptr[3]) o.ptr[3][i] = epilogue(o, 3, i, 0.5f * pv);
 }
 
+// packed-FP32 variant of the symmetric forward (lddmm_sym_pk.hpp)
+template <int D, bool DIV>
+__global__ void sym_fwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
+                                  int64_t slot_stride);
+
 template <int D, bool DIV>
 int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
-                   hipStream_t st) {
+                   hipStream_t st, bool pk = false) {
   using S = SymFwd<D, DIV>;
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M);
@@ -788,8 +793,12 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   }
   float* slab = reinterpret_cast<float*>(ws);
   const int64_t stride = M * S::W;
-  sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
-                                                                              slab, stride);
+  if (pk)
+    sym_fwd_pk_kernel<D, DIV><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
+        a, sc, M, g.nG, g.L, slab, stride);
+  else
+    sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
+                                                                                slab, stride);
   int rc = check_launch("ode_self_fwd(sym)");
   if (rc) return rc;
   sym_fwd_merge_kernel<D, DIV><<<dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st>>>(

@@ -377,4 +377,78 @@ __global__ __launch_bounds__(256) void sym_bwd_eta_pk_kernel(Args a, Scal sc, in
   sym_pk_body<SymBwdEtaPk<D>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
+// Packed-FP32 rows of the symmetric (pair-once) eta = 0 forward (lddmm_sym.hpp SymFwd): the
+// lane's two rows as float2; per unordered pair the row side (V, Gs', Z') is packed and the
+// column side (K p_i, -Kpp z, -K z) is summed over the two rows in scalar form before the
+// DPP rotation.  Same slots and merge as sym_kernel<SymFwd>.
+template <int D, bool DIV>
+struct SymFwdPk {
+  using S = SymFwd<D, DIV>;
+  static constexpr int W = S::W;
+  struct Prm {};
+  __device__ static Prm params(const Args&, const Scal&) { return Prm{}; }
+  struct Row2 {
+    f2 q[D], p[D];
+  };
+  __device__ static void pack(const typename S::Row& r0, const typename S::Row& r1, Row2& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      r.q[d] = f2{r0.q[d], r1.q[d]};
+      r.p[d] = f2{r0.p[d], r1.p[d]};
+    }
+  }
+  __device__ static void pair_row(const Prm&, const Row2& r, const float* rec, f2* acc) {
+    f2 z[D];
+    f2 r2 = splat(0.f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      z[d] = r.q[d] - splat(rec[d]);
+      r2 = pk_fma(z[d], z[d], r2);
+    }
+    const f2 K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    const float* pj = rec + D;
+    f2 pp = r.p[0] * splat(pj[0]);
+#pragma unroll
+    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+    const f2 Kpp = K * pp;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = pk_fma(K, splat(pj[d]), acc[d]);
+      acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
+      if (DIV) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
+    }
+  }
+  __device__ static void pair_sym(const Prm&, const Row2& r, const float* rec, f2* acc, float* ct) {
+    f2 z[D];
+    f2 r2 = splat(0.f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      z[d] = r.q[d] - splat(rec[d]);
+      r2 = pk_fma(z[d], z[d], r2);
+    }
+    const f2 K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    const float* pj = rec + D;
+    f2 pp = r.p[0] * splat(pj[0]);
+#pragma unroll
+    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+    const f2 Kpp = K * pp;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = pk_fma(K, splat(pj[d]), acc[d]);
+      acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
+      if (DIV) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
+      // column j's side: sum over the lane's two rows, (i, j) -> (j, i) flips z
+      ct[d] = fmaf(K.x, r.p[d].x, K.y * r.p[d].y);
+      ct[D + d] = -fmaf(Kpp.x, z[d].x, Kpp.y * z[d].y);
+      if (DIV) ct[2 * D + d] = -fmaf(K.x, z[d].x, K.y * z[d].y);
+    }
+  }
+};
+
+template <int D, bool DIV>
+__global__ __launch_bounds__(256) void sym_fwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+                                                         float* __restrict__ slab, int64_t slot_stride) {
+  sym_pk_body<SymFwdPk<D, DIV>>(a, sc, M, nG, L, slab, slot_stride, 0, 1);
+}
+
 }  // namespace dicp

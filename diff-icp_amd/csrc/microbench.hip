@@ -104,6 +104,90 @@ __global__ __launch_bounds__(256) void mix_probe(float* out, int iters, float se
   if (s == 12345.f) out[threadIdx.x] = s;
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// MFMA / VALU overlap probes (the matrix-core forward's loop shape): per iteration
+//   MODE 0: 4 independent v_mfma_f32_16x16x4_f32 (MFMA only)
+//   MODE 1: 24 v_fma_f32 + 4 v_exp_f32 on independent chains (VALU only)
+//   MODE 2: both in the same wave, interleaved (each MFMA's A operand = a fresh exp result)
+//   MODE 3: waves 0,2 of the workgroup run MODE 0's body, waves 1,3 MODE 1's (cross-wave)
+template <int MODE>
+__global__ __launch_bounds__(256) void mfma_mix_probe(float* out, int iters, float seed) {
+  const int wv = threadIdx.x >> 6;
+  const bool do_m = MODE == 0 || MODE == 2 || (MODE == 3 && (wv & 1) == 0);
+  const bool do_v = MODE == 1 || MODE == 2 || (MODE == 3 && (wv & 1) == 1);
+  f4v acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = f4v{0.f, 0.f, 0.f, 0.f};
+  float a[6], b = seed * 0.5f, e[4];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) a[k] = seed * (threadIdx.x + k) * 1e-3f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[k] = seed * (threadIdx.x + k) * 1e-7f;
+  const float bm = seed * 1e-3f * (threadIdx.x & 15);
+  for (int it = 0; it < iters; ++it) {
+    if (do_v) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[k] = fmaf(a[k], b, 0.999f);
+        e[r] = __builtin_amdgcn_exp2f(-e[r] * e[r]);
+        if (do_m) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(e[r], bm, acc[r], 0, 0, 0);
+      }
+    } else if (do_m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(e[r], bm, acc[r], 0, 0, 0);
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) s += a[k];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s += e[r] + acc[r][0] + acc[r][1] + acc[r][2] + acc[r][3];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
+typedef short bf8v __attribute__((ext_vector_type(8)));
+
+// The same with v_mfma_f32_16x16x32_bf16 (16 cycles, 16x as many flops): per iteration
+//   MODE 0: 4 MFMAs, MODE 1: 24 FMA + 4 exp, MODE 2: both in one wave (the A operand of each
+//   MFMA takes bits of a fresh exp result)
+template <int MODE>
+__global__ __launch_bounds__(256) void bf16_mix_probe(float* out, int iters, float seed) {
+  f4v acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = f4v{0.f, 0.f, 0.f, 0.f};
+  float a[6], b = seed * 0.5f, e[4];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) a[k] = seed * (threadIdx.x + k) * 1e-3f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[k] = seed * (threadIdx.x + k) * 1e-7f;
+  bf8v bm;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bm[k] = (short)(0x3f80 + (threadIdx.x & 7) + k);
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (MODE >= 1) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[k] = fmaf(a[k], b, 0.999f);
+        e[r] = __builtin_amdgcn_exp2f(-e[r] * e[r]);
+      }
+      if (MODE != 1) {
+        bf8v av = bm;
+        if (MODE == 2) av[0] = (short)(__float_as_uint(e[r]) >> 16);
+        acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bm, acc[r], 0, 0, 0);
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) s += a[k];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s += e[r] + acc[r][0] + acc[r][1] + acc[r][2] + acc[r][3];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
 template <int CTRL>
 __global__ __launch_bounds__(64) void dpp_probe(int* out) {
   const int l = threadIdx.x;
@@ -122,8 +206,8 @@ extern "C" int dicp_mb_dpp(int which, int* out, void* stream) {
 }
 
 // kind: 0 = exp2, 1 = fma, 2 = pk_fma, 3 = dpp(wave_rol:1)+add, 4 = dpp(row_ror:1)+add,
-// 5 = kChains fma + 1 exp2 per iteration.  Returns 0 on success.  ops per launch:
-// blocks*256*iters*kChains (x2 lanes for pk_fma).
+// 5 = kChains fma + 1 exp2 per iteration, 10..13 = mfma_mix_probe<kind - 10>.  Returns 0 on
+// success.  ops per launch: blocks*256*iters*kChains (x2 lanes for pk_fma).
 extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 g(blocks), b(256);
@@ -132,7 +216,15 @@ extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void*
   else if (kind == 2) pkfma_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 3) dppadd_probe<0x134><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 4) dppadd_probe<0x121><<<g, b, 0, st>>>(out, iters, 1.0f);
-  else mix_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 5) mix_probe<<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 10) mfma_mix_probe<0><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 11) mfma_mix_probe<1><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 12) mfma_mix_probe<2><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 13) mfma_mix_probe<3><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 20) bf16_mix_probe<0><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 21) bf16_mix_probe<1><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 22) bf16_mix_probe<2><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else return 1;
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

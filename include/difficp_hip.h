@@ -162,6 +162,23 @@ int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, int64_t M, in
                                    float* q_next, float* p_next, float* g, void* ws,
                                    size_t ws_bytes, dicp_stream_t stream);
 
+/* General forms of the four forward entry points above: rows [row0, row0 + nrows) against
+ * all M columns, the rows visited in `row_order` (nrows int32 indices into the slice, a
+ * permutation of 0..nrows-1; NULL = natural order).  Outputs are indexed like the plain
+ * forms (by row, not by visit order), so the order never changes WHAT is computed, only which
+ * rows share a workgroup: the matrix-core forward (fwd_alg 3) centres the column channels on
+ * its workgroup's rows, and its fp32 error grows with their spread, so a spatial order (e.g.
+ * Morton, _lib.spatial_order) keeps it at the ordered-pair kernels' level for any cloud extent.
+ * No reference counterpart (KeOps has no row grouping to choose). */
+int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                    int64_t nrows, int D, double sigma, double eta,
+                                    const int32_t* row_order, float* v, float* mG, float* g,
+                                    float* h, void* ws, size_t ws_bytes, dicp_stream_t stream);
+int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                  int64_t nrows, int D, double sigma, double eta, double dt,
+                                  const int32_t* row_order, float* q_next, float* p_next,
+                                  float* g, void* ws, size_t ws_bytes, dicp_stream_t stream);
+
 /* Part `part` of `nparts` of dicp_lddmm_ode_self_bwd_f32: gq, gp (M, D) over a subset of
  * the pairs such that the SUM over the parts is the full VJP (eta = 0: the symmetric
  * kernel's quads Q = part mod nparts, every row touched; eta != 0: a row slice, other rows 0).
@@ -243,7 +260,9 @@ const char* dicp_version(void);
 int dicp_supports_dim(int D);
 /* Tuning / A-B knobs (process-wide; results of every setting agree to fp32 summation order):
  *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
- *                  rows (default; for eta != 0: 2 packed, otherwise ordered scalar rows)
+ *                  rows, 3 channel contraction on the matrix cores (default; fp32 error
+ *                  bounded by the rows' spread: pass a spatial row_order);
+ *                  eta != 0: >= 2 packed-FP32 rows, otherwise ordered scalar rows
  *   "bwd_alg"      eta = 0 VJP: 0 / 1 ordered pair algebras, 2 symmetric pair-once, 3 symmetric
  *                  with packed-FP32 rows (default)
  *   "bwd_eta_alg"  eta != 0 VJP: 0 ordered, 1 symmetric, 2 symmetric packed-FP32 (default)

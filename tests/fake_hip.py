@@ -77,7 +77,7 @@ def _self_terms(q, p, sigma, eta):
     return v, -G, g, h
 
 
-def ode_self_fwd(q, p, sigma, eta, want_div, want_h=False):
+def ode_self_fwd(q, p, sigma, eta, want_div, want_h=False, order=None):
     v, mG, g, h = _self_terms(_d(q), _d(p), sigma, eta)
     return (_out(v, q), _out(mG, q), _out(g, q) if (want_div or eta != 0) else None,
             _out(h, q) if want_h else None)
@@ -95,7 +95,7 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta):
     return _out(gq, q), _out(gp, q)
 
 
-def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=None):
+def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=None, order=None):
     v, mG, g, _ = ode_self_fwd(q, p, sigma, eta, want_div)
     if g_out is not None and g is not None:
         g_out.copy_(g)
@@ -200,14 +200,14 @@ def kernel_ridge_cg(x, v, sigma, alpha, eps=1e-6, maxiter=5000, chunk=32):
     return _out(b, v), {"status": st, "iterations": k, "residual2": 0.0, "threshold": 0.0}
 
 
-def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False):
+def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False, order=None):
     v, mG, g, h = ode_self_fwd(q, p, sigma, eta, want_div, want_h)
     sl = slice(row0, row0 + nrows)
     return v[sl].contiguous(), mG[sl].contiguous(), None if g is None else g[sl].contiguous(), \
         None if h is None else h[sl].contiguous()
 
 
-def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_out=None):
+def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_out=None, order=None):
     v, mG, g, _ = ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div)
     sl = slice(row0, row0 + nrows)
     return q[sl] + dt * v, p[sl] + dt * mG, g

@@ -12,6 +12,7 @@ from conftest import rel_err
 from oracle import torch_ref as R
 
 BWD_ALG_DEFAULT = 3  # lddmm.hip g_bwd_alg: symmetric pair-once VJP, packed-FP32 rows
+FWD_ALG_DEFAULT = 2  # lddmm.hip g_fwd_alg: eta = 0 packed-FP32 rows
 BWD_ETA_ALG_DEFAULT = 2  # lddmm.hip g_bwd_eta_alg (DICP_BWD_ETA_ALG)
 
 pytestmark = pytest.mark.gpu
@@ -100,13 +101,13 @@ def test_ode_self_fwd(dev, version, M, D):
     v64, mG64, c64 = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
     v32, mG32, c32 = m32.ODE(q.float(), p.float(), torch.zeros(1))
     H64, H32 = m.Hamiltonian(q, p), m32.Hamiltonian(q.float(), p.float())
-    for alg in (0, 1, 2):  # eta = 0: ordered rows, symmetric pair-once, packed-FP32 rows
+    for alg in (0, 1, 2, 3, 4):  # eta = 0: ordered rows, symmetric, packed rows, MFMA, symmetric packed
         L.set_option("fwd_alg", alg)
         try:
             v, mG, gdiv, h = L.ode_self_fwd(q.float().to(dev), p.float().to(dev), 0.15, m.eta, wl,
                                             want_h=True)
         finally:
-            L.set_option("fwd_alg", 2)
+            L.set_option("fwd_alg", FWD_ALG_DEFAULT)
         assert rel_err(v.cpu(), v64) <= _tol(v64, v32), alg
         assert rel_err(mG.cpu(), mG64) <= _tol(mG64, mG32), alg
         assert rel_err(h.sum().cpu(), H64) <= _tol(H64, H32), alg
@@ -236,11 +237,11 @@ def test_sym_bwd_vs_ordered(dev, M):
 
 @pytest.mark.parametrize("M", [1, 127, 128, 129, 1000, 5000, 50000])
 @pytest.mark.parametrize("want_div", [True, False])
-@pytest.mark.parametrize("alg", [1, 2])
+@pytest.mark.parametrize("alg", [1, 2, 3, 4])
 def test_sym_fwd_vs_ordered(dev, M, want_div, alg):
-    """Symmetric pair-once (alg 1) and packed-FP32 (alg 2) forwards == the ordered-row forward
-    up to fp32 summation order (partial last groups / row pairs included), every output incl.
-    the fused Euler epilogue; deterministic run to run."""
+    """Symmetric pair-once (alg 1), packed-FP32 (alg 2) and matrix-core (alg 3) forwards == the
+    ordered-row forward up to fp32 summation order (partial last groups / row pairs / row tiles
+    included), every output incl. the fused Euler epilogue; deterministic run to run."""
     L = _lib()
     g = torch.Generator().manual_seed(M + 11)
     q = torch.rand(M, 3, generator=g).to(dev)
@@ -254,15 +255,105 @@ def test_sym_fwd_vs_ordered(dev, M, want_div, alg):
         out2 = L.ode_self_fwd(q, p, 0.1, 0.0, want_div, want_h=True)
         qn1, pn1, _ = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div)
     finally:
-        L.set_option("fwd_alg", 2)
+        L.set_option("fwd_alg", FWD_ALG_DEFAULT)
+    # alg 3 splits z = q_i - q_j into centred row / column terms (mfma_fwd.hpp): its fp32
+    # error grows with the rows' spread against sigma -> the SURVEY 8c criterion, 1e-5
+    tol = 1e-5 if alg == 3 else 2e-6
     for k, (a, b) in enumerate(zip(out, ref)):
         if b is None:
             continue
-        assert rel_err(a, b) < 2e-6, (k, rel_err(a, b))
+        assert rel_err(a, b) < tol, (k, rel_err(a, b))
     for a, b in zip(out, out2):
         if a is not None:
             assert torch.equal(a, b)
-    assert rel_err(qn1, qn0) < 1e-7 and rel_err(pn1, pn0) < 2e-6
+    assert rel_err(qn1, qn0) < 1e-7 and rel_err(pn1, pn0) < tol
+
+
+@pytest.mark.parametrize("extent,ordered", [(1.0, False), (1.0, True), (5.0, True), (20.0, True)])
+@pytest.mark.parametrize("M", [1000, 30000])
+def test_mfma_fwd_precision_vs_extent(dev, M, extent, ordered):
+    """The matrix-core forward splits z = q_i - q_j into centred row / column terms; its error
+    grows with the spread of a workgroup's rows against sigma (cancellation).  With the rows
+    visited in spatial order (shooting.spatial_order, what LDDMMModel.Shoot passes) the error
+    stays within the SURVEY 8c criterion (1e-5) for clouds of extent 10 / 50 / 200 sigma;
+    unordered rows only at 10 sigma.  Against float64 sums on 256 sampled rows."""
+    from difficp_amd.core.shooting import spatial_order
+    L = _lib()
+    g = torch.Generator().manual_seed(M + int(extent))
+    q64 = extent * torch.rand(M, 3, generator=g, dtype=torch.float64)
+    p64 = 0.05 * torch.randn(M, 3, generator=g, dtype=torch.float64)
+    sig = 0.1
+    qd = q64.float().to(dev)
+    order = spatial_order(qd) if ordered else None
+    L.set_option("fwd_alg", 3)
+    try:
+        v, mG, gdiv, h = L.ode_self_fwd(qd, p64.float().to(dev), sig, 0.0, True, want_h=True,
+                                        order=order)
+        qn, pn, gn = L.euler_step(qd, p64.float().to(dev), sig, 0.0, 0.1, True, order=order)
+    finally:
+        L.set_option("fwd_alg", FWD_ALG_DEFAULT)
+    assert torch.equal(gn, gdiv)       # same kernel, same order: bitwise
+    assert rel_err(qn, qd + 0.1 * v) < 1e-7
+    rows = torch.randperm(M, generator=g)[:256]
+    qf = q64.float().double()   # the positions the kernel sees
+    z = qf[rows][:, None, :] - qf[None, :, :]
+    K = torch.exp(-(z ** 2).sum(-1) / (2 * sig ** 2))
+    pf = p64.float().double()
+    V = K @ pf
+    pp = pf[rows] @ pf.t()
+    mG64 = (1 / sig ** 2) * ((K * pp)[:, :, None] * z).sum(1)        # -GenDKRed(q,q,p,p)
+    Z = -(1 / sig ** 2) * (K[:, :, None] * z).sum(1)
+    assert rel_err(v[rows].cpu(), V) < 1e-5, rel_err(v[rows].cpu(), V)
+    assert rel_err(mG[rows].cpu(), mG64) < 1e-5, rel_err(mG[rows].cpu(), mG64)
+    gd = (pf[rows] * Z).sum(1)
+    assert rel_err(gdiv[rows].cpu(), gd) < 1e-5, rel_err(gdiv[rows].cpu(), gd)
+
+
+def _mfma_wg_modes(q, sigma, order):
+    """Which workgroups of the matrix-core forward take the MFMA branch (mfma_fwd.hpp: rows'
+    spread about their mean <= kMfRmax = 4 in scaled units), replicated on the host."""
+    import math
+    a = math.sqrt(1.4426950408889634 / (2 * sigma * sigma))
+    qs = (q.double() * a)[order.long()] if order is not None else q.double() * a
+    modes = []
+    for i0 in range(0, qs.shape[0], 256):
+        blk = qs[i0:i0 + 256]
+        modes.append(bool(((blk - blk.mean(0)) ** 2).sum(1).max() <= 16.0))
+    return modes
+
+
+@pytest.mark.parametrize("M", [1, 15, 255, 257, 1000, 20000])
+@pytest.mark.parametrize("sigma", [0.1, 0.5])
+@pytest.mark.parametrize("ordered", [False, True])
+def test_mfma_fwd_modes_vs_ordered(dev, M, sigma, ordered):
+    """Matrix-core forward (fwd_alg 3) in both workgroup branches (MFMA channel sums for
+    compact rows, direct VALU sums for spread rows) == the ordered-row forward (alg 0) to the
+    SURVEY 8c criterion, every output incl. the fused Euler epilogue, row orders honoured
+    (outputs indexed by row), deterministic run to run."""
+    from difficp_amd.core.shooting import spatial_order
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 3)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    order = spatial_order(q) if ordered else None
+    modes = _mfma_wg_modes(q.cpu(), sigma, None if order is None else order.cpu())
+    if ordered and (M >= 20000 or (sigma == 0.5 and M >= 1000)):
+        assert any(modes)          # the case exercises the MFMA branch
+    L.set_option("fwd_alg", 0)
+    try:
+        ref = L.ode_self_fwd(q, p, sigma, 0.0, True, want_h=True)
+        L.set_option("fwd_alg", 3)
+        out = L.ode_self_fwd(q, p, sigma, 0.0, True, want_h=True, order=order)
+        out2 = L.ode_self_fwd(q, p, sigma, 0.0, True, want_h=True, order=order)
+        qn, pn, gn = L.euler_step(q, p, sigma, 0.0, 0.1, True, order=order)
+    finally:
+        L.set_option("fwd_alg", FWD_ALG_DEFAULT)
+    for k, (a, b) in enumerate(zip(out, ref)):
+        assert rel_err(a, b) < 1e-5, (k, rel_err(a, b), modes)
+    for a, b in zip(out, out2):
+        assert torch.equal(a, b)
+    assert torch.equal(gn, out[2])
+    assert rel_err(qn, q + 0.1 * out[0]) < 1e-7 and rel_err(pn, p + 0.1 * out[1]) < 1e-6
 
 
 @pytest.mark.parametrize("M", [1, 128, 129, 1000, 5000, 50000])

@@ -268,3 +268,30 @@ def test_chui_fp32_oracle_deviation(fake):
             worst["x1"] = max(worst["x1"], rel_err(PS.x1[0, 0], torch.from_numpy(z[f"it{it}/x1"])))
     chui_case.run_chui({"device": "cpu", "dtype": torch.float32}, iters=4, check=check)
     assert worst["fe"] < 1.1e-3 and worst["sigma"] < 1.5e-3 and worst["x1"] < 2.25e-3, worst
+
+
+def test_spatial_order_permutation_and_locality():
+    """shooting.spatial_order (the row visit order the matrix-core forward gets from
+    LDDMMModel.Shoot): an int32 permutation, deterministic, and spatially local (consecutive
+    rows much closer than in the input order), in 2D and 3D; degenerate extents are safe."""
+    import torch
+    from difficp_amd.core.shooting import RowOrderCache, spatial_order
+    g = torch.Generator().manual_seed(3)
+    for D in (2, 3):
+        x = torch.rand(4000, D, generator=g)
+        o = spatial_order(x)
+        assert o.dtype == torch.int32 and sorted(o.tolist()) == list(range(4000))
+        assert torch.equal(o, spatial_order(x.clone()))
+        xs = x[o.long()]
+        step = (xs[1:] - xs[:-1]).norm(dim=1).mean()
+        assert step < 0.3 * (x[1:] - x[:-1]).norm(dim=1).mean()
+    flat = torch.zeros(50, 3)             # zero extent: any permutation, no NaN
+    assert sorted(spatial_order(flat).tolist()) == list(range(50))
+    c = RowOrderCache(maxsize=2)
+    x = torch.rand(300, 3, generator=g)
+    a = c.get(x)
+    assert c.get(x) is a                    # memoised per tensor
+    b = c.get(x, 100, 50)                   # slice order: indices into the slice
+    assert sorted(b.tolist()) == list(range(50))
+    x.add_(1.0)                             # in-place change -> new version -> recomputed
+    assert c.get(x) is not a
