@@ -207,11 +207,20 @@ def _main(out):
             import torch.distributed as dist
             dist.barrier()
 
+    # row split: the warmup iterations check after every VJP all-reduce that all ranks hold
+    # the same bits (RowSplit.verify; the replicated L-BFGS must take identical decisions) --
+    # a mismatch raises on every rank at once instead of letting the ranks diverge
+    rs = getattr(getattr(psr, "LMi", None), "row_split", None)
+    if rs is not None:
+        rs.verify = True
     for i in range(args.warmup):
         t0 = time.perf_counter()
         workloads.psr_iteration(psr)
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t0:.2f}s FE={psr.FE:.6g}")
+    if rs is not None:
+        log(f"[rank {rank}] row split: {rs.verified_calls} all-reduces verified bitwise identical across ranks")
+        rs.verify = False
 
     # frames optimised concurrently (atlas, one HIP stream per frame thread): kernels of
     # different frames overlap, so per-launch event times are not kernel durations -- the

@@ -1,8 +1,9 @@
-"""Parity at BASELINE full size (C2: 50k 3D points, sigma_LDDMM = 0.1, sigma_GMM = 0.05).
+"""Parity at BASELINE full sizes (C2: 50k, the metric's 100k and C3: 200k 3D points,
+sigma_LDDMM = 0.1, sigma_GMM = 0.05).
 
 A full fp64 oracle at 50k x 50k is 2.5e9 pairs per operator -- too slow for a test -- so the
 checks here are
-  * row-subset parity: 192 random rows of each output, each a reduction over ALL 50k
+  * row-subset parity: 192 random rows of each output, each a reduction over ALL the
     columns, against float64 torch formulas of the reference operators (the formulas are
     themselves checked against the oracle at small size, in the CPU test at the bottom);
   * size-independent properties: bitwise run-to-run determinism, invariance to the number of
@@ -87,9 +88,9 @@ def test_subset_formulas_match_oracle():
     assert rel_err(gqs, gq[sub]) < 1e-12 and rel_err(gps, gp[sub]) < 1e-12
 
 
-@pytest.fixture(scope="module")
-def full(dev):
-    q, p, a, b, sub = _points(M_FULL, 2024)
+@pytest.fixture(scope="module", params=[M_FULL, 100000, 200000], ids=["50k", "100k", "200k"])
+def full(dev, request):
+    q, p, a, b, sub = _points(request.param, 2024)
     f = lambda t: t.float().to(dev)
     return dict(q=q, p=p, a=a, b=b, sub=sub, qd=f(q), pd=f(p), ad=f(a), bd=f(b))
 
@@ -123,7 +124,7 @@ def test_bwd_fullsize_subset(full):
 def test_ext_fwd_fullsize_subset(full, dev):
     from difficp_amd import _lib
     g = torch.Generator().manual_seed(77)
-    x = torch.rand(M_FULL, 3, generator=g, dtype=torch.float64)
+    x = torch.rand(full["q"].shape[0], 3, generator=g, dtype=torch.float64)
     vx, gx = _lib.ode_ext_fwd(x.float().to(dev), full["qd"], full["pd"], SIG_L, 0.0, True)
     sub = full["sub"]
     v64 = R.KRed(x[sub], full["q"], full["p"], SIG_L)
