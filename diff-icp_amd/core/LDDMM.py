@@ -18,7 +18,7 @@ from ..tools.integrators import EulerIntegrator, RalstonIntegrator
 from ..tools.kernel import GaussKernel, SVDpow
 from ..tools.optim import LBFGS_optimization
 from ..tools.spec import defspec, getspec
-from .shooting import HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootFn
+from .shooting import HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootCache, ShootFn
 
 
 class Shoot(list):
@@ -70,6 +70,9 @@ class LDDMMModel:
         # only the matrix-core forward (library option fwd_alg 3) uses it: set
         # `row_orders = RowOrderCache()` together with that option
         self.row_orders = None
+        # the latest trajectory per q0, reused bitwise when the same shooting is asked for
+        # again (shooting.ShootCache: the first closure of each Reg_opt L-BFGS run)
+        self.shoot_cache = ShootCache()
 
     def set_row_split(self, group=None, enable=True, exact_reduce=None, verify=None):
         """Split every dense Euler shooting of this model over the ranks of a torch.distributed
@@ -95,6 +98,7 @@ class LDDMMModel:
         self.__dict__.update(state)
         if self.__dict__.get("row_orders") is not None:
             self.row_orders = RowOrderCache()
+        self.shoot_cache = ShootCache()
         self.Kernel = GaussKernel(self.Kernel.sigma, self.Kernel.D, self.Kernel.computversion,
                                   spec=defspec)
 
@@ -197,7 +201,8 @@ class LDDMMModel:
         outs = ShootFn.apply(q0.contiguous(), p0.contiguous(),
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
                              float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet),
-                             self.row_split, getattr(self, "row_orders", None))
+                             self.row_split, getattr(self, "row_orders", None),
+                             getattr(self, "shoot_cache", None))
         if x0 is None:
             Q, P, C, H0 = outs
             return Shoot(Q, P, C, None, H0)

@@ -87,6 +87,66 @@ class RowOrderCache:
 _ORDER_MIN_ROWS = 256
 
 
+class ShootCache:
+    """The most recent forward trajectory per support-point tensor q0, to be reused when the
+    same shooting (q0, p0[, x0] and the same model parameters) is asked for again.
+
+    Why: DiffPSR.Reg_opt starts every L-BFGS run at the momenta the previous run returned
+    (PSR.py:521-569 passes a0[k]); its first closure shoots exactly the trajectory the
+    previous run's final shoot computed -- only the data loss changed (new GMM targets), and
+    the trajectory does not depend on it.  The kernels are deterministic (no atomics, fixed
+    summation order), so a hit returns bitwise the tensors a recomputation would produce;
+    the backward runs the adjoint on them as usual.  One entry per q0 (key: storage pointer,
+    version counter, shape); the inputs are compared bitwise (torch.equal) before reuse."""
+
+    def __init__(self):
+        self._d = {}
+        self._lock = threading.Lock()
+        self.hits = 0
+
+    def __getstate__(self):
+        return {}
+
+    def __setstate__(self, state):
+        self.__init__()
+
+    def __deepcopy__(self, memo):
+        return ShootCache()
+
+    @staticmethod
+    def _key(q0):
+        return (q0.data_ptr(), q0._version, tuple(q0.shape), str(q0.device))
+
+    def lookup(self, q0, p0, x0, params):
+        with self._lock:
+            e = self._d.get(self._key(q0))
+        if e is None or e["params"] != params:
+            return None
+        if not torch.equal(e["p0"], p0):
+            return None
+        if (e["x0"] is None) != (x0 is None) or (x0 is not None and not torch.equal(e["x0"], x0)):
+            return None
+        self.hits += 1
+        # the cached tensors may have been produced on another stream (concurrent frames: a
+        # new stream per Reg_opt call); keep their memory from being reused while this stream
+        # still reads them
+        if p0.is_cuda:
+            st = torch.cuda.current_stream(p0.device)
+            for t in list(e["saved"]) + [t for t in e["outs"] if isinstance(t, torch.Tensor)]:
+                t.record_stream(st)
+        return e
+
+    def store(self, q0, p0, x0, params, outs, saved):
+        e = {"p0": p0.detach().clone(), "x0": None if x0 is None else x0.detach().clone(),
+             "params": params, "outs": outs, "saved": saved}
+        with self._lock:
+            self._d[self._key(q0)] = e
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+
+
 def _f_self(q, p, sigma, eta, want_div, want_h=False, order=None):
     """ODE right-hand side at the support points: (v, mG, div[1]) [+ per-row h]."""
     v, mG, g, h = _lib.ode_self_fwd(q, p, sigma, eta, want_div, want_h=want_h, order=order)
@@ -124,11 +184,24 @@ class ShootFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None, orders=None):
+    def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None, orders=None,
+                cache=None):
         """orders: optional RowOrderCache; the forward passes then visit the support rows in
-        the spatial order of q0 (kept for every step: the flow moves neighbours together)."""
+        the spatial order of q0 (kept for every step: the flow moves neighbours together).
+        cache: optional ShootCache (bitwise reuse of a repeated shooting, see there)."""
         ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
+        params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
+                  None if split is None else (split.rank, split.world))
+        hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
+        if hit is not None:
+            ctx.split = split if (split is not None and not has_x and scheme == "Euler"
+                                  and split.world > 1) else None
+            ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x = \
+                sigma, eta, nt, scheme, want_div, has_x
+            ctx.save_for_backward(*hit["saved"])
+            # fresh output tensors (autograd owns them); the saved ones are only read
+            return tuple(t.clone() for t in hit["outs"])
         # row-split over ranks (core/rowsplit.py): dense Euler shooting only; other schemes
         # run replicated on every rank
         if split is not None and (has_x or scheme != "Euler" or split.world == 1):
@@ -248,6 +321,11 @@ class ShootFn(torch.autograd.Function):
             saved += [qi, pi] + ([xi] if has_x else [])
         ctx.save_for_backward(*saved)
         outs = (Q, P, C, X, H0) if has_x else (Q, P, C, H0)
+        if cache is not None:
+            H0d = H0 if isinstance(H0, torch.Tensor) else torch.as_tensor(H0)
+            cache.store(q0, p0, x0, params, tuple(t.detach() if isinstance(t, torch.Tensor) else t
+                                                  for t in ((Q, P, C, X, H0d) if has_x else (Q, P, C, H0d))),
+                        [t.detach() for t in saved])
         return outs
 
     @staticmethod
@@ -345,7 +423,7 @@ class ShootFn(torch.autograd.Function):
         if gH is not None:
             lq = lq - gH * mG0
             lp = lp + gH * v0
-        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None
+        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None
 
 
 class HamiltonianFn(torch.autograd.Function):

@@ -15,7 +15,10 @@ using namespace dicp;
 
 namespace {
 
-constexpr int kR = 2;       // rows per thread for the light reductions
+#ifndef DICP_KR
+#define DICP_KR 2
+#endif
+constexpr int kR = DICP_KR;  // rows per thread for the light reductions (KRed etc.)
 
 // Rows per thread of the fused ODE passes (tuning knobs, env DICP_R_FWD / DICP_R_BWD in
 // {1, 2, 4}; read once).  Defaults chosen from measurements on MI355X.

@@ -295,3 +295,24 @@ def test_spatial_order_permutation_and_locality():
     assert sorted(b.tolist()) == list(range(50))
     x.add_(1.0)                             # in-place change -> new version -> recomputed
     assert c.get(x) is not a
+
+
+@pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
+def test_shoot_cache_reuse_is_bitwise(fake, scheme):
+    """shooting.ShootCache: Reg_opt's first closure re-shoots the trajectory the previous
+    Reg_opt ended on; reusing it must give bitwise the results of recomputing (PSR FE and a0
+    after two diff-ICP iterations), with at least one reuse per frame and iteration."""
+    from difficp_amd import workloads
+    res = []
+    for use_cache in (True, False):
+        psr = workloads.build_two_set(120, torch.device("cpu"), seed=4, nt=5)
+        psr.LMi.set_integration_scheme(scheme)
+        if not use_cache:
+            psr.LMi.shoot_cache = None
+        for _ in range(2):
+            workloads.psr_iteration(psr, max_repeat_GMM=3, tol=1e-6)
+        res.append((psr.FE, psr.a0[0].clone(), psr.x1[0, 0].clone(),
+                    None if psr.LMi.shoot_cache is None else psr.LMi.shoot_cache.hits))
+    (fe1, a1, x1, hits), (fe0, a0, x0, _) = res
+    assert hits >= 1
+    assert fe1 == fe0 and torch.equal(a1, a0) and torch.equal(x1, x0)
