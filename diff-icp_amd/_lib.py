@@ -171,6 +171,9 @@ FLOPS_PER_PAIR = {
 # symmetric pair-once VJP evaluates each unordered pair once.  bench.py reports the fraction
 # of the peak on both counts (roofline.frac = algorithmic, roofline.frac_executed).
 EXEC_FLOPS_PER_PAIR = {"ode_self_bwd": 53}
+# the gp-only VJP (last adjoint step when q0 needs no gradient): 32 of the 60 packed
+# instructions of the full symmetric loop -> priced at that share of the full VJP's figure
+FLOPS_PER_PAIR["ode_self_bwd_gp"] = round(70 * 32 / 60)
 
 
 class KernelProfile:
@@ -327,9 +330,11 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
     return qn, pn, g
 
 
-def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, addq=None, addp=None):
+def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, addq=None, addp=None,
+                       want_lq: bool = True):
     """(lq + dt gq + addq, lp + dt gp + addp) with (gq, gp) the ODE VJP for cotangents
-    (lq, lp, gdiv) -- one fused pass (dicp_lddmm_euler_adjoint_step_f32)."""
+    (lq, lp, gdiv) -- one fused pass (dicp_lddmm_euler_adjoint_step_f32).  want_lq=False:
+    (None, lp_next) only -- the gq half of the pair algebra is skipped (eta = 0)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     lq = _dev(lq, "lq")
@@ -338,12 +343,13 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
     addq = None if addq is None else _dev(addq, "addq")
     addp = None if addp is None else _dev(addp, "addp")
     M, D = q.shape
-    lqn = torch.empty_like(q)
+    lqn = torch.empty_like(q) if want_lq else None
     lpn = torch.empty_like(q)
     if M == 0:
         return lqn, lpn
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
-    rc = _launch(("ode_self_bwd_eta" if eta else "ode_self_bwd"), M * M, 4 * M * 8 * D,
+    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if want_lq else "ode_self_bwd_gp")
+    rc = _launch(name, M * M, 4 * M * (8 * D if want_lq else 7 * D),
                  lambda: lib().dicp_lddmm_euler_adjoint_step_f32(
                      _ptr(q), _ptr(p), _ptr(lq), _ptr(lp), _ptr(gdiv), M, D, float(sigma), float(eta),
                      float(dt), _ptr(addq), _ptr(addp), _ptr(lqn), _ptr(lpn), _ptr(ws), nb,
@@ -585,22 +591,24 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
     return qn, pn, g
 
 
-def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, nparts: int):
+def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, nparts: int,
+                      want_gq: bool = True):
     """Part `part` of `nparts` of ode_self_bwd (dicp_lddmm_ode_self_bwd_part_f32): (gq, gp)
-    over a pair subset; the sum over the parts is the full VJP."""
+    over a pair subset; the sum over the parts is the full VJP.  want_gq=False: (None, gp)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     gv = _dev(gv, "gv")
     gmG = _dev(gmG, "gmG")
     gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
     M, D = q.shape
-    gq = torch.empty_like(q)
+    gq = torch.empty_like(q) if want_gq else None
     gp = torch.empty_like(q)
     if M == 0:
         return gq, gp
     ws, nb = _workspace(WS_ODE_SELF_BWD_PART, M, nparts, D, q.device)
     pairs = (M * M) // nparts
-    rc = _launch(("ode_self_bwd_eta" if eta else "ode_self_bwd"), pairs, 4 * M * 6 * D,
+    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if want_gq else "ode_self_bwd_gp")
+    rc = _launch(name, pairs, 4 * M * 6 * D,
                  lambda: lib().dicp_lddmm_ode_self_bwd_part_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv),
                                                                 M, D, float(sigma), float(eta), int(part),
                                                                 int(nparts), _ptr(gq), _ptr(gp), _ptr(ws), nb,

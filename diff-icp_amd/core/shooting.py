@@ -363,13 +363,19 @@ class ShootFn(torch.autograd.Function):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
             if split is not None:
-                # this rank's part of the pair-once VJP, summed over ranks (one all-reduce)
+                # this rank's part of the pair-once VJP, summed over ranks (one all-reduce);
+                # the last step needs gp only when q0 needs no gradient (half the bytes too)
+                want_lq = t > 0 or ctx.needs_input_grad[0]
                 gq_l, gp_l = _lib.ode_self_bwd_part(q, p, lq, lp, lc if want_div else None, sigma,
-                                                    eta, split.rank, split.world)
-                g = split.all_reduce_(torch.cat([gq_l, gp_l], 1))
-                lq = torch.add(lq, g[:, :D], alpha=dt)
-                lp = torch.add(lp, g[:, D:], alpha=dt)
-                if gQ is not None:
+                                                    eta, split.rank, split.world, want_gq=want_lq)
+                if want_lq:
+                    g = split.all_reduce_(torch.cat([gq_l, gp_l], 1))
+                    lq = torch.add(lq, g[:, :D], alpha=dt)
+                    lp = torch.add(lp, g[:, D:], alpha=dt)
+                else:
+                    lp = torch.add(lp, split.all_reduce_(gp_l), alpha=dt)
+                    lq = None
+                if gQ is not None and lq is not None:
                     lq = lq + gQ[t]
                 if gP is not None:
                     lp = lp + gP[t]
@@ -382,9 +388,12 @@ class ShootFn(torch.autograd.Function):
                 if gC is not None and lc_suffix is None:
                     lc_suffix = torch.flip(torch.cumsum(torch.flip(gC, (0,)), 0), (0,))
                 lct = lc if gC is None else lc_suffix[t + 1]
+                # last step: the cotangent of q0 is only needed if q0 requires a gradient (the
+                # support points of Reg_opt do not) -- then the gq half is skipped
+                want_lq = t > 0 or ctx.needs_input_grad[0]
                 lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lct if want_div else None, sigma, eta,
                                                  dt, None if gQ is None else gQ[t],
-                                                 None if gP is None else gP[t])
+                                                 None if gP is None else gP[t], want_lq=want_lq)
                 if gC is not None:
                     lc = lc_suffix[t]
                 continue
@@ -421,8 +430,11 @@ class ShootFn(torch.autograd.Function):
             if has_x and gX is not None:
                 lx = lx + gX[t]
         if gH is not None:
-            lq = lq - gH * mG0
+            if lq is not None:
+                lq = lq - gH * mG0
             lp = lp + gH * v0
+        if not ctx.needs_input_grad[0]:
+            lq = None
         return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None
 
 

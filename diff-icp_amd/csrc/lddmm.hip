@@ -330,7 +330,7 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
   const int64_t per = (M + nparts - 1) / nparts;
   const int64_t r0 = per * part < M ? per * part : M;
   const int64_t r1 = r0 + per < M ? r0 + per : M;
-  if (hipMemsetAsync(gq, 0, (size_t)M * D * sizeof(float), st) != hipSuccess ||
+  if ((gq && hipMemsetAsync(gq, 0, (size_t)M * D * sizeof(float), st) != hipSuccess) ||
       hipMemsetAsync(gp, 0, (size_t)M * D * sizeof(float), st) != hipSuccess) {
     set_error("ode_self_bwd_part: hipMemsetAsync failed");
     return DICP_ERR_HIP;
@@ -338,7 +338,7 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
   if (r1 <= r0) return DICP_OK;
   const int64_t o0 = r0 * D;
   Args a = {q + o0, p + o0, gv + o0, gmG + o0, q, p, gv, gmG, 0.f};
-  const Outs o = make_outs(gq + o0, gp + o0);
+  const Outs o = make_outs(gq ? gq + o0 : nullptr, gp + o0);
   if (eta != 0.0) {
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
@@ -448,7 +448,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const
                                            float* gp, void* ws, size_t ws_bytes,
                                            dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (M < 0 || (M > 0 && (!q || !p || !gv || !gmG || !gq || !gp)) || !(sigma > 0)) {
+  if (M < 0 || (M > 0 && (!q || !p || !gv || !gmG || !gp)) || !(sigma > 0)) {
     set_error("dicp_lddmm_ode_self_bwd_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }
@@ -496,9 +496,10 @@ extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const float* ins[4] = {q, p, lq, lp};
   bool alias = false;
-  for (const float* x : ins) alias = alias || x == lq_next || x == lp_next;
-  if (M < 0 || (M > 0 && (!q || !p || !lq || !lp || !lq_next || !lp_next || alias)) ||
-      !(sigma > 0)) {
+  for (const float* x : ins) alias = alias || (lq_next && x == lq_next) || x == lp_next;
+  // lq_next may be NULL: only lp_next is produced (the gq half of the eta = 0 symmetric VJP is
+  // then never evaluated -- the last adjoint step when the start points need no gradient)
+  if (M < 0 || (M > 0 && (!q || !p || !lq || !lp || !lp_next || alias)) || !(sigma > 0)) {
     set_error("dicp_lddmm_euler_adjoint_step_f32: invalid arguments (outputs must not alias inputs)");
     return DICP_ERR_INVALID;
   }
@@ -645,7 +646,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, 
                                                 size_t ws_bytes, dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || nparts < 1 || part < 0 || part >= nparts ||
-      (M > 0 && (!q || !p || !gv || !gmG || !gq || !gp)) || !(sigma > 0)) {
+      (M > 0 && (!q || !p || !gv || !gmG || !gp)) || !(sigma > 0)) {  // gq may be NULL (gp only)
     set_error("dicp_lddmm_ode_self_bwd_part_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }

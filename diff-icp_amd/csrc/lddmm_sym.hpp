@@ -680,12 +680,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxW
 // Pair-subset mode (row-split over ranks): only the quads Q = qoff (mod qstride) ran, so a
 // row of quad Q_T sums its column slots Q <= Q_T of those quads and, if Q_T is one of them,
 // its row slots; (qoff, qstride) = (0, 1) is every slot in slot order.
-template <int D, bool kPart>
+// W = 2D: [gp, gq] channels; W = D: gp only (the gp-only VJP, sym_bwd_pk_kernel<D, false>).
+// Null output pointers are skipped (a caller that needs only gp).
+template <int D, bool kPart, int W = 2 * D>
 __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
                                                         int64_t slot_stride, int64_t M, int nG,
                                                         int L, float s, float alpha, Outs o,
                                                         int qoff, int qstride) {
-  constexpr int W = 2 * D;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= M * W) return;
   const int64_t row = e / W;
@@ -724,10 +725,10 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
   }
   if (c < D) {
     const int64_t idx = row * D + c;
-    o.ptr[1][idx] = epilogue(o, 1, idx, alpha * acc);
+    if (o.ptr[1]) o.ptr[1][idx] = epilogue(o, 1, idx, alpha * acc);
   } else {
     const int64_t idx = row * D + (c - D);
-    o.ptr[0][idx] = epilogue(o, 0, idx, s * acc);
+    if (o.ptr[0]) o.ptr[0][idx] = epilogue(o, 0, idx, s * acc);
   }
 }
 
@@ -826,8 +827,8 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
     set_error("ode_self_bwd(sym eta): workspace too small (%zu < %zu bytes)", wsb, need);
     return DICP_ERR_WORKSPACE;
   }
-  if (o.ptr[0] == nullptr || o.ptr[1] == nullptr) {
-    set_error("ode_self_bwd(sym eta): both outputs are required");
+  if (o.ptr[1] == nullptr) {
+    set_error("ode_self_bwd(sym eta): the gp output is required");
     return DICP_ERR_INVALID;
   }
   float* slab = reinterpret_cast<float*>(ws);
@@ -853,8 +854,8 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
   return check_launch("ode_self_bwd(sym eta merge)");
 }
 
-// packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp)
-template <int D>
+// packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp); GQ = false: gp half only
+template <int D, bool GQ>
 __global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                   int64_t slot_stride, int qoff, int qstride);
 
@@ -868,16 +869,35 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     set_error("ode_self_bwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
     return DICP_ERR_WORKSPACE;
   }
-  if (o.ptr[0] == nullptr || o.ptr[1] == nullptr) {
-    set_error("ode_self_bwd(sym): both outputs are required");
+  if (o.ptr[1] == nullptr) {
+    set_error("ode_self_bwd(sym): the gp output is required");
     return DICP_ERR_INVALID;
   }
   float* slab = reinterpret_cast<float*>(ws);
+  if (pk && o.ptr[0] == nullptr) {
+    // gp only: the gq half of the pair algebra is never evaluated (also per pair-subset part)
+    const int64_t stride1 = M * D;
+    const int nq1 = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
+    if (nq1 > 0) {
+      sym_bwd_pk_kernel<D, false><<<dim3((unsigned)g.Kmax, (unsigned)nq1), dim3(256), 0, st>>>(
+          a, sc, M, g.nG, g.L, slab, stride1, part, nparts);
+      int rc = check_launch("ode_self_bwd(sym gp)");
+      if (rc) return rc;
+    }
+    const dim3 mg((unsigned)((M * D + 255) / 256));
+    if (nparts > 1)
+      sym_merge_kernel<D, true, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
+                                                             part, nparts);
+    else
+      sym_merge_kernel<D, false, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
+                                                              0, 1);
+    return check_launch("ode_self_bwd(sym gp merge)");
+  }
   const int64_t stride = M * 2 * D;
   const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
   if (nq_own > 0) {
     if (pk)
-      sym_bwd_pk_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+      sym_bwd_pk_kernel<D, true><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
           a, sc, M, g.nG, g.L, slab, stride, part, nparts);
     else
       sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(

@@ -10,9 +10,14 @@
 
 namespace dicp {
 
-template <int D>
+// GQ = false: the gp half only (dL/dp of the VJP), for the last adjoint step of a shooting
+// whose start points need no gradient (the support points in Reg_opt): the pair scalars
+// pp, u, zu, iap, w and every gq accumulation drop out -- 32 of the 60 packed instructions
+// per step remain.
+template <int D, bool GQ = true>
 struct SymBwdPk {
   using S = SymBwd<D>;
+  static constexpr int W = GQ ? 2 * D : D;
   static constexpr int kMaxWaves = 4;
   struct Prm {
     float gt, c;  // gam s1 / alpha, s1 / alpha (SymBwd::Prm)
@@ -50,25 +55,32 @@ struct SymBwdPk {
       r2 = pk_fma(t.z[d], t.z[d], r2);
     }
     t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
-    f2 pp = r.p[0] * splat(pj[0]);
+    if constexpr (GQ) {
+      f2 pp = r.p[0] * splat(pj[0]);
 #pragma unroll
-    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
-    f2 db[D];
+      for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+      f2 db[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      db[d] = r.b[d] - splat(bj[d]);
-      t.u[d] = pk_fma(-pp, db[d], r.gp[d] - splat(gpj[d]));
+      for (int d = 0; d < D; ++d) {
+        db[d] = r.b[d] - splat(bj[d]);
+        t.u[d] = pk_fma(-pp, db[d], r.gp[d] - splat(gpj[d]));
+      }
+      f2 zu = t.z[0] * t.u[0], zb = t.z[0] * db[0];
+      f2 iap = pk_fma(r.ia_a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+#pragma unroll
+      for (int d = 1; d < D; ++d) {
+        zu = pk_fma(t.z[d], t.u[d], zu);
+        zb = pk_fma(t.z[d], db[d], zb);
+        iap = pk_fma(r.ia_a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), iap));
+      }
+      t.w = pk_fma(splat(kS2), zu, -iap);
+      t.cKzb = (splat(c) * zb) * t.K;
+    } else {
+      f2 zb = t.z[0] * (r.b[0] - splat(bj[0]));
+#pragma unroll
+      for (int d = 1; d < D; ++d) zb = pk_fma(t.z[d], r.b[d] - splat(bj[d]), zb);
+      t.cKzb = (splat(c) * zb) * t.K;
     }
-    f2 zu = t.z[0] * t.u[0], zb = t.z[0] * db[0];
-    f2 iap = pk_fma(r.ia_a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
-#pragma unroll
-    for (int d = 1; d < D; ++d) {
-      zu = pk_fma(t.z[d], t.u[d], zu);
-      zb = pk_fma(t.z[d], db[d], zb);
-      iap = pk_fma(r.ia_a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), iap));
-    }
-    t.w = pk_fma(splat(kS2), zu, -iap);
-    t.cKzb = (splat(c) * zb) * t.K;
   }
   // ordered pairs (i, j) of both rows, row side only (diag blocks)
   __device__ static void pair_row(const Prm& prm, const Row2& r, const float* rec, f2* acc) {
@@ -80,7 +92,7 @@ struct SymBwdPk {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
-      acc[D + d] = pk_fma(t.K, pk_fma(t.w, t.z[d], -t.u[d]), acc[D + d]);
+      if constexpr (GQ) acc[D + d] = pk_fma(t.K, pk_fma(t.w, t.z[d], -t.u[d]), acc[D + d]);
     }
   }
   // unordered pairs {i, j} of both rows: row side into acc, the column's total (both rows)
@@ -93,14 +105,16 @@ struct SymBwdPk {
     const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const f2 e = pk_fma(t.w, t.z[d], -t.u[d]);
-      const f2 Ke = t.K * e;
       acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
-      acc[D + d] = acc[D + d] + Ke;
       const f2 tt = pk_fma(splat(gt), t.z[d], r.ia_a[d]);
       const f2 cg = pk_fma(t.cKzb, r.p[d], t.K * tt);
       ct[d] = cg.x + cg.y;
-      ct[D + d] = -(Ke.x + Ke.y);
+      if constexpr (GQ) {
+        const f2 e = pk_fma(t.w, t.z[d], -t.u[d]);
+        const f2 Ke = t.K * e;
+        acc[D + d] = acc[D + d] + Ke;
+        ct[D + d] = -(Ke.x + Ke.y);
+      }
     }
   }
 };
@@ -122,7 +136,7 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
                                             float* __restrict__ slab, int64_t slot_stride, int qoff,
                                             int qstride) {
   using S = typename P::S;
-  constexpr int CW = S::CW, W = S::W;
+  constexpr int CW = S::CW, W = P::W;
   __shared__ float4 planes[2][CW][kSymG];
   __shared__ float colacc[kSymQ][kSymG][W];
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
@@ -269,11 +283,11 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
   }
 }
 
-template <int D>
+template <int D, bool GQ>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
-  sym_pk_body<SymBwdPk<D>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdPk<D, GQ>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 // Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /
@@ -283,6 +297,7 @@ template <int D>
 struct SymBwdEtaPk {
   using S = SymBwdEta<D>;
   using Prm = typename S::Prm;
+  static constexpr int W = S::W;
   __device__ static Prm params(const Args& a, const Scal& sc) { return S::params(a, sc); }
   struct Row2 {
     f2 q[D], p[D], a[D], b[D];

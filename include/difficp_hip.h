@@ -100,7 +100,9 @@ int dicp_lddmm_ode_self_fwd_f32(const float* q, const float* p, int64_t M, int D
 
 /* Vector-Jacobian product of the fused self ODE (what KeOps autodiff provides at
  * optim.py:46).  Cotangents: gv (M,D) on v, gmG (M,D) on mG, and gdiv = cotangent of
- * sum_i g_i, a DEVICE scalar (may be NULL = 0).  Outputs gq, gp (M,D), overwritten. */
+ * sum_i g_i, a DEVICE scalar (may be NULL = 0).  Outputs gq, gp (M,D), overwritten; gq may be
+ * NULL (gp only: for eta = 0 with the default symmetric kernel the gq half of the pair
+ * algebra -- about half of it -- is then skipped). */
 int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const float* gv,
                                 const float* gmG, const float* gdiv, int64_t M, int D,
                                 double sigma, double eta, float* gq, float* gp, void* ws,
@@ -117,6 +119,8 @@ int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t M, int D, 
 /* Its exact discrete adjoint (the reverse sweep of optim.py:46's backward through the Euler
  * loop): with (gq, gp) the VJP of dicp_lddmm_ode_self_bwd_f32 for cotangents (lq, lp, gdiv),
  *   lq_next = lq + dt gq + addq,  lp_next = lp + dt gp + addp   (addq/addp (M,D) or NULL).
+ * lq_next may be NULL (the last step of a sweep whose start points q0 need no gradient:
+ * only lp_next, with the gq half skipped as above).
  * Outputs must not alias inputs.  Workspace kind DICP_WS_ODE_SELF_BWD. */
 int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
                                       const float* lp, const float* gdiv, int64_t M, int D,

@@ -110,14 +110,14 @@ def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=Non
     return qn, pn, g
 
 
-def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None):
+def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None, want_lq=True):
     gq, gp = ode_self_bwd(q, p, lq, lp, gdiv, sigma, eta)
     lqn, lpn = lq + dt * gq, lp + dt * gp
     if addq is not None:
         lqn = lqn + addq
     if addp is not None:
         lpn = lpn + addp
-    return lqn, lpn
+    return (lqn if want_lq else None), lpn
 
 
 def _ext_terms(x, q, p, sigma, eta):
@@ -213,7 +213,7 @@ def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_o
     return q[sl] + dt * v, p[sl] + dt * mG, g
 
 
-def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts):
+def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True):
     """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
     its rows, zeros elsewhere; the sum over parts is the VJP."""
     gq, gp = ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta)
@@ -222,7 +222,7 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts):
     r0, r1 = min(per * part, M), min(per * part + per, M)
     mask = torch.zeros(M, 1, dtype=gq.dtype)
     mask[r0:r1] = 1
-    return gq * mask, gp * mask
+    return (gq * mask if want_gq else None), gp * mask
 
 
 _ENTRIES = ("ode_self_fwd_rows", "euler_step_rows", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",

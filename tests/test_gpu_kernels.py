@@ -195,6 +195,27 @@ def test_fused_euler_steps(dev, M, eta):
         assert rel_err(lqn, ref_q) < 1e-6 and rel_err(lpn, lp + dt * gp) < 1e-6
 
 
+@pytest.mark.parametrize("M", [1, 129, 5000, 50000])
+@pytest.mark.parametrize("eta", [0.0, 0.02])
+def test_adjoint_step_gp_only(dev, M, eta):
+    """euler_adjoint_step(want_lq=False) (lq_next = NULL at the C-ABI: the gq half of the
+    symmetric eta = 0 VJP is skipped) gives the lp_next of the full step."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 9)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    lq = torch.randn(M, 3, generator=g).to(dev)
+    lp = torch.randn(M, 3, generator=g).to(dev)
+    ap = torch.randn(M, 3, generator=g).to(dev)
+    gd = torch.full((1,), 0.3, device=dev)
+    lqn, lpn = L.euler_adjoint_step(q, p, lq, lp, gd, 0.1, eta, 0.1, None, ap)
+    none, lpn1 = L.euler_adjoint_step(q, p, lq, lp, gd, 0.1, eta, 0.1, None, ap, want_lq=False)
+    assert none is None
+    assert rel_err(lpn1, lpn) < 1e-6, rel_err(lpn1, lpn)
+    none, lpn2 = L.euler_adjoint_step(q, p, lq, lp, gd, 0.1, eta, 0.1, None, ap, want_lq=False)
+    assert torch.equal(lpn1, lpn2)      # deterministic
+
+
 def test_dpp_wave_rol_semantics(dev):
     """The symmetric VJP rotates column sums with DPP wave_rol:1 assuming lane l reads lane
     l + 1 (lddmm_sym.hpp rol1); pin that on the hardware."""

@@ -64,13 +64,17 @@ def test_bwd_parts_sum(dev, M, W, eta):
     q, p, a, b = _state(M, 7 * M + W, dev)
     gd = torch.full((1,), 0.3, device=dev)
     gq, gp = L.ode_self_bwd(q, p, a, b, gd, 0.1, eta)
-    sq, sp = torch.zeros_like(gq), torch.zeros_like(gp)
+    sq, sp, sp1 = torch.zeros_like(gq), torch.zeros_like(gp), torch.zeros_like(gp)
     for r in range(W):
         pq, pp = L.ode_self_bwd_part(q, p, a, b, gd, 0.1, eta, r, W)
         sq += pq
         sp += pp
+        none, pp1 = L.ode_self_bwd_part(q, p, a, b, gd, 0.1, eta, r, W, want_gq=False)   # gp only
+        assert none is None
+        sp1 += pp1
     assert rel_err(sq, gq) < 2e-6, rel_err(sq, gq)
     assert rel_err(sp, gp) < 2e-6, rel_err(sp, gp)
+    assert rel_err(sp1, gp) < 2e-6, rel_err(sp1, gp)
     one = L.ode_self_bwd_part(q, p, a, b, gd, 0.1, eta, 0, 1)   # one part = the full VJP
     assert torch.equal(one[0], gq) and torch.equal(one[1], gp)
 
