@@ -174,6 +174,8 @@ EXEC_FLOPS_PER_PAIR = {"ode_self_bwd": 53}
 # the gp-only VJP (last adjoint step when q0 needs no gradient): 32 of the 60 packed
 # instructions of the full symmetric loop -> priced at that share of the full VJP's figure
 FLOPS_PER_PAIR["ode_self_bwd_gp"] = round(70 * 32 / 60)
+# zero momentum cotangent (first adjoint step): 40 of 60 packed instructions remain
+FLOPS_PER_PAIR["ode_self_bwd_b0"] = round(70 * 40 / 60)
 
 
 class KernelProfile:
@@ -334,11 +336,14 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
                        want_lq: bool = True):
     """(lq + dt gq + addq, lp + dt gp + addp) with (gq, gp) the ODE VJP for cotangents
     (lq, lp, gdiv) -- one fused pass (dicp_lddmm_euler_adjoint_step_f32).  want_lq=False:
-    (None, lp_next) only -- the gq half of the pair algebra is skipped (eta = 0)."""
+    (None, lp_next) only -- the gq half of the pair algebra is skipped (eta = 0).  lp=None: a
+    zero momentum cotangent (the b terms of the pair algebra are skipped, eta = 0)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     lq = _dev(lq, "lq")
-    lp = _dev(lp, "lp")
+    if lp is None and eta != 0:
+        lp = torch.zeros_like(q)        # the zero-cotangent shortcut exists for eta = 0 only
+    lp = None if lp is None else _dev(lp, "lp")
     gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
     addq = None if addq is None else _dev(addq, "addq")
     addp = None if addp is None else _dev(addp, "addp")
@@ -348,7 +353,9 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
     if M == 0:
         return lqn, lpn
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
-    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if want_lq else "ode_self_bwd_gp")
+    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if (want_lq and lp is not None)
+                                           else "ode_self_bwd_gp" if lp is not None
+                                           else "ode_self_bwd_b0")
     rc = _launch(name, M * M, 4 * M * (8 * D if want_lq else 7 * D),
                  lambda: lib().dicp_lddmm_euler_adjoint_step_f32(
                      _ptr(q), _ptr(p), _ptr(lq), _ptr(lp), _ptr(gdiv), M, D, float(sigma), float(eta),
@@ -598,7 +605,9 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
     q = _dev(q, "q")
     p = _dev(p, "p")
     gv = _dev(gv, "gv")
-    gmG = _dev(gmG, "gmG")
+    if gmG is None and eta != 0:
+        gmG = torch.zeros_like(q)       # the zero-cotangent shortcut exists for eta = 0 only
+    gmG = None if gmG is None else _dev(gmG, "gmG")
     gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
     M, D = q.shape
     gq = torch.empty_like(q) if want_gq else None
@@ -607,7 +616,9 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
         return gq, gp
     ws, nb = _workspace(WS_ODE_SELF_BWD_PART, M, nparts, D, q.device)
     pairs = (M * M) // nparts
-    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if want_gq else "ode_self_bwd_gp")
+    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if (want_gq and gmG is not None)
+                                           else "ode_self_bwd_gp" if gmG is not None
+                                           else "ode_self_bwd_b0")
     rc = _launch(name, pairs, 4 * M * 6 * D,
                  lambda: lib().dicp_lddmm_ode_self_bwd_part_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv),
                                                                 M, D, float(sigma), float(eta), int(part),

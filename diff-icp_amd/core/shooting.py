@@ -354,7 +354,11 @@ class ShootFn(torch.autograd.Function):
             return G[t]
 
         lq = g_or_zero(gQ, nt, (M, D)).clone()
-        lp = g_or_zero(gP, nt, (M, D)).clone()
+        # no cotangent on the final momenta (the usual loss: trajloss + data term on q1 / x1):
+        # lp stays None for the first fused adjoint step, whose VJP then skips the b terms
+        fused = split is None and scheme == "Euler" and not has_x
+        lp = gP[nt].clone() if gP is not None else (
+            None if (fused or (split is not None and eta == 0)) else torch.zeros((M, D), device=dev, dtype=Q.dtype))
         lc = g_or_zero(gC, nt, (1,)).clone()
         lx = g_or_zero(gX, nt, tuple(X.shape[1:])).clone() if has_x else None
 
@@ -371,9 +375,10 @@ class ShootFn(torch.autograd.Function):
                 if want_lq:
                     g = split.all_reduce_(torch.cat([gq_l, gp_l], 1))
                     lq = torch.add(lq, g[:, :D], alpha=dt)
-                    lp = torch.add(lp, g[:, D:], alpha=dt)
+                    lp = g[:, D:].mul(dt) if lp is None else torch.add(lp, g[:, D:], alpha=dt)
                 else:
-                    lp = torch.add(lp, split.all_reduce_(gp_l), alpha=dt)
+                    gp_r = split.all_reduce_(gp_l)
+                    lp = gp_r.mul_(dt) if lp is None else torch.add(lp, gp_r, alpha=dt)
                     lq = None
                 if gQ is not None and lq is not None:
                     lq = lq + gQ[t]

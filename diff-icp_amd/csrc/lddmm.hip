@@ -288,7 +288,15 @@ template <int D>
 int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float* gmG,
                    const float* gdiv, int64_t M, double sigma, double eta, const Outs& o,
                    void* ws, size_t wsb, hipStream_t st) {
-  Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
+  // gmG == NULL: zero cotangent on mG (eta = 0 only; the B0 symmetric kernel never reads it,
+  // the record slot is pointed at gv so every address stays valid)
+  const bool b0 = gmG == nullptr;
+  if (b0 && eta != 0.0) {
+    set_error("ode_self_bwd: a NULL mG cotangent (zero) is supported for eta = 0 only");
+    return DICP_ERR_INVALID;
+  }
+  const float* gb = b0 ? gv : gmG;
+  Args a = {q, p, gv, gb, q, p, gv, gb, 0.f};
   if (eta != 0.0) {
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
@@ -298,6 +306,7 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
+  if (b0) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, true, true);
   if (g_bwd_alg >= 2) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, g_bwd_alg == 3);
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
@@ -314,12 +323,19 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
                         int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
   if (nparts == 1)  // the whole VJP: exactly the single-device kernel
     return ode_self_bwd_d<D>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, wsb, st);
-  if (eta == 0.0 && g_bwd_alg >= 2) {
-    Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
+  const bool b0 = gmG == nullptr;  // zero mG cotangent: eta = 0, symmetric packed kernel only
+  if (eta == 0.0 && (g_bwd_alg >= 2 || b0)) {
+    const float* gb = b0 ? gv : gmG;
+    Args a = {q, p, gv, gb, q, p, gv, gb, 0.f};
     Scal sc = make_scal(sigma, 0.0);
     scale_coords(a, sc, sigma);
     sc.dev0 = gdiv;
-    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts, g_bwd_alg == 3);
+    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts,
+                             b0 || g_bwd_alg == 3, b0);
+  }
+  if (b0) {
+    set_error("ode_self_bwd_part: a NULL mG cotangent (zero) is supported for eta = 0 only");
+    return DICP_ERR_INVALID;
   }
   if (eta != 0.0 && g_bwd_eta_alg == 2) {  // symmetric packed eta VJP: quads Q = part (mod nparts)
     Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
@@ -448,7 +464,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const
                                            float* gp, void* ws, size_t ws_bytes,
                                            dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (M < 0 || (M > 0 && (!q || !p || !gv || !gmG || !gp)) || !(sigma > 0)) {
+  if (M < 0 || (M > 0 && (!q || !p || !gv || !gp)) || !(sigma > 0)) {  // gmG NULL = zero (eta = 0)
     set_error("dicp_lddmm_ode_self_bwd_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }
@@ -496,10 +512,12 @@ extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const float* ins[4] = {q, p, lq, lp};
   bool alias = false;
-  for (const float* x : ins) alias = alias || (lq_next && x == lq_next) || x == lp_next;
+  for (const float* x : ins) alias = alias || (x && ((lq_next && x == lq_next) || x == lp_next));
   // lq_next may be NULL: only lp_next is produced (the gq half of the eta = 0 symmetric VJP is
-  // then never evaluated -- the last adjoint step when the start points need no gradient)
-  if (M < 0 || (M > 0 && (!q || !p || !lq || !lp || !lp_next || alias)) || !(sigma > 0)) {
+  // then never evaluated -- the last adjoint step when the start points need no gradient).
+  // lp may be NULL: a zero cotangent on the momenta (the first adjoint step when the loss does
+  // not depend on the final momenta; eta = 0), the b terms of the VJP are then skipped.
+  if (M < 0 || (M > 0 && (!q || !p || !lq || !lp_next || alias)) || !(sigma > 0)) {
     set_error("dicp_lddmm_euler_adjoint_step_f32: invalid arguments (outputs must not alias inputs)");
     return DICP_ERR_INVALID;
   }
@@ -646,7 +664,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, 
                                                 size_t ws_bytes, dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || nparts < 1 || part < 0 || part >= nparts ||
-      (M > 0 && (!q || !p || !gv || !gmG || !gp)) || !(sigma > 0)) {  // gq may be NULL (gp only)
+      (M > 0 && (!q || !p || !gv || !gp)) || !(sigma > 0)) {  // gq may be NULL (gp only), gmG NULL = 0
     set_error("dicp_lddmm_ode_self_bwd_part_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }

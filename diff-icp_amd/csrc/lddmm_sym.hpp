@@ -855,13 +855,15 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
 }
 
 // packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp); GQ = false: gp half only
-template <int D, bool GQ>
+template <int D, bool GQ, bool B0>
 __global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                   int64_t slot_stride, int qoff, int qstride);
 
+// b0: the cotangent on mG (Args r3 / c3) is identically zero -- those pointers are then not
+// read (SymBwdPk<., ., true>, packed kernel only)
 template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
-                   hipStream_t st, int part = 0, int nparts = 1, bool pk = false) {
+                   hipStream_t st, int part = 0, int nparts = 1, bool pk = false, bool b0 = false) {
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M, nparts);
   const size_t need = sym_ws_bytes(M, 2 * D, nparts);
@@ -879,8 +881,12 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     const int64_t stride1 = M * D;
     const int nq1 = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
     if (nq1 > 0) {
-      sym_bwd_pk_kernel<D, false><<<dim3((unsigned)g.Kmax, (unsigned)nq1), dim3(256), 0, st>>>(
-          a, sc, M, g.nG, g.L, slab, stride1, part, nparts);
+      if (b0)
+        sym_bwd_pk_kernel<D, false, true><<<dim3((unsigned)g.Kmax, (unsigned)nq1), dim3(256), 0, st>>>(
+            a, sc, M, g.nG, g.L, slab, stride1, part, nparts);
+      else
+        sym_bwd_pk_kernel<D, false, false><<<dim3((unsigned)g.Kmax, (unsigned)nq1), dim3(256), 0, st>>>(
+            a, sc, M, g.nG, g.L, slab, stride1, part, nparts);
       int rc = check_launch("ode_self_bwd(sym gp)");
       if (rc) return rc;
     }
@@ -896,8 +902,11 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   const int64_t stride = M * 2 * D;
   const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
   if (nq_own > 0) {
-    if (pk)
-      sym_bwd_pk_kernel<D, true><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+    if (pk && b0)
+      sym_bwd_pk_kernel<D, true, true><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
+          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    else if (pk)
+      sym_bwd_pk_kernel<D, true, false><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
           a, sc, M, g.nG, g.L, slab, stride, part, nparts);
     else
       sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(

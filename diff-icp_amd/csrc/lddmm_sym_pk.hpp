@@ -14,7 +14,9 @@ namespace dicp {
 // whose start points need no gradient (the support points in Reg_opt): the pair scalars
 // pp, u, zu, iap, w and every gq accumulation drop out -- 32 of the 60 packed instructions
 // per step remain.
-template <int D, bool GQ = true>
+// B0 = true: the cotangent b on mG is zero (the first adjoint step: the loss does not depend
+// on the final momenta), so db, zb, pp and every cKzb term drop out -- 40 of 60 remain.
+template <int D, bool GQ = true, bool B0 = false>
 struct SymBwdPk {
   using S = SymBwd<D>;
   static constexpr int W = GQ ? 2 * D : D;
@@ -55,7 +57,23 @@ struct SymBwdPk {
       r2 = pk_fma(t.z[d], t.z[d], r2);
     }
     t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
-    if constexpr (GQ) {
+    if constexpr (B0) {
+      // b = 0: u = gam (p_i - p_j), zb = 0
+      if constexpr (GQ) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) t.u[d] = r.gp[d] - splat(gpj[d]);
+        f2 zu = t.z[0] * t.u[0];
+        f2 iap = pk_fma(r.ia_a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+#pragma unroll
+        for (int d = 1; d < D; ++d) {
+          zu = pk_fma(t.z[d], t.u[d], zu);
+          iap = pk_fma(r.ia_a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), iap));
+        }
+        t.w = pk_fma(splat(kS2), zu, -iap);
+      }
+      (void)bj;
+      (void)c;
+    } else if constexpr (GQ) {
       f2 pp = r.p[0] * splat(pj[0]);
 #pragma unroll
       for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
@@ -91,7 +109,10 @@ struct SymBwdPk {
     const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
+      if constexpr (B0)
+        acc[d] = pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]);
+      else
+        acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
       if constexpr (GQ) acc[D + d] = pk_fma(t.K, pk_fma(t.w, t.z[d], -t.u[d]), acc[D + d]);
     }
   }
@@ -105,10 +126,16 @@ struct SymBwdPk {
     const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
       const f2 tt = pk_fma(splat(gt), t.z[d], r.ia_a[d]);
-      const f2 cg = pk_fma(t.cKzb, r.p[d], t.K * tt);
-      ct[d] = cg.x + cg.y;
+      if constexpr (B0) {
+        acc[d] = pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]);
+        const f2 cg = t.K * tt;
+        ct[d] = cg.x + cg.y;
+      } else {
+        acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
+        const f2 cg = pk_fma(t.cKzb, r.p[d], t.K * tt);
+        ct[d] = cg.x + cg.y;
+      }
       if constexpr (GQ) {
         const f2 e = pk_fma(t.w, t.z[d], -t.u[d]);
         const f2 Ke = t.K * e;
@@ -283,11 +310,11 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
   }
 }
 
-template <int D, bool GQ>
+template <int D, bool GQ, bool B0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
-  sym_pk_body<SymBwdPk<D, GQ>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdPk<D, GQ, B0>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 // Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /

@@ -120,7 +120,9 @@ int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t M, int D, 
  * loop): with (gq, gp) the VJP of dicp_lddmm_ode_self_bwd_f32 for cotangents (lq, lp, gdiv),
  *   lq_next = lq + dt gq + addq,  lp_next = lp + dt gp + addp   (addq/addp (M,D) or NULL).
  * lq_next may be NULL (the last step of a sweep whose start points q0 need no gradient:
- * only lp_next, with the gq half skipped as above).
+ * only lp_next, with the gq half skipped as above).  lp may be NULL = a zero cotangent on the
+ * momenta (the first step of a sweep whose loss does not depend on the final momenta;
+ * eta = 0 only): the terms of the VJP in it are then skipped.
  * Outputs must not alias inputs.  Workspace kind DICP_WS_ODE_SELF_BWD. */
 int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
                                       const float* lp, const float* gdiv, int64_t M, int D,

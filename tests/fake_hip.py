@@ -111,6 +111,8 @@ def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=Non
 
 
 def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None, want_lq=True):
+    if lp is None:   # zero momentum cotangent
+        lp = torch.zeros_like(lq)
     gq, gp = ode_self_bwd(q, p, lq, lp, gdiv, sigma, eta)
     lqn, lpn = lq + dt * gq, lp + dt * gp
     if addq is not None:
@@ -214,6 +216,8 @@ def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_o
 
 
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True):
+    if gmG is None:   # zero momentum cotangent
+        gmG = torch.zeros_like(gv)
     """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
     its rows, zeros elsewhere; the sum over parts is the VJP."""
     gq, gp = ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta)

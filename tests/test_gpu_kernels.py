@@ -216,6 +216,37 @@ def test_adjoint_step_gp_only(dev, M, eta):
     assert torch.equal(lpn1, lpn2)      # deterministic
 
 
+@pytest.mark.parametrize("M", [1, 129, 5000, 50000])
+@pytest.mark.parametrize("want_lq", [True, False])
+def test_adjoint_step_zero_momentum_cotangent(dev, M, want_lq):
+    """euler_adjoint_step(lp=None) (lp = NULL at the C-ABI: zero cotangent on mG, the b
+    terms of the symmetric VJP skipped; also with the gq half skipped) == the step with
+    explicit zeros."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 13)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    lq = torch.randn(M, 3, generator=g).to(dev)
+    aq = torch.randn(M, 3, generator=g).to(dev)
+    gd = torch.full((1,), 0.3, device=dev)
+    z = torch.zeros_like(lq)
+    lqn, lpn = L.euler_adjoint_step(q, p, lq, z, gd, 0.1, 0.0, 0.1, aq, None, want_lq=want_lq)
+    lqn0, lpn0 = L.euler_adjoint_step(q, p, lq, None, gd, 0.1, 0.0, 0.1, aq, None, want_lq=want_lq)
+    assert rel_err(lpn0, lpn) < 1e-6, rel_err(lpn0, lpn)
+    if want_lq:
+        assert rel_err(lqn0, lqn) < 1e-6, rel_err(lqn0, lqn)
+    else:
+        assert lqn0 is None
+    for W in (2, 3):   # pair-subset parts with a zero cotangent (row split)
+        sq, sp = torch.zeros_like(lq), torch.zeros_like(lq)
+        for r in range(W):
+            pq, pp = L.ode_self_bwd_part(q, p, lq, None, gd, 0.1, 0.0, r, W)
+            sq += pq
+            sp += pp
+        gq, gp = L.ode_self_bwd(q, p, lq, z, gd, 0.1, 0.0)
+        assert rel_err(sq, gq) < 2e-6 and rel_err(sp, gp) < 2e-6
+
+
 def test_dpp_wave_rol_semantics(dev):
     """The symmetric VJP rotates column sums with DPP wave_rol:1 assuming lane l reads lane
     l + 1 (lddmm_sym.hpp rol1); pin that on the hardware."""
