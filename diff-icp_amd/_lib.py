@@ -176,6 +176,8 @@ EXEC_FLOPS_PER_PAIR = {"ode_self_bwd": 53}
 FLOPS_PER_PAIR["ode_self_bwd_gp"] = round(70 * 32 / 60)
 # zero momentum cotangent (first adjoint step): 40 of 60 packed instructions remain
 FLOPS_PER_PAIR["ode_self_bwd_b0"] = round(70 * 40 / 60)
+# forward without the momentum update (last step of a shooting whose p1 is unused): V, Z'
+FLOPS_PER_PAIR["ode_self_fwd_nog"] = 33 - 14
 
 
 class KernelProfile:
@@ -303,17 +305,20 @@ def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = 
 
 
 def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=None, p_out=None,
-               g_out=None, order=None):
+               g_out=None, order=None, want_p: bool = True):
     """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_ord_f32);
     q_out / p_out / g_out: optional contiguous destinations (must not overlap q, p); order:
-    optional int32 row visit order (see ode_self_fwd)."""
+    optional int32 row visit order (see ode_self_fwd); want_p=False: (q_next, None, g) -- the
+    momentum update is not formed (eta = 0: the pass skips its Gs' sums)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     order = _order(order, M, q.device)
     qn = torch.empty_like(q) if q_out is None else q_out
-    pn = torch.empty_like(q) if p_out is None else p_out
+    pn = (torch.empty_like(q) if p_out is None else p_out) if want_p else None
     for t, name in ((qn, "q_out"), (pn, "p_out")):
+        if t is None:
+            continue
         if not t.is_contiguous() or t.shape != q.shape or t.dtype != torch.float32:
             raise ValueError(f"{name} must be a contiguous float32 tensor shaped like q")
     g = None
@@ -324,7 +329,8 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
     if M == 0:
         return qn, pn, g
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, q.device)
-    rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), M * M, 4 * M * (4 * D + 1),
+    name = "ode_self_fwd_eta" if eta else ("ode_self_fwd" if want_p else "ode_self_fwd_nog")
+    rc = _launch(name, M * M, 4 * M * (4 * D + 1),
                  lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, 0, M, D, float(sigma),
                                                              float(eta), float(dt), _ptr(order), _ptr(qn),
                                                              _ptr(pn), _ptr(g), _ptr(ws), nb, _stream(q.device)))

@@ -18,7 +18,8 @@ from ..tools.integrators import EulerIntegrator, RalstonIntegrator
 from ..tools.kernel import GaussKernel, SVDpow
 from ..tools.optim import LBFGS_optimization
 from ..tools.spec import defspec, getspec
-from .shooting import HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootCache, ShootFn
+from .shooting import (HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootCache, ShootFn,
+                       complete_p1, skip_p1)
 
 
 class Shoot(list):
@@ -190,9 +191,11 @@ class LDDMMModel:
         raise ValueError("Unknown version")
 
     # ------------------------------------------------------------------------------------
-    def Shoot(self, q0, p0, x0=None):
+    def Shoot(self, q0, p0, x0=None, need_p1=True):
         """Geodesic shooting from (q0, p0[, x0]); returns the list of (q, p, cost[, x])
-        at the nt+1 times (LDDMM.py:286-299)."""
+        at the nt+1 times (LDDMM.py:286-299).  need_p1=False (extension, used by Optimize's
+        loss closures): the final momenta may be left unformed (NaN; `shoot.p1_missing`) --
+        the loss never reads them, and the last step then skips the momentum update's sums."""
         getspec(q0, p0, x0)
         if self.try_trajcost_optim and self.withlogdet and self.gradcomponent and x0 is None:
             # rarely used reference variant: generic integrator over the per-step ODE
@@ -202,11 +205,24 @@ class LDDMMModel:
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
                              float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet),
                              self.row_split, getattr(self, "row_orders", None),
-                             getattr(self, "shoot_cache", None))
+                             getattr(self, "shoot_cache", None), bool(need_p1))
         if x0 is None:
             Q, P, C, H0 = outs
-            return Shoot(Q, P, C, None, H0)
-        return Shoot(*outs)
+            sh = Shoot(Q, P, C, None, H0)
+        else:
+            sh = Shoot(*outs)
+        split = self.row_split if (self.row_split is not None and self.row_split.world > 1) else None
+        sh.p1_missing = skip_p1(need_p1, self.scheme, x0 is not None, float(self.eta), split,
+                                int(self.nt))
+        return sh
+
+    def complete_shoot(self, shoot):
+        """Form the final momenta of a shoot made with need_p1=False (no-op otherwise)."""
+        if getattr(shoot, "p1_missing", False):
+            complete_p1(shoot.Q, shoot.P, self.Kernel.sigma, float(self.eta),
+                        bool(self.withlogdet), int(self.nt))
+            shoot.p1_missing = False
+        return shoot
 
     def BasicQuadLossFunctor(self, y, cmul=1):
         y = y.detach()
@@ -240,9 +256,10 @@ class LDDMMModel:
         last_eval = {}
 
         def lossfunc(p0):
-            shoot = self.Shoot(q0, p0, x0)
+            shoot = self.Shoot(q0, p0, x0, need_p1=False)   # the loss never reads p1
             last = shoot[-1][-1] if is_x else shoot[-1][0]
             last_eval["p0"], last_eval["shoot"] = p0.detach().clone(), shoot.detach()
+            last_eval["p1_missing"] = getattr(shoot, "p1_missing", False)
             return self.trajloss(shoot) + dataloss(last)
 
         p0, _, nsteps, change = LBFGS_optimization([p0], lossfunc, nmax=nmax, tol=tol,
@@ -253,6 +270,8 @@ class LDDMMModel:
             # last closure evaluation was at the returned p0 its trajectory is reused
             if "p0" in last_eval and torch.equal(last_eval["p0"], p0):
                 shoot = last_eval["shoot"]
+                shoot.p1_missing = last_eval["p1_missing"]
+                self.complete_shoot(shoot)              # the returned shoot is complete
             else:
                 shoot = self.Shoot(q0, p0, x0)
             trajl = self.trajloss(shoot).item()

@@ -173,6 +173,22 @@ def _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div):
     return gq, gp, gx
 
 
+def skip_p1(need_p1, scheme, has_x, eta, split, nt):
+    """Whether ShootFn leaves the final momenta P[nt] unformed: only on request, and only on
+    the path whose last step is a fused Euler step (eta = 0, no external points, no row split,
+    nt >= 2)."""
+    return (not need_p1) and scheme == "Euler" and not has_x and eta == 0 and split is None and nt >= 2
+
+
+def complete_p1(Q, P, sigma, eta, want_div, nt, order=None):
+    """Form P[nt] of a trajectory shot with need_p1=False: the last Euler step again, by the
+    same fused pass a full shooting uses (bitwise the P[nt] it would have produced)."""
+    with torch.no_grad():
+        scratch = torch.empty_like(Q[nt])
+        _lib.euler_step(Q[nt - 1], P[nt - 1], sigma, eta, 1.0 / nt, want_div, q_out=scratch,
+                        p_out=P[nt], order=order)
+
+
 class ShootFn(torch.autograd.Function):
     """(q0, p0[, x0]) -> stacked trajectory Q, P (nt+1, M, D), C (nt+1, 1)[, X (nt+1, N, D)],
     H0 = H(q0, p0).
@@ -185,14 +201,18 @@ class ShootFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None, orders=None,
-                cache=None):
+                cache=None, need_p1=True):
         """orders: optional RowOrderCache; the forward passes then visit the support rows in
         the spatial order of q0 (kept for every step: the flow moves neighbours together).
-        cache: optional ShootCache (bitwise reuse of a repeated shooting, see there)."""
+        cache: optional ShootCache (bitwise reuse of a repeated shooting, see there).
+        need_p1=False: the final momenta P[nt] are not formed when skip_p1(...) holds (the last
+        fused Euler step skips its Gs' sums) and P[nt] is filled with NaN; the caller must not
+        read it (LDDMMModel.Optimize's closures do not) or complete it (complete_p1)."""
         ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
+        skip = skip_p1(need_p1, scheme, has_x, eta, split, nt)
         params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
-                  None if split is None else (split.rank, split.world))
+                  None if split is None else (split.rank, split.world), skip)
         hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
         if hit is not None:
             ctx.split = split if (split is not None and not has_x and scheme == "Euler"
@@ -262,8 +282,11 @@ class ShootFn(torch.autograd.Function):
                 # divergence terms go to Gd[t] and the cost is accumulated once after the loop
                 if Gd is None:
                     Gd = torch.empty((nt, M), device=dev, dtype=q0.dtype) if want_div else False
+                last_skip = skip and t == nt - 1
                 _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1],
-                                g_out=Gd[t] if want_div else None, order=order)
+                                g_out=Gd[t] if want_div else None, order=order, want_p=not last_skip)
+                if last_skip:
+                    P[t + 1].fill_(float("nan"))   # not formed: make any read loud
                 fused_from = t if fused_from is None else fused_from
                 continue
             if has_x:
@@ -440,7 +463,7 @@ class ShootFn(torch.autograd.Function):
             lp = lp + gH * v0
         if not ctx.needs_input_grad[0]:
             lq = None
-        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None
+        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None, None
 
 
 class HamiltonianFn(torch.autograd.Function):

@@ -236,6 +236,10 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     return g_fwd_alg >= 2
                ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, true>>("ode_self_fwd_eta(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
+  if (o.ptr[1] == nullptr)  // mG not wanted (eta = 0): the packed forward without the Gs' sums
+    return o.ptr[2] != nullptr
+               ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, false>>("ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st)
+               : launch_rowred_pk<OpOdeSelfFwdPk<D, false, false, false>>("ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st);
   if ((g_fwd_alg == 1 || g_fwd_alg == 4) && all)
     return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st, g_fwd_alg == 4)
                                : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st, g_fwd_alg == 4);
@@ -261,6 +265,8 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(nrows, M),
                    mfma_fwd_ws_bytes<D, true>(nrows, M), mfma_fwd_ws_bytes<D, false>(nrows, M)})
     m = v > m ? v : m;
   return m;
@@ -279,6 +285,8 @@ size_t ode_self_fwd_ws(int64_t M) {
   for (size_t e : {rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(M, M),
                    mfma_fwd_ws_bytes<D, true>(M, M), mfma_fwd_ws_bytes<D, false>(M, M)})
     a = a > e ? a : e;
   return a;
@@ -639,9 +647,10 @@ extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int
                                              float* q_next, float* p_next, float* g, void* ws,
                                              size_t ws_bytes, dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // p_next may be NULL: the momenta update is not wanted (eta = 0: its Gs' sums are skipped)
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
-      (nrows > 0 && (!q || !p || !q_next || !p_next)) || !(sigma > 0) ||
-      (nrows > 0 && (q_next == q || q_next == p || p_next == q || p_next == p))) {
+      (nrows > 0 && (!q || !p || !q_next)) || !(sigma > 0) ||
+      (nrows > 0 && (q_next == q || q_next == p || (p_next && (p_next == q || p_next == p))))) {
     set_error("dicp_lddmm_euler_step_ord_f32: invalid arguments (outputs must not alias inputs)");
     return DICP_ERR_INVALID;
   }

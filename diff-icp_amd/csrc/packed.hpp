@@ -18,9 +18,14 @@ __device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
 
 // OpOdeSelfFwd<D, ETA, DIV> (lddmm_ops.hpp) on two rows at once: V, Gs' (, Z'), and for
 // eta != 0 (ETA, which implies Z') the Hs, GL' and L sums of the logdet / gradcomponent model.
-template <int D, bool DIV, bool ETA = false>
+// G = false (eta = 0 only): the Gs' sums are not formed (mG not wanted: the last step of a
+// shooting whose final momenta are not used) -- 7 of the 19 per-pair instructions drop.
+template <int D, bool DIV, bool ETA = false, bool G = true>
 struct OpOdeSelfFwdPk {
+  static_assert(G || !ETA, "mG-less forward: eta = 0 only");
   using Base = OpOdeSelfFwd<D, ETA, DIV || ETA>;
+  // column splits as the full pass: the same chunk boundaries, hence bitwise the same v / g
+  using SplitAs = OpOdeSelfFwdPk<D, DIV, ETA, true>;
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = Base::NACC;
   static constexpr int kNOut = Base::kNOut;
@@ -48,14 +53,17 @@ struct OpOdeSelfFwdPk {
     }
     const f2 K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
     const float* pj = rec + D;
-    f2 pp = r.p[0] * splat(pj[0]);
+    if constexpr (G) {
+      f2 pp = r.p[0] * splat(pj[0]);
 #pragma unroll
-    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
-    const f2 Kpp = K * pp;
+      for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+      const f2 Kpp = K * pp;
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       acc[d] = pk_fma(K, splat(pj[d]), acc[d]);
-      acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
       if (DIV || ETA) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
     }
     if (ETA) {  // OpOdeSelfFwd::pair, eta != 0 terms
@@ -183,10 +191,16 @@ int64_t rowred_pk_capacity() {
   return cap;
 }
 
+template <class T, class = void>
+struct split_as { using type = T; };
+template <class T>
+struct split_as<T, std::void_t<typename T::SplitAs>> { using type = typename T::SplitAs; };
+
 template <class Op>
 int rowred_pk_splits(int64_t M, int64_t N) {
   using Base = typename Op::Base;
-  return num_splits_cap(M, N, 2, rowred_pk_capacity<Op>(), round_rows_of<Base>::rows,
+  using SOp = typename split_as<Op>::type;   // ops may borrow another variant's geometry
+  return num_splits_cap(M, N, 2, rowred_pk_capacity<SOp>(), round_rows_of<Base>::rows,
                         round_rows_of<Base>::max);
 }
 

@@ -175,7 +175,9 @@ int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, int64_t M, in
  * rows share a workgroup: the matrix-core forward (fwd_alg 3) centres the column channels on
  * its workgroup's rows, and its fp32 error grows with their spread, so a spatial order (e.g.
  * Morton, _lib.spatial_order) keeps it at the ordered-pair kernels' level for any cloud extent.
- * No reference counterpart (KeOps has no row grouping to choose). */
+ * No reference counterpart (KeOps has no row grouping to choose).  In the Euler form p_next
+ * may be NULL: the momentum update is then not formed (eta = 0: the Gs' sums of the pass are
+ * skipped) -- the last step of a shooting whose final momenta are not used. */
 int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, int64_t M, int64_t row0,
                                     int64_t nrows, int D, double sigma, double eta,
                                     const int32_t* row_order, float* v, float* mG, float* g,
@@ -266,8 +268,9 @@ const char* dicp_version(void);
 int dicp_supports_dim(int D);
 /* Tuning / A-B knobs (process-wide; results of every setting agree to fp32 summation order):
  *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
- *                  rows, 3 channel contraction on the matrix cores (default; fp32 error
- *                  bounded by the rows' spread: pass a spatial row_order);
+ *                  rows (default), 3 channel contraction on the matrix cores (opt-in; fp32
+ *                  error bounded by the rows' spread: pass a spatial row_order), 4 symmetric
+ *                  pair-once with packed-FP32 rows;
  *                  eta != 0: >= 2 packed-FP32 rows, otherwise ordered scalar rows
  *   "bwd_alg"      eta = 0 VJP: 0 / 1 ordered pair algebras, 2 symmetric pair-once, 3 symmetric
  *                  with packed-FP32 rows (default)

@@ -95,8 +95,11 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta):
     return _out(gq, q), _out(gp, q)
 
 
-def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=None, order=None):
+def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=None, order=None,
+               want_p=True):
     v, mG, g, _ = ode_self_fwd(q, p, sigma, eta, want_div)
+    if not want_p:   # like the device pass: p_next is not formed
+        p_out = None
     if g_out is not None and g is not None:
         g_out.copy_(g)
         g = g_out
@@ -107,7 +110,7 @@ def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=Non
     if p_out is not None:
         p_out.copy_(pn)
         pn = p_out
-    return qn, pn, g
+    return qn, (pn if want_p else None), g
 
 
 def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None, want_lq=True):
@@ -216,10 +219,10 @@ def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_o
 
 
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True):
-    if gmG is None:   # zero momentum cotangent
-        gmG = torch.zeros_like(gv)
     """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
     its rows, zeros elsewhere; the sum over parts is the VJP."""
+    if gmG is None:   # zero momentum cotangent
+        gmG = torch.zeros_like(gv)
     gq, gp = ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta)
     M = q.shape[0]
     per = -(-M // nparts)

@@ -173,3 +173,45 @@ def test_concurrent_frames_bitwise_equal_sequential(dev):
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1] + out[0][2], out[1][1] + out[1][2]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M", [1, 129, 5000, 50000])
+def test_euler_step_without_momentum_update(dev, M):
+    """euler_step(want_p=False) (p_next = NULL at the C-ABI: the Gs' sums skipped) gives
+    bitwise the q_next and g of the full step: the mG-less pass keeps the full pass's column
+    splits (packed.hpp OpOdeSelfFwdPk::SplitAs)."""
+    from difficp_amd import _lib as L
+    g = torch.Generator().manual_seed(M + 21)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    for want_div in (False, True):
+        qn, pn, gd = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div)
+        qn1, none, gd1 = L.euler_step(q, p, 0.1, 0.0, 0.1, want_div, want_p=False)
+        assert none is None and pn is not None
+        assert torch.equal(qn1, qn)
+        if want_div:
+            assert torch.equal(gd1, gd)
+
+
+@pytest.mark.parametrize("version", ["classic", "hybrid"])
+def test_optimize_final_shoot_complete(dev, version):
+    """LDDMMModel.Optimize's loss closures shoot with need_p1=False (the final momenta are
+    never read by the loss); the shoot it returns is completed and equals, bitwise, a fresh
+    full shooting at the returned p0 (trajectory, cost and final momenta)."""
+    from difficp_amd.core.LDDMM import LDDMMModel
+    g = torch.Generator().manual_seed(5)
+    M = 3000
+    q0 = torch.rand(M, 2, generator=g).to(dev)
+    p0 = torch.zeros(M, 2, device=dev)
+    tgt = (torch.rand(M, 2, generator=g) * 0.1).to(dev) + q0
+    LM = LDDMMModel(sigma=0.1, D=2, lambd=5.0, version=version, scheme="Euler", nt=6,
+                    spec={"device": dev, "dtype": torch.float32})
+    sh0 = LM.Shoot(q0, p0, need_p1=False)
+    assert sh0.p1_missing and torch.isnan(sh0.P[-1]).all()
+    p, shoot, trajl, datal, nsteps, change = LM.Optimize(
+        lambda q: ((q - tgt) ** 2).sum(), q0, p0, nmax=4)
+    assert not getattr(shoot, "p1_missing", False)
+    LM.shoot_cache = None
+    ref = LM.Shoot(q0, p)
+    assert torch.equal(shoot.Q, ref.Q) and torch.equal(shoot.P, ref.P)
+    assert torch.equal(shoot.C, ref.C)
