@@ -106,9 +106,29 @@ def supports_dim(D: int) -> bool:
     return bool(lib().dicp_supports_dim(int(D)))
 
 
+# mirror of the library's algorithm choices that change what an entry accepts (a NULL mG
+# cotangent at eta != 0 needs the packed symmetric VJP, bwd_eta_alg 2 = the library default)
+_OPTIONS = {"bwd_eta_alg": 2}
+
+
 def set_option(name: str, value: int):
     """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
     _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")
+    if name in _OPTIONS:
+        _OPTIONS[name] = int(value)
+
+
+def _zero_b_ok(eta) -> bool:
+    """Whether a zero mG cotangent may be passed as NULL (the symmetric packed VJPs skip its
+    terms); otherwise the caller materialises zeros."""
+    return eta == 0 or _OPTIONS["bwd_eta_alg"] == 2
+
+
+def _bwd_name(eta, want_gq: bool, zero_b: bool) -> str:
+    base = "ode_self_bwd_eta" if eta else "ode_self_bwd"
+    if zero_b:
+        return base + "_b0"
+    return base if want_gq else base + "_gp"
 
 
 def num_splits(kind: int, M: int, N: int) -> int:
@@ -178,6 +198,11 @@ FLOPS_PER_PAIR["ode_self_bwd_gp"] = round(70 * 32 / 60)
 FLOPS_PER_PAIR["ode_self_bwd_b0"] = round(70 * 40 / 60)
 # forward without the momentum update (last step of a shooting whose p1 is unused): V, Z'
 FLOPS_PER_PAIR["ode_self_fwd_nog"] = 33 - 14
+# eta != 0 (logdet model), same pricing by packed-instruction share of the full loop: gp only
+# 39 of 98 per column, zero mG cotangent 56 of 98; forward without mG 14 of 39
+FLOPS_PER_PAIR["ode_self_bwd_eta_gp"] = round(120 * 39 / 98)
+FLOPS_PER_PAIR["ode_self_bwd_eta_b0"] = round(120 * 56 / 98)
+FLOPS_PER_PAIR["ode_self_fwd_eta_nog"] = round(70 * 14 / 39)
 
 
 class KernelProfile:
@@ -309,7 +334,7 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
     """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_ord_f32);
     q_out / p_out / g_out: optional contiguous destinations (must not overlap q, p); order:
     optional int32 row visit order (see ode_self_fwd); want_p=False: (q_next, None, g) -- the
-    momentum update is not formed (eta = 0: the pass skips its Gs' sums)."""
+    momentum update is not formed (the packed pass skips the sums that feed mG only)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
@@ -329,7 +354,7 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
     if M == 0:
         return qn, pn, g
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, q.device)
-    name = "ode_self_fwd_eta" if eta else ("ode_self_fwd" if want_p else "ode_self_fwd_nog")
+    name = ("ode_self_fwd_eta" if eta else "ode_self_fwd") + ("" if want_p else "_nog")
     rc = _launch(name, M * M, 4 * M * (4 * D + 1),
                  lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, 0, M, D, float(sigma),
                                                              float(eta), float(dt), _ptr(order), _ptr(qn),
@@ -342,13 +367,13 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
                        want_lq: bool = True):
     """(lq + dt gq + addq, lp + dt gp + addp) with (gq, gp) the ODE VJP for cotangents
     (lq, lp, gdiv) -- one fused pass (dicp_lddmm_euler_adjoint_step_f32).  want_lq=False:
-    (None, lp_next) only -- the gq half of the pair algebra is skipped (eta = 0).  lp=None: a
-    zero momentum cotangent (the b terms of the pair algebra are skipped, eta = 0)."""
+    (None, lp_next) only -- the gq half of the pair algebra is skipped.  lp=None: a zero
+    momentum cotangent (the b terms of the pair algebra are skipped)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     lq = _dev(lq, "lq")
-    if lp is None and eta != 0:
-        lp = torch.zeros_like(q)        # the zero-cotangent shortcut exists for eta = 0 only
+    if lp is None and not _zero_b_ok(eta):
+        lp = torch.zeros_like(q)        # this VJP variant has no zero-cotangent shortcut
     lp = None if lp is None else _dev(lp, "lp")
     gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
     addq = None if addq is None else _dev(addq, "addq")
@@ -359,9 +384,7 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
     if M == 0:
         return lqn, lpn
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
-    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if (want_lq and lp is not None)
-                                           else "ode_self_bwd_gp" if lp is not None
-                                           else "ode_self_bwd_b0")
+    name = _bwd_name(eta, want_lq, lp is None)
     rc = _launch(name, M * M, 4 * M * (8 * D if want_lq else 7 * D),
                  lambda: lib().dicp_lddmm_euler_adjoint_step_f32(
                      _ptr(q), _ptr(p), _ptr(lq), _ptr(lp), _ptr(gdiv), M, D, float(sigma), float(eta),
@@ -611,8 +634,8 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
     q = _dev(q, "q")
     p = _dev(p, "p")
     gv = _dev(gv, "gv")
-    if gmG is None and eta != 0:
-        gmG = torch.zeros_like(q)       # the zero-cotangent shortcut exists for eta = 0 only
+    if gmG is None and not _zero_b_ok(eta):
+        gmG = torch.zeros_like(q)       # this VJP variant has no zero-cotangent shortcut
     gmG = None if gmG is None else _dev(gmG, "gmG")
     gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
     M, D = q.shape
@@ -622,9 +645,7 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
         return gq, gp
     ws, nb = _workspace(WS_ODE_SELF_BWD_PART, M, nparts, D, q.device)
     pairs = (M * M) // nparts
-    name = "ode_self_bwd_eta" if eta else ("ode_self_bwd" if (want_gq and gmG is not None)
-                                           else "ode_self_bwd_gp" if gmG is not None
-                                           else "ode_self_bwd_b0")
+    name = _bwd_name(eta, want_gq, gmG is None)
     rc = _launch(name, pairs, 4 * M * 6 * D,
                  lambda: lib().dicp_lddmm_ode_self_bwd_part_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv),
                                                                 M, D, float(sigma), float(eta), int(part),

@@ -175,9 +175,9 @@ def _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div):
 
 def skip_p1(need_p1, scheme, has_x, eta, split, nt):
     """Whether ShootFn leaves the final momenta P[nt] unformed: only on request, and only on
-    the path whose last step is a fused Euler step (eta = 0, no external points, no row split,
-    nt >= 2)."""
-    return (not need_p1) and scheme == "Euler" and not has_x and eta == 0 and split is None and nt >= 2
+    the path whose last step is a fused Euler step (no external points, no row split, nt >= 2).
+    `eta` is accepted for the callers' symmetry: both models have the mG-less pass."""
+    return (not need_p1) and scheme == "Euler" and not has_x and split is None and nt >= 2
 
 
 def complete_p1(Q, P, sigma, eta, want_div, nt, order=None):
@@ -381,7 +381,7 @@ class ShootFn(torch.autograd.Function):
         # lp stays None for the first fused adjoint step, whose VJP then skips the b terms
         fused = split is None and scheme == "Euler" and not has_x
         lp = gP[nt].clone() if gP is not None else (
-            None if (fused or (split is not None and eta == 0)) else torch.zeros((M, D), device=dev, dtype=Q.dtype))
+            None if (fused or split is not None) else torch.zeros((M, D), device=dev, dtype=Q.dtype))
         lc = g_or_zero(gC, nt, (1,)).clone()
         lx = g_or_zero(gX, nt, tuple(X.shape[1:])).clone() if has_x else None
 

@@ -232,10 +232,14 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
-  if (eta != 0.0)
+  if (eta != 0.0) {
+    if (g_fwd_alg >= 2 && o.ptr[1] == nullptr)  // mG not wanted: without the Gs', Hs, GL' sums
+      return launch_rowred_pk<OpOdeSelfFwdPk<D, true, true, false>>("ode_self_fwd_eta(pk, no mG)", a, sc, nrows, M, o,
+                                                                     ws, wsb, st);
     return g_fwd_alg >= 2
                ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, true>>("ode_self_fwd_eta(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
+  }
   if (o.ptr[1] == nullptr)  // mG not wanted (eta = 0): the packed forward without the Gs' sums
     return o.ptr[2] != nullptr
                ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, false>>("ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st)
@@ -266,6 +270,7 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(nrows, M),
                    mfma_fwd_ws_bytes<D, true>(nrows, M), mfma_fwd_ws_bytes<D, false>(nrows, M)})
     m = v > m ? v : m;
@@ -286,6 +291,7 @@ size_t ode_self_fwd_ws(int64_t M) {
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(M, M),
                    mfma_fwd_ws_bytes<D, true>(M, M), mfma_fwd_ws_bytes<D, false>(M, M)})
     a = a > e ? a : e;
@@ -296,11 +302,11 @@ template <int D>
 int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float* gmG,
                    const float* gdiv, int64_t M, double sigma, double eta, const Outs& o,
                    void* ws, size_t wsb, hipStream_t st) {
-  // gmG == NULL: zero cotangent on mG (eta = 0 only; the B0 symmetric kernel never reads it,
-  // the record slot is pointed at gv so every address stays valid)
+  // gmG == NULL: zero cotangent on mG (the B0 symmetric packed kernels never read it; the
+  // record slot is pointed at gv so every address stays valid)
   const bool b0 = gmG == nullptr;
-  if (b0 && eta != 0.0) {
-    set_error("ode_self_bwd: a NULL mG cotangent (zero) is supported for eta = 0 only");
+  if (b0 && eta != 0.0 && g_bwd_eta_alg != 2) {
+    set_error("ode_self_bwd: a NULL mG cotangent (zero) needs the packed eta kernel (bwd_eta_alg 2)");
     return DICP_ERR_INVALID;
   }
   const float* gb = b0 ? gv : gmG;
@@ -308,7 +314,8 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   if (eta != 0.0) {
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
-    if (g_bwd_eta_alg >= 1) return launch_sym_bwd_eta<D>(a, sc, M, o, ws, wsb, st, g_bwd_eta_alg == 2);
+    if (g_bwd_eta_alg >= 1)
+      return launch_sym_bwd_eta<D>(a, sc, M, o, ws, wsb, st, g_bwd_eta_alg == 2, 0, 1, b0);
     return launch_r<OpOdeSelfBwdEta<D>>(r_bwd(), "ode_self_bwd_eta", a, sc, M, M, o, ws, wsb, st);
   }
   Scal sc = make_scal(sigma, 0.0);
@@ -331,7 +338,7 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
                         int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
   if (nparts == 1)  // the whole VJP: exactly the single-device kernel
     return ode_self_bwd_d<D>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, wsb, st);
-  const bool b0 = gmG == nullptr;  // zero mG cotangent: eta = 0, symmetric packed kernel only
+  const bool b0 = gmG == nullptr;  // zero mG cotangent: symmetric packed kernels only
   if (eta == 0.0 && (g_bwd_alg >= 2 || b0)) {
     const float* gb = b0 ? gv : gmG;
     Args a = {q, p, gv, gb, q, p, gv, gb, 0.f};
@@ -341,15 +348,16 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
     return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts,
                              b0 || g_bwd_alg == 3, b0);
   }
-  if (b0) {
-    set_error("ode_self_bwd_part: a NULL mG cotangent (zero) is supported for eta = 0 only");
-    return DICP_ERR_INVALID;
-  }
   if (eta != 0.0 && g_bwd_eta_alg == 2) {  // symmetric packed eta VJP: quads Q = part (mod nparts)
-    Args a = {q, p, gv, gmG, q, p, gv, gmG, 0.f};
+    const float* gb = b0 ? gv : gmG;
+    Args a = {q, p, gv, gb, q, p, gv, gb, 0.f};
     Scal sc = make_scal(sigma, eta);
     sc.dev0 = gdiv;
-    return launch_sym_bwd_eta<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, true, part, nparts);
+    return launch_sym_bwd_eta<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, true, part, nparts, b0);
+  }
+  if (b0) {
+    set_error("ode_self_bwd_part: a NULL mG cotangent (zero) needs a symmetric packed kernel");
+    return DICP_ERR_INVALID;
   }
   const int64_t per = (M + nparts - 1) / nparts;
   const int64_t r0 = per * part < M ? per * part : M;
@@ -647,7 +655,8 @@ extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int
                                              float* q_next, float* p_next, float* g, void* ws,
                                              size_t ws_bytes, dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // p_next may be NULL: the momenta update is not wanted (eta = 0: its Gs' sums are skipped)
+  // p_next may be NULL: the momenta update is not wanted (the packed pass skips its Gs' / Hs /
+  // GL' sums)
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
       (nrows > 0 && (!q || !p || !q_next)) || !(sigma > 0) ||
       (nrows > 0 && (q_next == q || q_next == p || (p_next && (p_next == q || p_next == p))))) {

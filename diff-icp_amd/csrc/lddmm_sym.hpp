@@ -807,18 +807,23 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   return check_launch("ode_self_fwd(sym merge)");
 }
 
-// packed-FP32 rows of the eta != 0 VJP (lddmm_sym_pk.hpp)
-template <int D>
+// packed-FP32 rows of the eta != 0 VJP (lddmm_sym_pk.hpp); GQ = false: gp half only, B0: zero
+// cotangent on mG
+template <int D, bool GQ, bool B0>
 __global__ void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                       int64_t slot_stride, int qoff, int qstride);
 
+// b0: the cotangent on mG (Args r3 / c3) is identically zero and is not read (packed kernel
+// only); o.ptr[0] == NULL with the packed kernel: the gq half is never evaluated
 template <int D>
 int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws,
-                       size_t wsb, hipStream_t st, bool pk = false, int part = 0, int nparts = 1) {
+                       size_t wsb, hipStream_t st, bool pk = false, int part = 0, int nparts = 1,
+                       bool b0 = false) {
   using S = SymBwdEta<D>;
   if (M <= 0) return DICP_OK;
-  if (nparts > 1 && !pk) {
-    set_error("ode_self_bwd(sym eta): pair-subset parts need the packed kernel (bwd_eta_alg 2)");
+  if ((nparts > 1 || b0) && !pk) {
+    set_error("ode_self_bwd(sym eta): pair-subset parts and a zero mG cotangent need the packed "
+              "kernel (bwd_eta_alg 2)");
     return DICP_ERR_INVALID;
   }
   const SymGeom g = sym_geom(M, nparts);
@@ -832,25 +837,38 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
     return DICP_ERR_INVALID;
   }
   float* slab = reinterpret_cast<float*>(ws);
-  const int64_t stride = M * S::W;
+  const bool gq = !pk || o.ptr[0] != nullptr;
+  const int W = gq ? S::W : D;
+  const int64_t stride = M * W;
   const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
   if (nq_own > 0) {
-    if (pk)
-      sym_bwd_eta_pk_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
-          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    const dim3 grid((unsigned)g.Kmax, (unsigned)nq_own);
+    if (pk && gq && b0)
+      sym_bwd_eta_pk_kernel<D, true, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    else if (pk && gq)
+      sym_bwd_eta_pk_kernel<D, true, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    else if (pk && b0)
+      sym_bwd_eta_pk_kernel<D, false, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    else if (pk)
+      sym_bwd_eta_pk_kernel<D, false, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
     else
       sym_kernel<S><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(a, sc, M, g.nG, g.L,
                                                                                   slab, stride);
     int rc = check_launch("ode_self_bwd(sym eta)");
     if (rc) return rc;
   }
-  const int64_t n = M * S::W;
-  if (nparts > 1)
-    sym_merge_kernel<D, true><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, 1.f, 1.f, o, part, nparts);
-  else
-    sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, 1.f, 1.f, o, 0, 1);
+  const dim3 mg((unsigned)((M * W + 255) / 256));
+  if (gq) {
+    if (nparts > 1)
+      sym_merge_kernel<D, true><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, 1.f, 1.f, o, part, nparts);
+    else
+      sym_merge_kernel<D, false><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, 1.f, 1.f, o, 0, 1);
+  } else {
+    if (nparts > 1)
+      sym_merge_kernel<D, true, D><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, 1.f, 1.f, o, part, nparts);
+    else
+      sym_merge_kernel<D, false, D><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, 1.f, 1.f, o, 0, 1);
+  }
   return check_launch("ode_self_bwd(sym eta merge)");
 }
 

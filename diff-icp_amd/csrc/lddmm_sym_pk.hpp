@@ -320,11 +320,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD
 // Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /
 // gradcomponent model): the same per-pair algebra on float2 rows, column side summed over the
 // lane's two rows before the rotation (the scalar kernel's ct = cgp(row 0) + cgp(row 1)).
-template <int D>
+// GQ = false: the gp half only (the last adjoint step when q0 needs no gradient): the pair
+// scalars pp, ap, zp, za, bp, Phi, czq, cdb, cdp and the G terms drop out.
+// B0 = true: the cotangent b on mG is zero (the first adjoint step): db, zb, bp, pp and szbK
+// drop out, Tv = -gs z.
+template <int D, bool GQ = true, bool B0 = false>
 struct SymBwdEtaPk {
   using S = SymBwdEta<D>;
   using Prm = typename S::Prm;
-  static constexpr int W = S::W;
+  static constexpr int W = GQ ? S::W : D;
   __device__ static Prm params(const Args& a, const Scal& sc) { return S::params(a, sc); }
   struct Row2 {
     f2 q[D], p[D], a[D], b[D];
@@ -351,33 +355,72 @@ struct SymBwdEtaPk {
     for (int d = 0; d < D; ++d) {
       t.z[d] = r.q[d] - splat(rec[d]);
       r2 = pk_fma(t.z[d], t.z[d], r2);
-      t.da[d] = r.a[d] - splat(aj[d]);
-      t.db[d] = r.b[d] - splat(bj[d]);
-      t.dp[d] = r.p[d] - splat(pj[d]);
+      if constexpr (GQ) {
+        t.da[d] = r.a[d] - splat(aj[d]);
+        t.dp[d] = r.p[d] - splat(pj[d]);
+      }
+      if constexpr (!B0) t.db[d] = r.b[d] - splat(bj[d]);
     }
     t.K = f2{fast_exp2(P.nc * r2.x), fast_exp2(P.nc * r2.y)};
-    f2 pp = r.p[0] * splat(pj[0]);
-    f2 ap = pk_fma(r.a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
-    f2 zb = t.z[0] * t.db[0], zp = t.z[0] * t.dp[0], za = t.z[0] * t.da[0], bp = t.db[0] * t.dp[0];
+    if constexpr (!GQ) {
+      if constexpr (!B0) {
+        f2 zb = t.z[0] * t.db[0];
 #pragma unroll
-    for (int d = 1; d < D; ++d) {
-      pp = pk_fma(r.p[d], splat(pj[d]), pp);
-      ap = pk_fma(r.a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), ap));
-      zb = pk_fma(t.z[d], t.db[d], zb);
-      zp = pk_fma(t.z[d], t.dp[d], zp);
-      za = pk_fma(t.z[d], t.da[d], za);
-      bp = pk_fma(t.db[d], t.dp[d], bp);
+        for (int d = 1; d < D; ++d) zb = pk_fma(t.z[d], t.db[d], zb);
+        t.czp = splat(P.s) * zb * splat(P.es) - splat(P.gs);
+        t.szbK = splat(P.s) * zb * t.K;
+      }
+    } else if constexpr (B0) {
+      f2 ap = pk_fma(r.a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+      f2 zp = t.z[0] * t.dp[0], za = t.z[0] * t.da[0];
+#pragma unroll
+      for (int d = 1; d < D; ++d) {
+        ap = pk_fma(r.a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), ap));
+        zp = pk_fma(t.z[d], t.dp[d], zp);
+        za = pk_fma(t.z[d], t.da[d], za);
+      }
+      const f2 sr2 = splat(P.s) * r2;
+      const f2 Phi = ap + splat(P.es) * za - splat(P.gs) * zp +
+                     splat(2.f * P.gam * P.es) * (sr2 - splat((float)D));
+      t.czq = splat(4.f * P.gam * P.es2) - splat(P.s) * Phi;
+    } else {
+      f2 pp = r.p[0] * splat(pj[0]);
+      f2 ap = pk_fma(r.a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+      f2 zb = t.z[0] * t.db[0], zp = t.z[0] * t.dp[0], za = t.z[0] * t.da[0], bp = t.db[0] * t.dp[0];
+#pragma unroll
+      for (int d = 1; d < D; ++d) {
+        pp = pk_fma(r.p[d], splat(pj[d]), pp);
+        ap = pk_fma(r.a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), ap));
+        zb = pk_fma(t.z[d], t.db[d], zb);
+        zp = pk_fma(t.z[d], t.dp[d], zp);
+        za = pk_fma(t.z[d], t.da[d], za);
+        bp = pk_fma(t.db[d], t.dp[d], bp);
+      }
+      const f2 sr2 = splat(P.s) * r2;
+      const f2 sr2D2 = sr2 - splat((float)(D + 2));
+      const f2 Phi = ap + splat(P.es) * za + splat(P.s) * pp * zb +
+                     splat(P.es) * (splat(P.s) * zp * zb - bp) - splat(P.e2s2) * zb * sr2D2 -
+                     splat(P.gs) * zp + splat(2.f * P.gam * P.es) * (sr2 - splat((float)D));
+      t.czp = splat(P.s) * zb * splat(P.es) - splat(P.gs);
+      t.czq = splat(-2.f * P.e2s2 * P.s) * zb + splat(4.f * P.gam * P.es2) - splat(P.s) * Phi;
+      t.cdb = splat(P.s) * pp + splat(P.es2) * zp - splat(P.e2s2) * sr2D2;
+      t.cdp = splat(P.es2) * zb - splat(P.gs);
+      t.szbK = splat(P.s) * zb * t.K;
     }
-    const f2 sr2 = splat(P.s) * r2;
-    const f2 sr2D2 = sr2 - splat((float)(D + 2));
-    const f2 Phi = ap + splat(P.es) * za + splat(P.s) * pp * zb +
-                   splat(P.es) * (splat(P.s) * zp * zb - bp) - splat(P.e2s2) * zb * sr2D2 -
-                   splat(P.gs) * zp + splat(2.f * P.gam * P.es) * (sr2 - splat((float)D));
-    t.czp = splat(P.s) * zb * splat(P.es) - splat(P.gs);
-    t.czq = splat(-2.f * P.e2s2 * P.s) * zb + splat(4.f * P.gam * P.es2) - splat(P.s) * Phi;
-    t.cdb = splat(P.s) * pp + splat(P.es2) * zp - splat(P.e2s2) * sr2D2;
-    t.cdp = splat(P.es2) * zb - splat(P.gs);
-    t.szbK = splat(P.s) * zb * t.K;
+  }
+  // Tv_d = czp z_d - es db_d (B0: czp = -gs, db = 0)
+  __device__ static f2 tv(const Prm& P, const Shared& t, int d) {
+    if constexpr (B0)
+      return splat(-P.gs) * t.z[d];
+    else
+      return pk_fma(t.czp, t.z[d], splat(-P.es) * t.db[d]);
+  }
+  // G_d (before the factor K) = es da_d + cdb db_d + cdp dp_d + czq z_d (B0: cdb db = 0, cdp = -gs)
+  __device__ static f2 gterm(const Prm& P, const Shared& t, int d) {
+    if constexpr (B0)
+      return pk_fma(splat(P.es), t.da[d], pk_fma(splat(-P.gs), t.dp[d], t.czq * t.z[d]));
+    else
+      return pk_fma(splat(P.es), t.da[d], pk_fma(t.cdb, t.db[d], pk_fma(t.cdp, t.dp[d], t.czq * t.z[d])));
   }
   // ordered pairs of both rows, row side only (diag blocks)
   __device__ static void pair_row(const Prm& P, const Row2& r, const float* rec, f2* acc) {
@@ -387,10 +430,12 @@ struct SymBwdEtaPk {
     const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const f2 Tv = pk_fma(t.czp, t.z[d], splat(-P.es) * t.db[d]);
-      acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, pk_fma(t.szbK, splat(pj[d]), acc[d]));
-      const f2 G = pk_fma(splat(P.es), t.da[d], pk_fma(t.cdb, t.db[d], pk_fma(t.cdp, t.dp[d], t.czq * t.z[d])));
-      acc[D + d] = pk_fma(t.K, G, acc[D + d]);
+      const f2 Tv = tv(P, t, d);
+      if constexpr (B0)
+        acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, acc[d]);
+      else
+        acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, pk_fma(t.szbK, splat(pj[d]), acc[d]));
+      if constexpr (GQ) acc[D + d] = pk_fma(t.K, gterm(P, t, d), acc[D + d]);
     }
   }
   // unordered pairs of both rows: row side into acc, the column's total (both rows) into ct
@@ -401,22 +446,30 @@ struct SymBwdEtaPk {
     const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const f2 Tv = pk_fma(t.czp, t.z[d], splat(-P.es) * t.db[d]);
-      const f2 G = t.K * pk_fma(splat(P.es), t.da[d], pk_fma(t.cdb, t.db[d], pk_fma(t.cdp, t.dp[d], t.czq * t.z[d])));
-      acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, pk_fma(t.szbK, splat(pj[d]), acc[d]));
-      acc[D + d] = acc[D + d] + G;
-      const f2 cgp = pk_fma(t.K, r.a[d] - Tv, t.szbK * r.p[d]);
+      const f2 Tv = tv(P, t, d);
+      f2 cgp;
+      if constexpr (B0) {
+        acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, acc[d]);
+        cgp = t.K * (r.a[d] - Tv);
+      } else {
+        acc[d] = pk_fma(t.K, splat(aj[d]) + Tv, pk_fma(t.szbK, splat(pj[d]), acc[d]));
+        cgp = pk_fma(t.K, r.a[d] - Tv, t.szbK * r.p[d]);
+      }
       ct[d] = cgp.x + cgp.y;
-      ct[D + d] = -G.x - G.y;
+      if constexpr (GQ) {
+        const f2 G = t.K * gterm(P, t, d);
+        acc[D + d] = acc[D + d] + G;
+        ct[D + d] = -G.x - G.y;
+      }
     }
   }
 };
 
-template <int D>
+template <int D, bool GQ, bool B0>
 __global__ __launch_bounds__(256) void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,
                                                              float* __restrict__ slab, int64_t slot_stride,
                                                              int qoff, int qstride) {
-  sym_pk_body<SymBwdEtaPk<D>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdEtaPk<D, GQ, B0>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 // Packed-FP32 rows of the symmetric (pair-once) eta = 0 forward (lddmm_sym.hpp SymFwd): the

@@ -18,11 +18,11 @@ __device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
 
 // OpOdeSelfFwd<D, ETA, DIV> (lddmm_ops.hpp) on two rows at once: V, Gs' (, Z'), and for
 // eta != 0 (ETA, which implies Z') the Hs, GL' and L sums of the logdet / gradcomponent model.
-// G = false (eta = 0 only): the Gs' sums are not formed (mG not wanted: the last step of a
-// shooting whose final momenta are not used) -- 7 of the 19 per-pair instructions drop.
+// G = false: the sums feeding mG only (Gs', and for eta != 0 Hs and GL') are not formed (mG not
+// wanted: the last step of a shooting whose final momenta are not used) -- eta = 0: 7 of the
+// 19 per-pair packed instructions drop; eta != 0: 25 of 39.
 template <int D, bool DIV, bool ETA = false, bool G = true>
 struct OpOdeSelfFwdPk {
-  static_assert(G || !ETA, "mG-less forward: eta = 0 only");
   using Base = OpOdeSelfFwd<D, ETA, DIV || ETA>;
   // column splits as the full pass: the same chunk boundaries, hence bitwise the same v / g
   using SplitAs = OpOdeSelfFwdPk<D, DIV, ETA, true>;
@@ -67,19 +67,21 @@ struct OpOdeSelfFwdPk {
       if (DIV || ETA) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
     }
     if (ETA) {  // OpOdeSelfFwd::pair, eta != 0 terms
-      f2 u[D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) u[d] = r.p[d] - splat(pj[d]);
-      f2 zu = z[0] * u[0];
-#pragma unroll
-      for (int d = 1; d < D; ++d) zu = pk_fma(z[d], u[d], zu);
-      const f2 szu = splat(kS2) * zu;
       const f2 sr2 = splat(kS2) * r2;
-      const f2 KGL = K * (sr2 - splat((float)(D + 2)));
+      if constexpr (G) {  // Hs, GL' feed mG only
+        f2 u[D];
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        acc[3 * D + d] = pk_fma(K, pk_fma(szu, z[d], -u[d]), acc[3 * D + d]);  // Hs
-        acc[4 * D + d] = pk_fma(KGL, z[d], acc[4 * D + d]);                     // GL'
+        for (int d = 0; d < D; ++d) u[d] = r.p[d] - splat(pj[d]);
+        f2 zu = z[0] * u[0];
+#pragma unroll
+        for (int d = 1; d < D; ++d) zu = pk_fma(z[d], u[d], zu);
+        const f2 szu = splat(kS2) * zu;
+        const f2 KGL = K * (sr2 - splat((float)(D + 2)));
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          acc[3 * D + d] = pk_fma(K, pk_fma(szu, z[d], -u[d]), acc[3 * D + d]);  // Hs
+          acc[4 * D + d] = pk_fma(KGL, z[d], acc[4 * D + d]);                     // GL'
+        }
       }
       acc[5 * D] = pk_fma(K, sr2 - splat((float)D), acc[5 * D]);  // L
     }

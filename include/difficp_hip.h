@@ -101,8 +101,9 @@ int dicp_lddmm_ode_self_fwd_f32(const float* q, const float* p, int64_t M, int D
 /* Vector-Jacobian product of the fused self ODE (what KeOps autodiff provides at
  * optim.py:46).  Cotangents: gv (M,D) on v, gmG (M,D) on mG, and gdiv = cotangent of
  * sum_i g_i, a DEVICE scalar (may be NULL = 0).  Outputs gq, gp (M,D), overwritten; gq may be
- * NULL (gp only: for eta = 0 with the default symmetric kernel the gq half of the pair
- * algebra -- about half of it -- is then skipped). */
+ * NULL (gp only: with the default symmetric packed kernels -- both models -- the gq half of the
+ * pair algebra, about half of it, is then skipped).  gmG may be NULL = a zero cotangent (with
+ * the default symmetric packed kernels; eta != 0 with another "bwd_eta_alg": DICP_ERR_INVALID). */
 int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const float* gv,
                                 const float* gmG, const float* gdiv, int64_t M, int D,
                                 double sigma, double eta, float* gq, float* gp, void* ws,
@@ -121,8 +122,8 @@ int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t M, int D, 
  *   lq_next = lq + dt gq + addq,  lp_next = lp + dt gp + addp   (addq/addp (M,D) or NULL).
  * lq_next may be NULL (the last step of a sweep whose start points q0 need no gradient:
  * only lp_next, with the gq half skipped as above).  lp may be NULL = a zero cotangent on the
- * momenta (the first step of a sweep whose loss does not depend on the final momenta;
- * eta = 0 only): the terms of the VJP in it are then skipped.
+ * momenta (the first step of a sweep whose loss does not depend on the final momenta; as gmG
+ * above): the terms of the VJP in it are then skipped.
  * Outputs must not alias inputs.  Workspace kind DICP_WS_ODE_SELF_BWD. */
 int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
                                       const float* lp, const float* gdiv, int64_t M, int D,
@@ -176,8 +177,9 @@ int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, int64_t M, in
  * its workgroup's rows, and its fp32 error grows with their spread, so a spatial order (e.g.
  * Morton, _lib.spatial_order) keeps it at the ordered-pair kernels' level for any cloud extent.
  * No reference counterpart (KeOps has no row grouping to choose).  In the Euler form p_next
- * may be NULL: the momentum update is then not formed (eta = 0: the Gs' sums of the pass are
- * skipped) -- the last step of a shooting whose final momenta are not used. */
+ * may be NULL: the momentum update is then not formed (the packed pass skips the sums that feed
+ * mG only: Gs', and for eta != 0 Hs and GL') -- the last step of a shooting whose final
+ * momenta are not used. */
 int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, int64_t M, int64_t row0,
                                     int64_t nrows, int D, double sigma, double eta,
                                     const int32_t* row_order, float* v, float* mG, float* g,

@@ -218,10 +218,11 @@ def test_adjoint_step_gp_only(dev, M, eta):
 
 @pytest.mark.parametrize("M", [1, 129, 5000, 50000])
 @pytest.mark.parametrize("want_lq", [True, False])
-def test_adjoint_step_zero_momentum_cotangent(dev, M, want_lq):
+@pytest.mark.parametrize("eta", [0.0, 0.02])
+def test_adjoint_step_zero_momentum_cotangent(dev, M, want_lq, eta):
     """euler_adjoint_step(lp=None) (lp = NULL at the C-ABI: zero cotangent on mG, the b
     terms of the symmetric VJP skipped; also with the gq half skipped) == the step with
-    explicit zeros."""
+    explicit zeros; both models (eta = 0: SymBwdPk<., ., true>, eta != 0: SymBwdEtaPk)."""
     L = _lib()
     g = torch.Generator().manual_seed(M + 13)
     q = torch.rand(M, 3, generator=g).to(dev)
@@ -230,8 +231,8 @@ def test_adjoint_step_zero_momentum_cotangent(dev, M, want_lq):
     aq = torch.randn(M, 3, generator=g).to(dev)
     gd = torch.full((1,), 0.3, device=dev)
     z = torch.zeros_like(lq)
-    lqn, lpn = L.euler_adjoint_step(q, p, lq, z, gd, 0.1, 0.0, 0.1, aq, None, want_lq=want_lq)
-    lqn0, lpn0 = L.euler_adjoint_step(q, p, lq, None, gd, 0.1, 0.0, 0.1, aq, None, want_lq=want_lq)
+    lqn, lpn = L.euler_adjoint_step(q, p, lq, z, gd, 0.1, eta, 0.1, aq, None, want_lq=want_lq)
+    lqn0, lpn0 = L.euler_adjoint_step(q, p, lq, None, gd, 0.1, eta, 0.1, aq, None, want_lq=want_lq)
     assert rel_err(lpn0, lpn) < 1e-6, rel_err(lpn0, lpn)
     if want_lq:
         assert rel_err(lqn0, lqn) < 1e-6, rel_err(lqn0, lqn)
@@ -240,11 +241,36 @@ def test_adjoint_step_zero_momentum_cotangent(dev, M, want_lq):
     for W in (2, 3):   # pair-subset parts with a zero cotangent (row split)
         sq, sp = torch.zeros_like(lq), torch.zeros_like(lq)
         for r in range(W):
-            pq, pp = L.ode_self_bwd_part(q, p, lq, None, gd, 0.1, 0.0, r, W)
-            sq += pq
+            pq, pp = L.ode_self_bwd_part(q, p, lq, None, gd, 0.1, eta, r, W, want_gq=want_lq)
+            if want_lq:
+                sq += pq
+            else:
+                assert pq is None
             sp += pp
-        gq, gp = L.ode_self_bwd(q, p, lq, z, gd, 0.1, 0.0)
-        assert rel_err(sq, gq) < 2e-6 and rel_err(sp, gp) < 2e-6
+        gq, gp = L.ode_self_bwd(q, p, lq, z, gd, 0.1, eta)
+        assert rel_err(sp, gp) < 2e-6, rel_err(sp, gp)
+        if want_lq:
+            assert rel_err(sq, gq) < 2e-6, rel_err(sq, gq)
+
+
+@pytest.mark.parametrize("M", [129, 5000])
+def test_eta_zero_cotangent_on_other_algs(dev, M):
+    """With a non-packed eta VJP selected (bwd_eta_alg 0 / 1, no zero-cotangent shortcut) the
+    host materialises the zeros: lp=None still gives the step with explicit zeros."""
+    L = _lib()
+    g = torch.Generator().manual_seed(M + 17)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    lq = torch.randn(M, 3, generator=g).to(dev)
+    gd = torch.full((1,), 0.3, device=dev)
+    ref = L.euler_adjoint_step(q, p, lq, None, gd, 0.1, 0.02, 0.1)
+    try:
+        for alg in (0, 1):
+            L.set_option("bwd_eta_alg", alg)
+            got = L.euler_adjoint_step(q, p, lq, None, gd, 0.1, 0.02, 0.1)
+            assert rel_err(got[0], ref[0]) < 2e-6 and rel_err(got[1], ref[1]) < 2e-6
+    finally:
+        L.set_option("bwd_eta_alg", 2)
 
 
 def test_dpp_wave_rol_semantics(dev):

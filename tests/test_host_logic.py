@@ -320,9 +320,9 @@ def test_shoot_cache_reuse_is_bitwise(fake, scheme):
 
 @pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])
 def test_optimize_skips_final_momenta_then_completes(fake, version):
-    """Optimize's closures shoot with need_p1=False (skipped only on the fused Euler, eta = 0
-    path: P[nt] is NaN there); the returned shoot is completed and equals a fresh full
-    shooting at the returned p0."""
+    """Optimize's closures shoot with need_p1=False (skipped on the fused Euler path: P[nt]
+    is NaN there); the returned shoot is completed and equals a fresh full shooting at the
+    returned p0."""
     from difficp_amd.core.LDDMM import LDDMMModel
     g = torch.Generator().manual_seed(11)
     M = 40
@@ -331,7 +331,7 @@ def test_optimize_skips_final_momenta_then_completes(fake, version):
     LM = LDDMMModel(sigma=0.3, D=2, lambd=5.0, version=version, scheme="Euler", nt=5,
                     spec={"device": "cpu", "dtype": torch.float32})
     sh = LM.Shoot(q0, torch.zeros(M, 2), need_p1=False)
-    assert sh.p1_missing == (LM.eta == 0) and (LM.eta == 0) == (version != "logdet")
+    assert sh.p1_missing and (LM.eta == 0) == (version != "logdet")
     if sh.p1_missing:
         assert torch.isnan(sh.P[-1]).all() and not torch.isnan(sh.P[-2]).any()
     p, shoot, *_ = LM.Optimize(lambda q: ((q - tgt) ** 2).sum(), q0, torch.zeros(M, 2), nmax=3)
