@@ -600,25 +600,29 @@ def ode_self_fwd_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, wan
 
 
 def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: float,
-                    want_div: bool, q_out=None, p_out=None, order=None):
+                    want_div: bool, q_out=None, p_out=None, order=None, want_p: bool = True):
     """Rows [row0, row0 + nrows) of euler_step (dicp_lddmm_euler_step_ord_f32):
     (q + dt v, p + dt mG, g) for the slice; q_out / p_out: optional contiguous (nrows, D);
-    order: optional int32 visit order of the slice's rows."""
+    order: optional int32 visit order of the slice's rows; want_p=False: p_next is None (not
+    formed, as euler_step)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
     order = _order(order, nrows, dev)
     qn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if q_out is None else q_out
-    pn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if p_out is None else p_out
+    pn = (torch.empty((nrows, D), device=dev, dtype=torch.float32) if p_out is None else p_out) if want_p else None
     for t, name in ((qn, "q_out"), (pn, "p_out")):
+        if t is None:
+            continue
         if not t.is_contiguous() or tuple(t.shape) != (nrows, D) or t.dtype != torch.float32:
             raise ValueError(f"{name} must be a contiguous float32 ({nrows}, {D}) tensor")
     g = torch.empty(nrows, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
     if nrows == 0:
         return qn, pn, g
     ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
-    rc = _launch(("ode_self_fwd_eta" if eta else "ode_self_fwd"), nrows * M, 4 * (nrows * (4 * D + 1) + 2 * M * D),
+    name = ("ode_self_fwd_eta" if eta else "ode_self_fwd") + ("" if want_p else "_nog")
+    rc = _launch(name, nrows * M, 4 * (nrows * (4 * D + 1) + 2 * M * D),
                  lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
                                                              float(sigma), float(eta), float(dt), _ptr(order),
                                                              _ptr(qn), _ptr(pn), _ptr(g), _ptr(ws), nb,

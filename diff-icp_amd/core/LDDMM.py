@@ -211,16 +211,18 @@ class LDDMMModel:
             sh = Shoot(Q, P, C, None, H0)
         else:
             sh = Shoot(*outs)
-        split = self.row_split if (self.row_split is not None and self.row_split.world > 1) else None
-        sh.p1_missing = skip_p1(need_p1, self.scheme, x0 is not None, float(self.eta), split,
-                                int(self.nt))
+        sh.p1_missing = skip_p1(need_p1, self.scheme, x0 is not None, float(self.eta),
+                                self._split(), int(self.nt))
         return sh
+
+    def _split(self):
+        return self.row_split if (self.row_split is not None and self.row_split.world > 1) else None
 
     def complete_shoot(self, shoot):
         """Form the final momenta of a shoot made with need_p1=False (no-op otherwise)."""
         if getattr(shoot, "p1_missing", False):
             complete_p1(shoot.Q, shoot.P, self.Kernel.sigma, float(self.eta),
-                        bool(self.withlogdet), int(self.nt))
+                        bool(self.withlogdet), int(self.nt), split=self._split())
             shoot.p1_missing = False
         return shoot
 

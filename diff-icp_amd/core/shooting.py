@@ -175,15 +175,25 @@ def _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div):
 
 def skip_p1(need_p1, scheme, has_x, eta, split, nt):
     """Whether ShootFn leaves the final momenta P[nt] unformed: only on request, and only on
-    the path whose last step is a fused Euler step (no external points, no row split, nt >= 2).
-    `eta` is accepted for the callers' symmetry: both models have the mG-less pass."""
-    return (not need_p1) and scheme == "Euler" and not has_x and split is None and nt >= 2
+    the paths whose last step is a fused Euler step (no external points, nt >= 2; single
+    device or row split).  `eta` is accepted for the callers' symmetry: both models have the
+    mG-less pass."""
+    return (not need_p1) and scheme == "Euler" and not has_x and nt >= 2
 
 
-def complete_p1(Q, P, sigma, eta, want_div, nt, order=None):
+def complete_p1(Q, P, sigma, eta, want_div, nt, order=None, split=None):
     """Form P[nt] of a trajectory shot with need_p1=False: the last Euler step again, by the
-    same fused pass a full shooting uses (bitwise the P[nt] it would have produced)."""
+    same fused pass a full shooting uses (bitwise the P[nt] it would have produced; row split:
+    each rank's slice, one all-gather)."""
     with torch.no_grad():
+        if split is not None:
+            M = Q.shape[1]
+            r0, n, _ = split.rows(M)
+            _, pn_l, _ = _lib.euler_step_rows(Q[nt - 1], P[nt - 1], r0, n, sigma, eta, 1.0 / nt,
+                                              want_div, order=order)
+            (pn,), _ = split.gather_rows([pn_l], M)
+            P[nt].copy_(pn)
+            return
         scratch = torch.empty_like(Q[nt])
         _lib.euler_step(Q[nt - 1], P[nt - 1], sigma, eta, 1.0 / nt, want_div, q_out=scratch,
                         p_out=P[nt], order=order)
@@ -265,6 +275,14 @@ class ShootFn(torch.autograd.Function):
                     torch.add(q, v0, alpha=dt, out=Q[t + 1])
                     torch.add(p, mG0, alpha=dt, out=P[t + 1])
                     div = sums[1:2]
+                elif skip and t == nt - 1:
+                    # final momenta not wanted: mG-less pass, half the all-gather
+                    qn_l, _, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div,
+                                                        order=order_l, want_p=False)
+                    gs = g_l.sum().reshape(1) if g_l is not None else None
+                    (qn,), div = split.gather_rows([qn_l], M, scalar=gs)
+                    Q[t + 1].copy_(qn)
+                    P[t + 1].fill_(float("nan"))   # not formed: make any read loud
                 else:
                     qn_l, pn_l, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div,
                                                            order=order_l)

@@ -212,10 +212,11 @@ def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False, ord
         None if h is None else h[sl].contiguous()
 
 
-def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_out=None, order=None):
+def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_out=None, order=None,
+                    want_p=True):
     v, mG, g, _ = ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div)
     sl = slice(row0, row0 + nrows)
-    return q[sl] + dt * v, p[sl] + dt * mG, g
+    return q[sl] + dt * v, (p[sl] + dt * mG if want_p else None), g
 
 
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True):

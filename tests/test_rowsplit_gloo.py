@@ -49,6 +49,16 @@ def _run(split, mode=None):
     res["cost1"] = sh[-1][2].detach().clone()
     res["L"] = L.detach().clone()
     res["grad"] = p.grad.clone()
+    # 1b. Optimize: its closures leave the final momenta unformed (mG-less last step, half the
+    # last all-gather); the returned shoot is completed (row-split last step + all-gather)
+    LM.shoot_cache = None
+    p_opt, sh_opt, *_ = LM.Optimize(lambda q: ((q - tgt) ** 2).sum(), q0, p0.clone(), nmax=3)
+    assert not getattr(sh_opt, "p1_missing", False)
+    res["opt_p"] = p_opt.detach().clone()
+    res["opt_P1"] = sh_opt.P[-1].detach().clone()
+    res["opt_Q1"] = sh_opt.Q[-1].detach().clone()
+    with torch.no_grad():   # a fresh full shooting at the returned p0 (cache off): same bits
+        res["opt_P1_ref"] = LM.Shoot(q0, p_opt)[-1][1].detach().clone()
     # 2. one diff-ICP iteration of a small two-set match (GMM_opt + Reg_opt(nmax=1))
     psr = workloads.build_two_set(120, torch.device("cpu"), seed=2, nt=5)
     if split:
@@ -94,7 +104,11 @@ def test_rowsplit_matches_single_process(world, mode):
             assert float(res.pop("verified")) > 0
         # a0 comes out of L-BFGS, which amplifies the fp32 rounding of a different summation
         # order of the gradient (sum of per-rank parts)
-        for key, tol in (("q1", 2e-5), ("cost1", 2e-5), ("L", 2e-5), ("grad", 2e-5), ("a0", 5e-3)):
+        assert np.isfinite(res["opt_P1"]).all()
+        assert np.array_equal(res["opt_P1"], res["opt_P1_ref"])   # completion == full last step
+        # Optimize's iterates: L-BFGS amplifies the rounding of the per-rank summation order
+        for key, tol in (("q1", 2e-5), ("cost1", 2e-5), ("L", 2e-5), ("grad", 2e-5), ("a0", 5e-3),
+                         ("opt_p", 2e-2), ("opt_Q1", 2e-2), ("opt_P1", 2e-2)):
             ref = single[key]
             err = np.abs(res[key] - ref).max() / max(1e-12, np.abs(ref).max())
             assert err < tol, (world, rank, key, err)
