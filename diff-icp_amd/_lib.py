@@ -57,6 +57,12 @@ _SIGNATURES = {
                                       _P, _SZ, _P],
     "dicp_lddmm_ode_self_bwd_part_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _INT, _INT, _P,
                                          _P, _P, _SZ, _P],
+    "dicp_lddmm_euler_step_zs_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P, _P,
+                                     _P, _P, _SZ, _P],
+    "dicp_lddmm_euler_adjoint_step_zs_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P,
+                                             _P, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_self_bwd_part_zs_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _INT, _INT, _P,
+                                            _I64, _I64, _P, _P, _P, _SZ, _P],
     "dicp_kernel_ridge_cg_f32": [_P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _INT, _INT, _P, _SZ, _P],
     "dicp_workspace_bytes": [_INT, _I64, _I64, _INT],
     "dicp_last_error": [],
@@ -108,7 +114,26 @@ def supports_dim(D: int) -> bool:
 
 # mirror of the library's algorithm choices that change what an entry accepts (a NULL mG
 # cotangent at eta != 0 needs the packed symmetric VJP, bwd_eta_alg 2 = the library default)
-_OPTIONS = {"bwd_eta_alg": 2}
+_OPTIONS = {"bwd_eta_alg": 2, "fwd_alg": 2, "bwd_alg": 3}
+
+# divergence-row reuse (dicp_lddmm_*_zs_f32): the forward's per-row sums zs_i = sum_j K z_ij
+# feed the VJP's divergence-cotangent term (env DICP_ZS=0 turns it off, for A/B runs)
+USE_ZS = os.environ.get("DICP_ZS", "1") != "0"
+
+
+def zs_ok(eta) -> bool:
+    """Whether the fused Euler steps can hand divergence rows from the forward to the VJP
+    (eta = 0 with the packed ordered forward and the packed symmetric VJP, the defaults)."""
+    return USE_ZS and eta == 0 and _OPTIONS["fwd_alg"] == 2 and _OPTIONS["bwd_alg"] == 3
+
+
+def _zs_buf(zs, rows, D, dev, name="zs_out"):
+    if zs is None:
+        return None
+    if (not zs.is_contiguous() or tuple(zs.shape) != (rows, D) or zs.dtype != torch.float32
+            or zs.device != dev):
+        raise ValueError(f"{name} must be a contiguous float32 ({rows}, {D}) tensor on {dev}")
+    return zs
 
 
 def set_option(name: str, value: int):
@@ -330,15 +355,18 @@ def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = 
 
 
 def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=None, p_out=None,
-               g_out=None, order=None, want_p: bool = True):
+               g_out=None, order=None, want_p: bool = True, zs_out=None):
     """(q + dt v, p + dt mG, g rows or None) in one fused pass (dicp_lddmm_euler_step_ord_f32);
     q_out / p_out / g_out: optional contiguous destinations (must not overlap q, p); order:
     optional int32 row visit order (see ode_self_fwd); want_p=False: (q_next, None, g) -- the
-    momentum update is not formed (the packed pass skips the sums that feed mG only)."""
+    momentum update is not formed (the packed pass skips the sums that feed mG only);
+    zs_out: optional (M, D) destination of the divergence rows (dicp_lddmm_euler_step_zs_f32,
+    eta = 0)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     order = _order(order, M, q.device)
+    zs_out = _zs_buf(zs_out, M, D, q.device)
     qn = torch.empty_like(q) if q_out is None else q_out
     pn = (torch.empty_like(q) if p_out is None else p_out) if want_p else None
     for t, name in ((qn, "q_out"), (pn, "p_out")):
@@ -356,19 +384,21 @@ def euler_step(q, p, sigma: float, eta: float, dt: float, want_div: bool, q_out=
     ws, nb = _workspace(WS_ODE_SELF_FWD, M, M, D, q.device)
     name = ("ode_self_fwd_eta" if eta else "ode_self_fwd") + ("" if want_p else "_nog")
     rc = _launch(name, M * M, 4 * M * (4 * D + 1),
-                 lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, 0, M, D, float(sigma),
-                                                             float(eta), float(dt), _ptr(order), _ptr(qn),
-                                                             _ptr(pn), _ptr(g), _ptr(ws), nb, _stream(q.device)))
+                 lambda: lib().dicp_lddmm_euler_step_zs_f32(_ptr(q), _ptr(p), M, 0, M, D, float(sigma),
+                                                            float(eta), float(dt), _ptr(order), _ptr(qn),
+                                                            _ptr(pn), _ptr(g), _ptr(zs_out), _ptr(ws), nb,
+                                                            _stream(q.device)))
     _check_rc(rc, "euler_step")
     return qn, pn, g
 
 
 def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, addq=None, addp=None,
-                       want_lq: bool = True):
+                       want_lq: bool = True, zs=None):
     """(lq + dt gq + addq, lp + dt gp + addp) with (gq, gp) the ODE VJP for cotangents
     (lq, lp, gdiv) -- one fused pass (dicp_lddmm_euler_adjoint_step_f32).  want_lq=False:
     (None, lp_next) only -- the gq half of the pair algebra is skipped.  lp=None: a zero
-    momentum cotangent (the b terms of the pair algebra are skipped)."""
+    momentum cotangent (the b terms of the pair algebra are skipped).  zs: the forward's
+    divergence rows at q (euler_step zs_out; dicp_lddmm_euler_adjoint_step_zs_f32)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     lq = _dev(lq, "lq")
@@ -379,6 +409,7 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
     addq = None if addq is None else _dev(addq, "addq")
     addp = None if addp is None else _dev(addp, "addp")
     M, D = q.shape
+    zs = _zs_buf(zs, M, D, q.device, "zs")
     lqn = torch.empty_like(q) if want_lq else None
     lpn = torch.empty_like(q)
     if M == 0:
@@ -386,9 +417,9 @@ def euler_adjoint_step(q, p, lq, lp, gdiv, sigma: float, eta: float, dt: float, 
     ws, nb = _workspace(WS_ODE_SELF_BWD, M, M, D, q.device)
     name = _bwd_name(eta, want_lq, lp is None)
     rc = _launch(name, M * M, 4 * M * (8 * D if want_lq else 7 * D),
-                 lambda: lib().dicp_lddmm_euler_adjoint_step_f32(
+                 lambda: lib().dicp_lddmm_euler_adjoint_step_zs_f32(
                      _ptr(q), _ptr(p), _ptr(lq), _ptr(lp), _ptr(gdiv), M, D, float(sigma), float(eta),
-                     float(dt), _ptr(addq), _ptr(addp), _ptr(lqn), _ptr(lpn), _ptr(ws), nb,
+                     float(dt), _ptr(addq), _ptr(addp), _ptr(zs), _ptr(lqn), _ptr(lpn), _ptr(ws), nb,
                      _stream(q.device)))
     _check_rc(rc, "euler_adjoint_step")
     return lqn, lpn
@@ -600,16 +631,18 @@ def ode_self_fwd_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, wan
 
 
 def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: float,
-                    want_div: bool, q_out=None, p_out=None, order=None, want_p: bool = True):
+                    want_div: bool, q_out=None, p_out=None, order=None, want_p: bool = True,
+                    zs_out=None):
     """Rows [row0, row0 + nrows) of euler_step (dicp_lddmm_euler_step_ord_f32):
     (q + dt v, p + dt mG, g) for the slice; q_out / p_out: optional contiguous (nrows, D);
     order: optional int32 visit order of the slice's rows; want_p=False: p_next is None (not
-    formed, as euler_step)."""
+    formed, as euler_step); zs_out: optional (nrows, D) divergence rows of the slice."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
     order = _order(order, nrows, dev)
+    zs_out = _zs_buf(zs_out, nrows, D, dev)
     qn = torch.empty((nrows, D), device=dev, dtype=torch.float32) if q_out is None else q_out
     pn = (torch.empty((nrows, D), device=dev, dtype=torch.float32) if p_out is None else p_out) if want_p else None
     for t, name in ((qn, "q_out"), (pn, "p_out")):
@@ -623,18 +656,19 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
     ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
     name = ("ode_self_fwd_eta" if eta else "ode_self_fwd") + ("" if want_p else "_nog")
     rc = _launch(name, nrows * M, 4 * (nrows * (4 * D + 1) + 2 * M * D),
-                 lambda: lib().dicp_lddmm_euler_step_ord_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
-                                                             float(sigma), float(eta), float(dt), _ptr(order),
-                                                             _ptr(qn), _ptr(pn), _ptr(g), _ptr(ws), nb,
-                                                             _stream(dev)))
+                 lambda: lib().dicp_lddmm_euler_step_zs_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                                                            float(sigma), float(eta), float(dt), _ptr(order),
+                                                            _ptr(qn), _ptr(pn), _ptr(g), _ptr(zs_out), _ptr(ws),
+                                                            nb, _stream(dev)))
     _check_rc(rc, "euler_step_rows")
     return qn, pn, g
 
 
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, nparts: int,
-                      want_gq: bool = True):
-    """Part `part` of `nparts` of ode_self_bwd (dicp_lddmm_ode_self_bwd_part_f32): (gq, gp)
-    over a pair subset; the sum over the parts is the full VJP.  want_gq=False: (None, gp)."""
+                      want_gq: bool = True, zs=None, zrow0: int = 0):
+    """Part `part` of `nparts` of ode_self_bwd (dicp_lddmm_ode_self_bwd_part_zs_f32): (gq, gp)
+    over a pair subset; the sum over the parts is the full VJP.  want_gq=False: (None, gp).
+    zs: the forward's divergence rows of rows [zrow0, zrow0 + len(zs)) (this rank's slice)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     gv = _dev(gv, "gv")
@@ -643,6 +677,10 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
     gmG = None if gmG is None else _dev(gmG, "gmG")
     gdiv = None if gdiv is None else _dev(gdiv.reshape(-1)[:1], "gdiv")
     M, D = q.shape
+    zn = 0
+    if zs is not None:
+        zn = int(zs.shape[0])
+        zs = _zs_buf(zs, zn, D, q.device, "zs")
     gq = torch.empty_like(q) if want_gq else None
     gp = torch.empty_like(q)
     if M == 0:
@@ -651,9 +689,10 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
     pairs = (M * M) // nparts
     name = _bwd_name(eta, want_gq, gmG is None)
     rc = _launch(name, pairs, 4 * M * 6 * D,
-                 lambda: lib().dicp_lddmm_ode_self_bwd_part_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG), _ptr(gdiv),
-                                                                M, D, float(sigma), float(eta), int(part),
-                                                                int(nparts), _ptr(gq), _ptr(gp), _ptr(ws), nb,
-                                                                _stream(q.device)))
+                 lambda: lib().dicp_lddmm_ode_self_bwd_part_zs_f32(_ptr(q), _ptr(p), _ptr(gv), _ptr(gmG),
+                                                                   _ptr(gdiv), M, D, float(sigma), float(eta),
+                                                                   int(part), int(nparts), _ptr(zs), int(zrow0),
+                                                                   zn, _ptr(gq), _ptr(gp), _ptr(ws), nb,
+                                                                   _stream(q.device)))
     _check_rc(rc, "ode_self_bwd_part")
     return gq, gp

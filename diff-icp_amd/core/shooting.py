@@ -221,8 +221,13 @@ class ShootFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
         skip = skip_p1(need_p1, scheme, has_x, eta, split, nt)
+        # divergence rows (dicp_lddmm_*_zs_f32): the fused Euler steps t >= 1 keep the forward's
+        # per-row sums zs = sum_j K z, which their adjoint steps reuse for the divergence
+        # cotangent's dL/dp term instead of re-summing it pair by pair (saved, nt x M x D floats)
+        use_zs = bool(want_div) and scheme == "Euler" and not has_x and nt >= 2 and _lib.zs_ok(eta)
+        ctx.has_zs = use_zs
         params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
-                  None if split is None else (split.rank, split.world), skip)
+                  None if split is None else (split.rank, split.world), skip, use_zs)
         hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
         if hit is not None:
             ctx.split = split if (split is not None and not has_x and scheme == "Euler"
@@ -259,6 +264,10 @@ class ShootFn(torch.autograd.Function):
             elif M > _ORDER_MIN_ROWS:
                 order = orders.get(q0)
         Gd, fused_from = None, None  # fused Euler steps: per-step divergence rows, first step
+        Zs = None
+        if use_zs:
+            zrows = split.rows(M)[1] if split is not None else M
+            Zs = torch.empty((nt, zrows, D), device=dev, dtype=q0.dtype)   # Zs[0] is not formed
         for t in range(nt):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
@@ -278,14 +287,16 @@ class ShootFn(torch.autograd.Function):
                 elif skip and t == nt - 1:
                     # final momenta not wanted: mG-less pass, half the all-gather
                     qn_l, _, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div,
-                                                        order=order_l, want_p=False)
+                                                        order=order_l, want_p=False,
+                                                        zs_out=None if Zs is None else Zs[t])
                     gs = g_l.sum().reshape(1) if g_l is not None else None
                     (qn,), div = split.gather_rows([qn_l], M, scalar=gs)
                     Q[t + 1].copy_(qn)
                     P[t + 1].fill_(float("nan"))   # not formed: make any read loud
                 else:
                     qn_l, pn_l, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div,
-                                                           order=order_l)
+                                                           order=order_l,
+                                                           zs_out=None if Zs is None else Zs[t])
                     gs = g_l.sum().reshape(1) if g_l is not None else None
                     (qn, pn), div = split.gather_rows([qn_l, pn_l], M, scalar=gs)
                     Q[t + 1].copy_(qn)
@@ -302,7 +313,8 @@ class ShootFn(torch.autograd.Function):
                     Gd = torch.empty((nt, M), device=dev, dtype=q0.dtype) if want_div else False
                 last_skip = skip and t == nt - 1
                 _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1],
-                                g_out=Gd[t] if want_div else None, order=order, want_p=not last_skip)
+                                g_out=Gd[t] if want_div else None, order=order, want_p=not last_skip,
+                                zs_out=None if Zs is None else Zs[t])
                 if last_skip:
                     P[t + 1].fill_(float("nan"))   # not formed: make any read loud
                 fused_from = t if fused_from is None else fused_from
@@ -360,6 +372,8 @@ class ShootFn(torch.autograd.Function):
         saved = [Q, P, v0, mG0] + ([X] if has_x else [])
         for (qi, pi, xi) in mids:
             saved += [qi, pi] + ([xi] if has_x else [])
+        if Zs is not None:
+            saved.append(Zs)   # last (ctx.has_zs)
         ctx.save_for_backward(*saved)
         outs = (Q, P, C, X, H0) if has_x else (Q, P, C, H0)
         if cache is not None:
@@ -376,6 +390,7 @@ class ShootFn(torch.autograd.Function):
             ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x
         split = ctx.split
         saved = ctx.saved_tensors
+        Zs = saved[-1] if ctx.has_zs else None
         Q, P, v0, mG0 = saved[:4]
         X = saved[4] if has_x else None
         k = 5 if has_x else 4
@@ -411,8 +426,10 @@ class ShootFn(torch.autograd.Function):
                 # this rank's part of the pair-once VJP, summed over ranks (one all-reduce);
                 # the last step needs gp only when q0 needs no gradient (half the bytes too)
                 want_lq = t > 0 or ctx.needs_input_grad[0]
+                zs_t = Zs[t] if (Zs is not None and t >= 1) else None
                 gq_l, gp_l = _lib.ode_self_bwd_part(q, p, lq, lp, lc if want_div else None, sigma,
-                                                    eta, split.rank, split.world, want_gq=want_lq)
+                                                    eta, split.rank, split.world, want_gq=want_lq,
+                                                    zs=zs_t, zrow0=split.rows(M)[0])
                 if want_lq:
                     g = split.all_reduce_(torch.cat([gq_l, gp_l], 1))
                     lq = torch.add(lq, g[:, :D], alpha=dt)
@@ -439,7 +456,8 @@ class ShootFn(torch.autograd.Function):
                 want_lq = t > 0 or ctx.needs_input_grad[0]
                 lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lct if want_div else None, sigma, eta,
                                                  dt, None if gQ is None else gQ[t],
-                                                 None if gP is None else gP[t], want_lq=want_lq)
+                                                 None if gP is None else gP[t], want_lq=want_lq,
+                                                 zs=Zs[t] if (Zs is not None and t >= 1) else None)
                 if gC is not None:
                     lc = lc_suffix[t]
                 continue

@@ -226,12 +226,29 @@ namespace {
 template <int D>
 int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, double eta,
                    const Outs& o, void* ws, size_t wsb, hipStream_t st, int64_t row0 = 0,
-                   int64_t nrows = -1, const int* order = nullptr) {
+                   int64_t nrows = -1, const int* order = nullptr, float* zs = nullptr) {
   if (nrows < 0) nrows = M;
   const bool all = row0 == 0 && nrows == M;
   Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
+  if (zs != nullptr) {
+    // divergence rows out through the (unused) h slot: the packed ordered pass only
+    if (eta != 0.0 || o.ptr[3] != nullptr || (o.ptr[1] != nullptr && g_fwd_alg != 2)) {
+      set_error("ode_self_fwd: divergence rows (zs) need eta = 0, no h output and fwd_alg 2");
+      return DICP_ERR_INVALID;
+    }
+    Outs oz = o;
+    oz.ptr[3] = zs;
+    oz.base[3] = oz.add[3] = nullptr;
+    oz.accumulate[3] = 0;
+    oz.alpha[3] = 1.f;
+    if (o.ptr[1] == nullptr)
+      return launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, false, true>>("ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
+                                                                           M, oz, ws, wsb, st);
+    return launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, true, true>>("ode_self_fwd(pk, zs)", a, sc, nrows, M, oz,
+                                                                        ws, wsb, st);
+  }
   if (eta != 0.0) {
     if (g_fwd_alg >= 2 && o.ptr[1] == nullptr)  // mG not wanted: without the Gs', Hs, GL' sums
       return launch_rowred_pk<OpOdeSelfFwdPk<D, true, true, false>>("ode_self_fwd_eta(pk, no mG)", a, sc, nrows, M, o,
@@ -272,6 +289,8 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(nrows, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, true>>(nrows, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, true>>(nrows, M),
                    mfma_fwd_ws_bytes<D, true>(nrows, M), mfma_fwd_ws_bytes<D, false>(nrows, M)})
     m = v > m ? v : m;
   return m;
@@ -293,6 +312,8 @@ size_t ode_self_fwd_ws(int64_t M) {
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(M, M),
                    rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, true>>(M, M),
+                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, true>>(M, M),
                    mfma_fwd_ws_bytes<D, true>(M, M), mfma_fwd_ws_bytes<D, false>(M, M)})
     a = a > e ? a : e;
   return a;
@@ -301,7 +322,12 @@ size_t ode_self_fwd_ws(int64_t M) {
 template <int D>
 int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float* gmG,
                    const float* gdiv, int64_t M, double sigma, double eta, const Outs& o,
-                   void* ws, size_t wsb, hipStream_t st) {
+                   void* ws, size_t wsb, hipStream_t st, const float* zs = nullptr, int64_t zr0 = 0,
+                   int64_t zn = 0) {
+  if (zs != nullptr && (eta != 0.0 || (gmG != nullptr && g_bwd_alg != 3))) {
+    set_error("ode_self_bwd: divergence rows (zs) need eta = 0 and the packed VJP (bwd_alg 3)");
+    return DICP_ERR_INVALID;
+  }
   // gmG == NULL: zero cotangent on mG (the B0 symmetric packed kernels never read it; the
   // record slot is pointed at gv so every address stays valid)
   const bool b0 = gmG == nullptr;
@@ -321,8 +347,9 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
-  if (b0) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, true, true);
-  if (g_bwd_alg >= 2) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, g_bwd_alg == 3);
+  if (b0) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, true, true, zs, zr0, zn);
+  if (g_bwd_alg >= 2)
+    return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, g_bwd_alg == 3, false, zs, zr0, zn);
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
@@ -335,10 +362,15 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
 template <int D>
 int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const float* gmG,
                         const float* gdiv, int64_t M, double sigma, double eta, int part,
-                        int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
+                        int nparts, float* gq, float* gp, void* ws, size_t wsb, hipStream_t st,
+                        const float* zs = nullptr, int64_t zr0 = 0, int64_t zn = 0) {
   if (nparts == 1)  // the whole VJP: exactly the single-device kernel
-    return ode_self_bwd_d<D>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, wsb, st);
+    return ode_self_bwd_d<D>(q, p, gv, gmG, gdiv, M, sigma, eta, make_outs(gq, gp), ws, wsb, st, zs, zr0, zn);
   const bool b0 = gmG == nullptr;  // zero mG cotangent: symmetric packed kernels only
+  if (zs != nullptr && (eta != 0.0 || !(b0 || g_bwd_alg == 3))) {
+    set_error("ode_self_bwd_part: divergence rows (zs) need eta = 0 and the packed VJP (bwd_alg 3)");
+    return DICP_ERR_INVALID;
+  }
   if (eta == 0.0 && (g_bwd_alg >= 2 || b0)) {
     const float* gb = b0 ? gv : gmG;
     Args a = {q, p, gv, gb, q, p, gv, gb, 0.f};
@@ -346,7 +378,7 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
     scale_coords(a, sc, sigma);
     sc.dev0 = gdiv;
     return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts,
-                             b0 || g_bwd_alg == 3, b0);
+                             b0 || g_bwd_alg == 3, b0, zs, zr0, zn);
   }
   if (eta != 0.0 && g_bwd_eta_alg == 2) {  // symmetric packed eta VJP: quads Q = part (mod nparts)
     const float* gb = b0 ? gv : gmG;
@@ -519,20 +551,21 @@ extern "C" int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t
 //   lq_next = lq + dt * d/dq[lq.v + lp.mG + gdiv sum g] + addq,
 //   lp_next = lp + dt * d/dp[...]                        + addp
 // (addq / addp: the loss's own cotangent on the state at this time, or NULL).
-extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
-                                                 const float* lp, const float* gdiv, int64_t M,
-                                                 int D, double sigma, double eta, double dt,
-                                                 const float* addq, const float* addp,
-                                                 float* lq_next, float* lp_next, void* ws,
-                                                 size_t ws_bytes, dicp_stream_t stream) {
+extern "C" int dicp_lddmm_euler_adjoint_step_zs_f32(const float* q, const float* p, const float* lq,
+                                                    const float* lp, const float* gdiv, int64_t M,
+                                                    int D, double sigma, double eta, double dt,
+                                                    const float* addq, const float* addp,
+                                                    const float* zs, float* lq_next, float* lp_next,
+                                                    void* ws, size_t ws_bytes, dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const float* ins[4] = {q, p, lq, lp};
+  const float* ins[5] = {q, p, lq, lp, zs};
   bool alias = false;
   for (const float* x : ins) alias = alias || (x && ((lq_next && x == lq_next) || x == lp_next));
   // lq_next may be NULL: only lp_next is produced (the gq half of the eta = 0 symmetric VJP is
   // then never evaluated -- the last adjoint step when the start points need no gradient).
   // lp may be NULL: a zero cotangent on the momenta (the first adjoint step when the loss does
   // not depend on the final momenta; eta = 0), the b terms of the VJP are then skipped.
+  // zs may be NULL (no divergence rows).
   if (M < 0 || (M > 0 && (!q || !p || !lq || !lp_next || alias)) || !(sigma > 0)) {
     set_error("dicp_lddmm_euler_adjoint_step_f32: invalid arguments (outputs must not alias inputs)");
     return DICP_ERR_INVALID;
@@ -544,10 +577,20 @@ extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p,
   o.add[1] = addp;
   o.alpha[0] = o.alpha[1] = (float)dt;
   switch (D) {
-    case 2: return ode_self_bwd_d<2>(q, p, lq, lp, gdiv, M, sigma, eta, o, ws, ws_bytes, st);
-    case 3: return ode_self_bwd_d<3>(q, p, lq, lp, gdiv, M, sigma, eta, o, ws, ws_bytes, st);
+    case 2: return ode_self_bwd_d<2>(q, p, lq, lp, gdiv, M, sigma, eta, o, ws, ws_bytes, st, zs, 0, M);
+    case 3: return ode_self_bwd_d<3>(q, p, lq, lp, gdiv, M, sigma, eta, o, ws, ws_bytes, st, zs, 0, M);
     default: set_error("euler_adjoint_step: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
+}
+
+extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p, const float* lq,
+                                                 const float* lp, const float* gdiv, int64_t M,
+                                                 int D, double sigma, double eta, double dt,
+                                                 const float* addq, const float* addp,
+                                                 float* lq_next, float* lp_next, void* ws,
+                                                 size_t ws_bytes, dicp_stream_t stream) {
+  return dicp_lddmm_euler_adjoint_step_zs_f32(q, p, lq, lp, gdiv, M, D, sigma, eta, dt, addq, addp, nullptr,
+                                              lq_next, lp_next, ws, ws_bytes, stream);
 }
 
 extern "C" int dicp_lddmm_ode_ext_fwd_f32(const float* x, int64_t N, const float* q,
@@ -649,17 +692,18 @@ extern "C" int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, i
   }
 }
 
-extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int64_t M,
-                                             int64_t row0, int64_t nrows, int D, double sigma,
-                                             double eta, double dt, const int32_t* row_order,
-                                             float* q_next, float* p_next, float* g, void* ws,
-                                             size_t ws_bytes, dicp_stream_t stream) {
+extern "C" int dicp_lddmm_euler_step_zs_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                            int64_t nrows, int D, double sigma, double eta, double dt,
+                                            const int32_t* row_order, float* q_next, float* p_next,
+                                            float* g, float* zs, void* ws, size_t ws_bytes,
+                                            dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // p_next may be NULL: the momenta update is not wanted (the packed pass skips its Gs' / Hs /
-  // GL' sums)
+  // GL' sums); zs may be NULL (no divergence rows)
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
       (nrows > 0 && (!q || !p || !q_next)) || !(sigma > 0) ||
-      (nrows > 0 && (q_next == q || q_next == p || (p_next && (p_next == q || p_next == p))))) {
+      (nrows > 0 && (q_next == q || q_next == p || (p_next && (p_next == q || p_next == p)) ||
+                     (zs && (zs == q || zs == p || zs == q_next || zs == p_next))))) {
     set_error("dicp_lddmm_euler_step_ord_f32: invalid arguments (outputs must not alias inputs)");
     return DICP_ERR_INVALID;
   }
@@ -669,9 +713,39 @@ extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int
   o.base[1] = p + row0 * D;
   o.alpha[0] = o.alpha[1] = (float)dt;
   switch (D) {
-    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows, row_order);
-    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows, row_order);
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows, row_order, zs);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, o, ws, ws_bytes, st, row0, nrows, row_order, zs);
     default: set_error("euler_step_ord: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
+extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int64_t M,
+                                             int64_t row0, int64_t nrows, int D, double sigma,
+                                             double eta, double dt, const int32_t* row_order,
+                                             float* q_next, float* p_next, float* g, void* ws,
+                                             size_t ws_bytes, dicp_stream_t stream) {
+  return dicp_lddmm_euler_step_zs_f32(q, p, M, row0, nrows, D, sigma, eta, dt, row_order, q_next, p_next, g,
+                                      nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int dicp_lddmm_ode_self_bwd_part_zs_f32(const float* q, const float* p, const float* gv,
+                                                   const float* gmG, const float* gdiv, int64_t M,
+                                                   int D, double sigma, double eta, int part,
+                                                   int nparts, const float* zs, int64_t zrow0,
+                                                   int64_t znrows, float* gq, float* gp, void* ws,
+                                                   size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || nparts < 1 || part < 0 || part >= nparts ||
+      (M > 0 && (!q || !p || !gv || !gp)) || !(sigma > 0) ||  // gq may be NULL (gp only), gmG NULL = 0
+      (zs && (zrow0 < 0 || znrows < 0 || zrow0 + znrows > M))) {
+    set_error("dicp_lddmm_ode_self_bwd_part_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  if (M == 0) return DICP_OK;
+  switch (D) {
+    case 2: return ode_self_bwd_part_d<2>(q, p, gv, gmG, gdiv, M, sigma, eta, part, nparts, gq, gp, ws, ws_bytes, st, zs, zrow0, znrows);
+    case 3: return ode_self_bwd_part_d<3>(q, p, gv, gmG, gdiv, M, sigma, eta, part, nparts, gq, gp, ws, ws_bytes, st, zs, zrow0, znrows);
+    default: set_error("ode_self_bwd_part: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
 
@@ -680,18 +754,8 @@ extern "C" int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, 
                                                 int D, double sigma, double eta, int part,
                                                 int nparts, float* gq, float* gp, void* ws,
                                                 size_t ws_bytes, dicp_stream_t stream) {
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (M < 0 || nparts < 1 || part < 0 || part >= nparts ||
-      (M > 0 && (!q || !p || !gv || !gp)) || !(sigma > 0)) {  // gq may be NULL (gp only), gmG NULL = 0
-    set_error("dicp_lddmm_ode_self_bwd_part_f32: invalid arguments");
-    return DICP_ERR_INVALID;
-  }
-  if (M == 0) return DICP_OK;
-  switch (D) {
-    case 2: return ode_self_bwd_part_d<2>(q, p, gv, gmG, gdiv, M, sigma, eta, part, nparts, gq, gp, ws, ws_bytes, st);
-    case 3: return ode_self_bwd_part_d<3>(q, p, gv, gmG, gdiv, M, sigma, eta, part, nparts, gq, gp, ws, ws_bytes, st);
-    default: set_error("ode_self_bwd_part: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
-  }
+  return dicp_lddmm_ode_self_bwd_part_zs_f32(q, p, gv, gmG, gdiv, M, D, sigma, eta, part, nparts, nullptr, 0, 0,
+                                             gq, gp, ws, ws_bytes, stream);
 }
 
 // Workspace sizes for the LDDMM entries (the GMM ones live in gmm.hip).

@@ -479,6 +479,22 @@ struct OpOdeSelfFwd {
   }
 };
 
+// OpOdeSelfFwd<D, false, true> whose fourth output is the row's divergence vector in original
+// units, zs_i = sum_j K_ij (q_i - q_j) = Z'_i / alpha (= -sigma^2 GradKRed(q,q)_i), instead of
+// the Hamiltonian row h_i: the per-row sum through which the cotangent of sum_i g_i enters
+// dL/dp of the VJP (gp_i gets -gdiv s zs_i), so the VJP need not re-sum it pair by pair.
+template <int D>
+struct OpOdeSelfFwdZs : OpOdeSelfFwd<D, false, true> {
+  using P = OpOdeSelfFwd<D, false, true>;
+  static constexpr int kOutW[4] = {D, D, 1, D};
+  __device__ static void store(const Scal& sc, const typename P::Row& r, const float* t, float* v) {
+    P::store(sc, r, t, v);
+    const float ia = sc.aux1 / sc.s;  // 1 / alpha
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[2 * D + 1 + d] = ia * t[2 * D + d];
+  }
+};
+
 // -------------------------------------------------------------------------------------
 // VJP of OpOdeSelfFwd (eta = 0): cotangents a = dL/dv, bm = dL/dmG, gam = dL/d(sum g).
 // Row m, column j, z = q_m - q_j (derivation in DESIGN.md; checked against torch autograd

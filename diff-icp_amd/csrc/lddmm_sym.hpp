@@ -682,11 +682,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxW
 // its row slots; (qoff, qstride) = (0, 1) is every slot in slot order.
 // W = 2D: [gp, gq] channels; W = D: gp only (the gp-only VJP, sym_bwd_pk_kernel<D, false>).
 // Null output pointers are skipped (a caller that needs only gp).
+// zs (rows [zr0, zr0 + zn), original units): the forward's divergence rows; the VJP kernel then
+// ran without the divergence cotangent's pair terms (SymBwdPk<., ., ., false>) and their row
+// total, -gam s zs_i (gam = *gdiv), is added here, once per row (row split: by the rank that
+// owns the row's forward slice).
 template <int D, bool kPart, int W = 2 * D>
 __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
                                                         int64_t slot_stride, int64_t M, int nG,
                                                         int L, float s, float alpha, Outs o,
-                                                        int qoff, int qstride) {
+                                                        int qoff, int qstride,
+                                                        const float* __restrict__ zs = nullptr,
+                                                        int64_t zr0 = 0, int64_t zn = 0,
+                                                        const float* __restrict__ gdiv = nullptr) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= M * W) return;
   const int64_t row = e / W;
@@ -725,7 +732,10 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
   }
   if (c < D) {
     const int64_t idx = row * D + c;
-    if (o.ptr[1]) o.ptr[1][idx] = epilogue(o, 1, idx, alpha * acc);
+    float gp = alpha * acc;
+    if (zs != nullptr && row >= zr0 && row < zr0 + zn && gdiv != nullptr)
+      gp = fmaf(-s * gdiv[0], zs[(row - zr0) * D + c], gp);
+    if (o.ptr[1]) o.ptr[1][idx] = epilogue(o, 1, idx, gp);
   } else {
     const int64_t idx = row * D + (c - D);
     if (o.ptr[0]) o.ptr[0][idx] = epilogue(o, 0, idx, s * acc);
@@ -872,17 +882,37 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
   return check_launch("ode_self_bwd(sym eta merge)");
 }
 
-// packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp); GQ = false: gp half only
-template <int D, bool GQ, bool B0>
+// packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp); GQ = false: gp half only; GT =
+// false: without the divergence cotangent's pair terms
+template <int D, bool GQ, bool B0, bool GT>
 __global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                   int64_t slot_stride, int qoff, int qstride);
 
+template <int D, bool GQ, bool B0>
+inline void sym_bwd_pk_launch(bool gt, dim3 grid, hipStream_t st, const Args& a, const Scal& sc, int64_t M,
+                              const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
+  if (gt)
+    sym_bwd_pk_kernel<D, GQ, B0, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+  else
+    sym_bwd_pk_kernel<D, GQ, B0, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+}
+
 // b0: the cotangent on mG (Args r3 / c3) is identically zero -- those pointers are then not
-// read (SymBwdPk<., ., true>, packed kernel only)
+// read (SymBwdPk<., ., true>, packed kernel only).
+// zs (rows [zr0, zr0 + zn)): the forward's divergence rows (OpOdeSelfFwdZs); with them, or
+// without a divergence cotangent (sc.dev0 == NULL: gam = 0), the packed kernels run without
+// the divergence cotangent's pair terms and the merge adds their row totals.
 template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
-                   hipStream_t st, int part = 0, int nparts = 1, bool pk = false, bool b0 = false) {
+                   hipStream_t st, int part = 0, int nparts = 1, bool pk = false, bool b0 = false,
+                   const float* zs = nullptr, int64_t zr0 = 0, int64_t zn = 0) {
   if (M <= 0) return DICP_OK;
+  if (zs != nullptr && !pk) {
+    set_error("ode_self_bwd(sym): divergence rows need the packed kernel (bwd_alg 3)");
+    return DICP_ERR_INVALID;
+  }
+  const bool gt = !(zs != nullptr || sc.dev0 == nullptr);  // pair loop with the gam terms
+  const float* gd = zs != nullptr ? sc.dev0 : nullptr;
   const SymGeom g = sym_geom(M, nparts);
   const size_t need = sym_ws_bytes(M, 2 * D, nparts);
   if (ws == nullptr || wsb < need) {
@@ -899,33 +929,31 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     const int64_t stride1 = M * D;
     const int nq1 = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
     if (nq1 > 0) {
+      const dim3 grid((unsigned)g.Kmax, (unsigned)nq1);
       if (b0)
-        sym_bwd_pk_kernel<D, false, true><<<dim3((unsigned)g.Kmax, (unsigned)nq1), dim3(256), 0, st>>>(
-            a, sc, M, g.nG, g.L, slab, stride1, part, nparts);
+        sym_bwd_pk_launch<D, false, true>(gt, grid, st, a, sc, M, g, slab, stride1, part, nparts);
       else
-        sym_bwd_pk_kernel<D, false, false><<<dim3((unsigned)g.Kmax, (unsigned)nq1), dim3(256), 0, st>>>(
-            a, sc, M, g.nG, g.L, slab, stride1, part, nparts);
+        sym_bwd_pk_launch<D, false, false>(gt, grid, st, a, sc, M, g, slab, stride1, part, nparts);
       int rc = check_launch("ode_self_bwd(sym gp)");
       if (rc) return rc;
     }
     const dim3 mg((unsigned)((M * D + 255) / 256));
     if (nparts > 1)
       sym_merge_kernel<D, true, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
-                                                             part, nparts);
+                                                             part, nparts, zs, zr0, zn, gd);
     else
       sym_merge_kernel<D, false, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
-                                                              0, 1);
+                                                              0, 1, zs, zr0, zn, gd);
     return check_launch("ode_self_bwd(sym gp merge)");
   }
   const int64_t stride = M * 2 * D;
   const int nq_own = part < g.nQ ? (g.nQ - part + nparts - 1) / nparts : 0;
   if (nq_own > 0) {
+    const dim3 grid((unsigned)g.Kmax, (unsigned)nq_own);
     if (pk && b0)
-      sym_bwd_pk_kernel<D, true, true><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
-          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+      sym_bwd_pk_launch<D, true, true>(gt, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else if (pk)
-      sym_bwd_pk_kernel<D, true, false><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
-          a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+      sym_bwd_pk_launch<D, true, false>(gt, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else
       sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
           a, sc, M, g.nG, g.L, slab, stride, part, nparts);
@@ -935,10 +963,10 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   const int64_t n = M * 2 * D;
   if (nparts > 1)
     sym_merge_kernel<D, true><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts);
+        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn, gd);
   else
     sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1);
+        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
   return check_launch("ode_self_bwd(sym merge)");
 }
 

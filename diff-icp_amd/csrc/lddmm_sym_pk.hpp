@@ -16,7 +16,16 @@ namespace dicp {
 // per step remain.
 // B0 = true: the cotangent b on mG is zero (the first adjoint step: the loss does not depend
 // on the final momenta), so db, zb, pp and every cKzb term drop out -- 40 of 60 remain.
-template <int D, bool GQ = true, bool B0 = false>
+// GT = false: the pair loop leaves out the divergence cotangent's gp terms -gt K z' (row side)
+// and +gt K z' (column side): gam = 0 (no cost cotangent), or their row sums are the forward's
+// divergence rows zs, which the merge adds once per row (sym_merge_kernel) -- 6 of the 60
+// packed instructions per step drop; the column contributions of the lane's two rows are then
+// summed by scalar FMAs (DICP_SYMBWD_SCALAR_CT), 6 more packed instructions become 4 scalar
+// ones each.
+#ifndef DICP_SYMBWD_SCALAR_CT
+#define DICP_SYMBWD_SCALAR_CT 1
+#endif
+template <int D, bool GQ = true, bool B0 = false, bool GT = true>
 struct SymBwdPk {
   using S = SymBwd<D>;
   static constexpr int W = GQ ? 2 * D : D;
@@ -109,10 +118,11 @@ struct SymBwdPk {
     const float* aj = rec + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
+      const f2 ka = GT ? pk_fma(splat(-gt), t.z[d], splat(aj[d])) : splat(aj[d]);
       if constexpr (B0)
-        acc[d] = pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]);
+        acc[d] = pk_fma(t.K, ka, acc[d]);
       else
-        acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
+        acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, ka, acc[d]));
       if constexpr (GQ) acc[D + d] = pk_fma(t.K, pk_fma(t.w, t.z[d], -t.u[d]), acc[D + d]);
     }
   }
@@ -124,6 +134,35 @@ struct SymBwdPk {
     shared_terms(prm.c, r, rec, t);
     const float* pj = rec + D;
     const float* aj = rec + 2 * D;
+    if constexpr (!GT) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if constexpr (B0)
+          acc[d] = pk_fma(t.K, splat(aj[d]), acc[d]);
+        else
+          acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, splat(aj[d]), acc[d]));
+#if DICP_SYMBWD_SCALAR_CT
+        float cg = fmaf(t.K.x, r.ia_a[d].x, t.K.y * r.ia_a[d].y);
+        if constexpr (!B0) cg = fmaf(t.cKzb.x, r.p[d].x, fmaf(t.cKzb.y, r.p[d].y, cg));
+        ct[d] = cg;
+#else
+        const f2 cg = B0 ? t.K * r.ia_a[d] : pk_fma(t.cKzb, r.p[d], t.K * r.ia_a[d]);
+        ct[d] = cg.x + cg.y;
+#endif
+        if constexpr (GQ) {
+          const f2 e = pk_fma(t.w, t.z[d], -t.u[d]);
+#if DICP_SYMBWD_SCALAR_CT
+          acc[D + d] = pk_fma(t.K, e, acc[D + d]);
+          ct[D + d] = -fmaf(t.K.x, e.x, t.K.y * e.y);
+#else
+          const f2 Ke = t.K * e;
+          acc[D + d] = acc[D + d] + Ke;
+          ct[D + d] = -(Ke.x + Ke.y);
+#endif
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const f2 tt = pk_fma(splat(gt), t.z[d], r.ia_a[d]);
@@ -310,11 +349,11 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
   }
 }
 
-template <int D, bool GQ, bool B0>
+template <int D, bool GQ, bool B0, bool GT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
-  sym_pk_body<SymBwdPk<D, GQ, B0>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdPk<D, GQ, B0, GT>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 // Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /

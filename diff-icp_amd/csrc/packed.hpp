@@ -21,9 +21,13 @@ __device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
 // G = false: the sums feeding mG only (Gs', and for eta != 0 Hs and GL') are not formed (mG not
 // wanted: the last step of a shooting whose final momenta are not used) -- eta = 0: 7 of the
 // 19 per-pair packed instructions drop; eta != 0: 25 of 39.
-template <int D, bool DIV, bool ETA = false, bool G = true>
+// ZS = true (eta = 0, DIV): the row's Z' sum also goes out, in original units, through the
+// h slot (which an Euler step does not use): zs_i = sum_j K (q_i - q_j) = Z'_i / alpha -- the
+// divergence rows the matching VJP reuses (OpOdeSelfFwdZs, sym_merge_kernel).
+template <int D, bool DIV, bool ETA = false, bool G = true, bool ZS = false>
 struct OpOdeSelfFwdPk {
-  using Base = OpOdeSelfFwd<D, ETA, DIV || ETA>;
+  static_assert(!ZS || (DIV && !ETA), "zs rows: eta = 0 with the divergence sums only");
+  using Base = std::conditional_t<ZS, OpOdeSelfFwdZs<D>, OpOdeSelfFwd<D, ETA, DIV || ETA>>;
   // column splits as the full pass: the same chunk boundaries, hence bitwise the same v / g
   using SplitAs = OpOdeSelfFwdPk<D, DIV, ETA, true>;
   static constexpr int CW4 = Base::CW4;

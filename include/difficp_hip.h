@@ -199,6 +199,47 @@ int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, const float
                                      float* gp, void* ws, size_t ws_bytes, dicp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------
+ * Divergence-row reuse (eta = 0, the hybrid / withlogdet model).  The divergence cotangent
+ * gdiv enters the VJP's dL/dp only through the per-row sums
+ *   zs_i = sum_j K(q_i - q_j) (q_i - q_j)     (= -sigma^2 GradKRed(q,q)_i, kernel.py:142;
+ *                                              g_i = -p_i.zs_i / sigma^2, LDDMM.py:133-138)
+ * (gp_i gets -gdiv zs_i / sigma^2), which the forward pass already forms.  The _zs forms let
+ * the forward write them (original units) and the VJP take them: its pair loop then drops
+ * those terms (the packed symmetric kernel: 90 instead of 120 packed instructions per 4
+ * unordered pairs) and its merge adds -gdiv zs_i / sigma^2 once per row.  Same results as the
+ * plain forms up to fp32 summation order.  No reference counterpart (KeOps autodiff
+ * re-differentiates GradKRed pair by pair).
+ * ---------------------------------------------------------------------------------- */
+
+/* dicp_lddmm_euler_step_ord_f32 that also writes zs (nrows, D) of the slice's rows (NULL: not
+ * formed, = the plain form).  zs needs eta = 0 and the packed ordered forward (fwd_alg 2;
+ * DICP_ERR_INVALID otherwise). */
+int dicp_lddmm_euler_step_zs_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                 int64_t nrows, int D, double sigma, double eta, double dt,
+                                 const int32_t* row_order, float* q_next, float* p_next,
+                                 float* g, float* zs, void* ws, size_t ws_bytes,
+                                 dicp_stream_t stream);
+
+/* dicp_lddmm_euler_adjoint_step_f32 given zs (M, D) of the same q (NULL = the plain form).
+ * zs needs eta = 0 and the packed symmetric VJP (bwd_alg 3, or lp = NULL). */
+int dicp_lddmm_euler_adjoint_step_zs_f32(const float* q, const float* p, const float* lq,
+                                         const float* lp, const float* gdiv, int64_t M, int D,
+                                         double sigma, double eta, double dt, const float* addq,
+                                         const float* addp, const float* zs, float* lq_next,
+                                         float* lp_next, void* ws, size_t ws_bytes,
+                                         dicp_stream_t stream);
+
+/* dicp_lddmm_ode_self_bwd_part_f32 given the zs rows [zrow0, zrow0 + znrows) (a rank's forward
+ * slice; NULL = the plain form): part `part` adds their -gdiv zs_i / sigma^2 term, so every
+ * row's term is added once over the parts when the ranks' slices tile 0..M-1. */
+int dicp_lddmm_ode_self_bwd_part_zs_f32(const float* q, const float* p, const float* gv,
+                                        const float* gmG, const float* gdiv, int64_t M, int D,
+                                        double sigma, double eta, int part, int nparts,
+                                        const float* zs, int64_t zrow0, int64_t znrows, float* gq,
+                                        float* gp, void* ws, size_t ws_bytes,
+                                        dicp_stream_t stream);
+
+/* ------------------------------------------------------------------------------------
  * GMM EM step reductions (GaussianMixtureUnif.EM_step_torch, GMM.py:236-325).
  * log2-domain internally; outputs in natural log.
  * ---------------------------------------------------------------------------------- */

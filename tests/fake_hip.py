@@ -95,8 +95,18 @@ def ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta):
     return _out(gq, q), _out(gp, q)
 
 
+def _zs_rows(q, row0, nrows, sigma, zs_out):
+    """divergence rows zs_i = sum_j K (q_i - q_j) = -sigma^2 GradKRed(q, q)_i of rows
+    [row0, row0 + nrows), into zs_out"""
+    Q = _d(q)
+    zs_out.copy_(-sigma ** 2 * R.GradKRed(Q[row0:row0 + nrows], Q, sigma))
+
+
 def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=None, order=None,
-               want_p=True):
+               want_p=True, zs_out=None):
+    if zs_out is not None:
+        assert eta == 0
+        _zs_rows(q, 0, q.shape[0], sigma, zs_out)
     v, mG, g, _ = ode_self_fwd(q, p, sigma, eta, want_div)
     if not want_p:   # like the device pass: p_next is not formed
         p_out = None
@@ -113,7 +123,12 @@ def euler_step(q, p, sigma, eta, dt, want_div, q_out=None, p_out=None, g_out=Non
     return qn, (pn if want_p else None), g
 
 
-def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None, want_lq=True):
+def euler_adjoint_step(q, p, lq, lp, gdiv, sigma, eta, dt, addq=None, addp=None, want_lq=True,
+                       zs=None):
+    if zs is not None:   # the divergence rows must be those of q (the device VJP trusts them)
+        ref = torch.empty_like(zs)
+        _zs_rows(q, 0, q.shape[0], sigma, ref)
+        assert torch.allclose(zs, ref, rtol=1e-5, atol=1e-6)
     if lp is None:   # zero momentum cotangent
         lp = torch.zeros_like(lq)
     gq, gp = ode_self_bwd(q, p, lq, lp, gdiv, sigma, eta)
@@ -213,15 +228,22 @@ def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False, ord
 
 
 def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_out=None, order=None,
-                    want_p=True):
+                    want_p=True, zs_out=None):
+    if zs_out is not None:
+        assert eta == 0
+        _zs_rows(q, row0, nrows, sigma, zs_out)
     v, mG, g, _ = ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div)
     sl = slice(row0, row0 + nrows)
     return q[sl] + dt * v, (p[sl] + dt * mG if want_p else None), g
 
 
-def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True):
+def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True, zs=None, zrow0=0):
     """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
     its rows, zeros elsewhere; the sum over parts is the VJP."""
+    if zs is not None:   # the rank's own forward slice of the divergence rows
+        ref = torch.empty_like(zs)
+        _zs_rows(q, zrow0, zs.shape[0], sigma, ref)
+        assert torch.allclose(zs, ref, rtol=1e-5, atol=1e-6)
     if gmG is None:   # zero momentum cotangent
         gmG = torch.zeros_like(gv)
     gq, gp = ode_self_bwd(q, p, gv, gmG, gdiv, sigma, eta)
