@@ -665,10 +665,11 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
 
 
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, nparts: int,
-                      want_gq: bool = True, zs=None, zrow0: int = 0):
+                      want_gq: bool = True, zs=None, zrow0: int = 0, gq_out=None, gp_out=None):
     """Part `part` of `nparts` of ode_self_bwd (dicp_lddmm_ode_self_bwd_part_zs_f32): (gq, gp)
     over a pair subset; the sum over the parts is the full VJP.  want_gq=False: (None, gp).
-    zs: the forward's divergence rows of rows [zrow0, zrow0 + len(zs)) (this rank's slice)."""
+    zs: the forward's divergence rows of rows [zrow0, zrow0 + len(zs)) (this rank's slice).
+    gq_out / gp_out: optional contiguous (M, D) destinations."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     gv = _dev(gv, "gv")
@@ -681,8 +682,9 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
     if zs is not None:
         zn = int(zs.shape[0])
         zs = _zs_buf(zs, zn, D, q.device, "zs")
-    gq = torch.empty_like(q) if want_gq else None
-    gp = torch.empty_like(q)
+    gq = (torch.empty_like(q) if gq_out is None else _zs_buf(gq_out, M, D, q.device, "gq_out")) \
+        if want_gq else None
+    gp = torch.empty_like(q) if gp_out is None else _zs_buf(gp_out, M, D, q.device, "gp_out")
     if M == 0:
         return gq, gp
     ws, nb = _workspace(WS_ODE_SELF_BWD_PART, M, nparts, D, q.device)

@@ -60,6 +60,19 @@ class RowSplit:
             dist.all_gather(list(out.chunk(self.world)), local, group=self.group)
         return out
 
+    def gather_into(self, out: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
+        """All-gather the ranks' equal-sized contiguous `local` slices straight into the
+        contiguous `out` (W x local.numel() elements, rank order): no staging buffer, no
+        copies (the row slices of a step when W divides M)."""
+        flat = out.view(-1)
+        if flat.numel() != self.world * local.numel():
+            raise ValueError("gather_into: out must hold W x local elements")
+        if self._gather_base:
+            dist.all_gather_into_tensor(flat, local.reshape(-1), group=self.group)
+        else:
+            dist.all_gather(list(flat.chunk(self.world)), local.reshape(-1), group=self.group)
+        return out
+
     def sum_ordered(self, t: torch.Tensor) -> torch.Tensor:
         """Cross-rank sum as all-gather + a sum in rank order: the same bits on every rank
         whatever algorithm the backend picks (used for the small (H0, div) scalars and, with

@@ -268,10 +268,34 @@ class ShootFn(torch.autograd.Function):
         if use_zs:
             zrows = split.rows(M)[1] if split is not None else M
             Zs = torch.empty((nt, zrows, D), device=dev, dtype=q0.dtype)   # Zs[0] is not formed
+        # row split with W | M: the fused steps write this rank's rows into send buffers and
+        # the all-gathers land straight in Q[t+1] / P[t+1]; the divergence partials are kept
+        # per step and exchanged once after the loop (rank-ordered, as the staged path)
+        direct = split is not None and M % split.world == 0
+        if direct:
+            n_l = M // split.world
+            qs_l = torch.empty((n_l, D), device=dev, dtype=q0.dtype)
+            ps_l = torch.empty((n_l, D), device=dev, dtype=q0.dtype)
+            dloc = torch.zeros(nt, device=dev, dtype=q0.dtype)
         for t in range(nt):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
             first = t == 0
+            if split is not None and direct and not first:
+                r0, n, _ = split.rows(M)
+                last_skip = skip and t == nt - 1
+                _, _, g_l = _lib.euler_step_rows(q, p, r0, n, sigma, eta, dt, want_div, q_out=qs_l,
+                                                 p_out=None if last_skip else ps_l, order=order_l,
+                                                 want_p=not last_skip,
+                                                 zs_out=None if Zs is None else Zs[t])
+                split.gather_into(Q[t + 1], qs_l)
+                if last_skip:
+                    P[t + 1].fill_(float("nan"))   # not formed: make any read loud
+                else:
+                    split.gather_into(P[t + 1], ps_l)
+                if g_l is not None:
+                    torch.sum(g_l, 0, keepdim=True, out=dloc[t:t + 1])
+                continue
             if split is not None:
                 r0, n, _ = split.rows(M)
                 if first:
@@ -356,6 +380,15 @@ class ShootFn(torch.autograd.Function):
                 if has_x:
                     X[t + 1].copy_(x + (0.25 * dt) * (vx + 3.0 * vx2))
                 mids.append((qi, pi, xi))
+        if direct and nt > 1:
+            # cost of the steps t >= 1: their divergence partials summed in rank order (one
+            # all-gather), then C[t+1] = C[t] + dt div_t as the staged path
+            if want_div:
+                divs = split.sum_ordered(dloc[1:])
+                for t in range(1, nt):
+                    torch.add(C[t], divs[t - 1:t], alpha=dt, out=C[t + 1])
+            else:
+                C[2:].copy_(C[1].expand(nt - 1, 1))
         if fused_from is not None:
             # cost of the fused steps: C[t+1] = C[t] + dt sum_i g_i(t), one reduction + scan
             if want_div:
@@ -427,13 +460,16 @@ class ShootFn(torch.autograd.Function):
                 # the last step needs gp only when q0 needs no gradient (half the bytes too)
                 want_lq = t > 0 or ctx.needs_input_grad[0]
                 zs_t = Zs[t] if (Zs is not None and t >= 1) else None
+                g2 = torch.empty((2, M, D), device=dev, dtype=Q.dtype) if want_lq else None
                 gq_l, gp_l = _lib.ode_self_bwd_part(q, p, lq, lp, lc if want_div else None, sigma,
                                                     eta, split.rank, split.world, want_gq=want_lq,
-                                                    zs=zs_t, zrow0=split.rows(M)[0])
+                                                    zs=zs_t, zrow0=split.rows(M)[0],
+                                                    gq_out=None if g2 is None else g2[0],
+                                                    gp_out=None if g2 is None else g2[1])
                 if want_lq:
-                    g = split.all_reduce_(torch.cat([gq_l, gp_l], 1))
-                    lq = torch.add(lq, g[:, :D], alpha=dt)
-                    lp = g[:, D:].mul(dt) if lp is None else torch.add(lp, g[:, D:], alpha=dt)
+                    g = split.all_reduce_(g2)   # (gq, gp) parts written side by side: no cat
+                    lq = torch.add(lq, g[0], alpha=dt)
+                    lp = g[1].mul(dt) if lp is None else torch.add(lp, g[1], alpha=dt)
                 else:
                     gp_r = split.all_reduce_(gp_l)
                     lp = gp_r.mul_(dt) if lp is None else torch.add(lp, gp_r, alpha=dt)

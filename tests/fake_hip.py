@@ -234,10 +234,16 @@ def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_o
         _zs_rows(q, row0, nrows, sigma, zs_out)
     v, mG, g, _ = ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div)
     sl = slice(row0, row0 + nrows)
-    return q[sl] + dt * v, (p[sl] + dt * mG if want_p else None), g
+    qn, pn = q[sl] + dt * v, (p[sl] + dt * mG if want_p else None)
+    if q_out is not None:
+        qn = q_out.copy_(qn)
+    if p_out is not None and want_p:
+        pn = p_out.copy_(pn)
+    return qn, pn, g
 
 
-def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True, zs=None, zrow0=0):
+def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True, zs=None, zrow0=0,
+                      gq_out=None, gp_out=None):
     """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
     its rows, zeros elsewhere; the sum over parts is the VJP."""
     if zs is not None:   # the rank's own forward slice of the divergence rows
@@ -252,7 +258,12 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=Tru
     r0, r1 = min(per * part, M), min(per * part + per, M)
     mask = torch.zeros(M, 1, dtype=gq.dtype)
     mask[r0:r1] = 1
-    return (gq * mask if want_gq else None), gp * mask
+    gq, gp = gq * mask, gp * mask
+    if gq_out is not None and want_gq:
+        gq = gq_out.copy_(gq)
+    if gp_out is not None:
+        gp = gp_out.copy_(gp)
+    return (gq if want_gq else None), gp
 
 
 _ENTRIES = ("ode_self_fwd_rows", "euler_step_rows", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
