@@ -57,6 +57,8 @@ _SIGNATURES = {
                                       _P, _SZ, _P],
     "dicp_lddmm_ode_self_bwd_part_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _INT, _INT, _P,
                                          _P, _P, _SZ, _P],
+    "dicp_lddmm_ode_self_fwd_zs_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
+                                       _P, _SZ, _P],
     "dicp_lddmm_euler_step_zs_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P, _P,
                                      _P, _P, _SZ, _P],
     "dicp_lddmm_euler_adjoint_step_zs_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P,
@@ -331,14 +333,20 @@ def radius_count(x, y, R: float):
 # ---------------------------------------------------------------------------------------
 # Fused LDDMM ODE
 # ---------------------------------------------------------------------------------------
-def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = False, order=None):
+def ode_self_fwd(q, p, sigma: float, eta: float, want_div: bool, want_h: bool = False, order=None,
+                 zs_out=None):
     """(v, mG, g rows, h rows) of the fused ODE (dicp_lddmm_ode_self_fwd_ord_f32); order: optional
-    int32 row visit order (spatial grouping for the matrix-core forward, see spatial_order)."""
+    int32 row visit order (spatial grouping for the matrix-core forward, see spatial_order);
+    zs_out: (M, D) divergence rows instead of h (dicp_lddmm_ode_self_fwd_zs_f32, eta = 0)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
     order = _order(order, M, dev)
+    if zs_out is not None:
+        if want_h:
+            raise ValueError("ode_self_fwd: zs_out replaces h (want_h must be False)")
+        return ode_self_fwd_rows(q, p, 0, M, sigma, eta, want_div, order=order, zs_out=zs_out)
     v = torch.empty_like(q)
     mG = torch.empty_like(q)
     g = torch.empty(M, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
@@ -605,15 +613,33 @@ def kernel_ridge_cg(x, v, sigma: float, alpha: float, eps: float = 1e-6, maxiter
 # Row-split of one frame over ranks (core/rowsplit.py)
 # ---------------------------------------------------------------------------------------
 def ode_self_fwd_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, want_div: bool,
-                      want_h: bool = False, order=None):
+                      want_h: bool = False, order=None, zs_out=None):
     """Rows [row0, row0 + nrows) of ode_self_fwd against all columns
     (dicp_lddmm_ode_self_fwd_ord_f32).  Returns (v, mG, g, h) for the slice; order: optional
-    int32 visit order of the slice's rows (indices into the slice)."""
+    int32 visit order of the slice's rows (indices into the slice); zs_out: (nrows, D)
+    divergence rows instead of h (dicp_lddmm_ode_self_fwd_zs_f32; h is then None)."""
     q = _dev(q, "q")
     p = _dev(p, "p")
     M, D = q.shape
     dev = q.device
     order = _order(order, nrows, dev)
+    if zs_out is not None:
+        if want_h:
+            raise ValueError("ode_self_fwd_rows: zs_out replaces h (want_h must be False)")
+        zs_out = _zs_buf(zs_out, nrows, D, dev)
+        v = torch.empty((nrows, D), device=dev, dtype=torch.float32)
+        mG = torch.empty_like(v)
+        g = torch.empty(nrows, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None
+        if nrows == 0:
+            return v, mG, g, None
+        ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, M, D, dev)
+        rc = _launch("ode_self_fwd", nrows * M, 4 * (nrows * (3 * D + 1) + 2 * M * D),
+                     lambda: lib().dicp_lddmm_ode_self_fwd_zs_f32(_ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                                                                  float(sigma), float(eta), _ptr(order), _ptr(v),
+                                                                  _ptr(mG), _ptr(g), _ptr(zs_out), _ptr(ws), nb,
+                                                                  _stream(dev)))
+        _check_rc(rc, "ode_self_fwd_zs")
+        return v, mG, g, None
     v = torch.empty((nrows, D), device=dev, dtype=torch.float32)
     mG = torch.empty_like(v)
     g = torch.empty(nrows, device=dev, dtype=torch.float32) if (want_div or eta != 0) else None

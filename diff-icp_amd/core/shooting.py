@@ -147,6 +147,12 @@ class ShootCache:
             self._d.clear()
 
 
+def _h_rows(p, v):
+    """Rows of the Hamiltonian at eta = 0, h_i = p_i.v_i / 2 (LDDMM.py:150-155), from the
+    forward's v (when its h slot carried the divergence rows)."""
+    return 0.5 * (p * v).sum(1)
+
+
 def _f_self(q, p, sigma, eta, want_div, want_h=False, order=None):
     """ODE right-hand side at the support points: (v, mG, div[1]) [+ per-row h]."""
     v, mG, g, h = _lib.ode_self_fwd(q, p, sigma, eta, want_div, want_h=want_h, order=order)
@@ -267,7 +273,7 @@ class ShootFn(torch.autograd.Function):
         Zs = None
         if use_zs:
             zrows = split.rows(M)[1] if split is not None else M
-            Zs = torch.empty((nt, zrows, D), device=dev, dtype=q0.dtype)   # Zs[0] is not formed
+            Zs = torch.empty((nt, zrows, D), device=dev, dtype=q0.dtype)
         # row split with W | M: the fused steps write this rank's rows into send buffers and
         # the all-gathers land straight in Q[t+1] / P[t+1]; the divergence partials are kept
         # per step and exchanged once after the loop (rank-ordered, as the staged path)
@@ -299,8 +305,13 @@ class ShootFn(torch.autograd.Function):
             if split is not None:
                 r0, n, _ = split.rows(M)
                 if first:
-                    v_l, mG_l, g_l, h_l = _lib.ode_self_fwd_rows(q, p, r0, n, sigma, eta, want_div,
-                                                                 want_h=True, order=order_l)
+                    if Zs is not None:   # zs in h's slot: H's rows as p.v / 2 (the kernel's h)
+                        v_l, mG_l, g_l, _ = _lib.ode_self_fwd_rows(q, p, r0, n, sigma, eta, want_div,
+                                                                   order=order_l, zs_out=Zs[0])
+                        h_l = _h_rows(p[r0:r0 + n], v_l)
+                    else:
+                        v_l, mG_l, g_l, h_l = _lib.ode_self_fwd_rows(q, p, r0, n, sigma, eta, want_div,
+                                                                     want_h=True, order=order_l)
                     loc = torch.stack([h_l.sum(), g_l.sum() if g_l is not None else h_l.sum() * 0])
                     (v0, mG0), _ = split.gather_rows([v_l, mG_l], M)
                     sums = split.sum_ordered(loc)   # (H0, div): rank-ordered, same bits everywhere
@@ -346,6 +357,11 @@ class ShootFn(torch.autograd.Function):
             if has_x:
                 out = _f_ext(q, p, x, sigma, eta, want_div, want_h=first, order=order)
                 v, mG, div, vx = out[:4]
+            elif first and Zs is not None:
+                v, mG, g, _ = _lib.ode_self_fwd(q, p, sigma, eta, want_div, order=order, zs_out=Zs[0])
+                div = g.sum().reshape(1)
+                out = (v, mG, div, _h_rows(p, v))
+                vx = None
             else:
                 out = _f_self(q, p, sigma, eta, want_div, want_h=first, order=order)
                 v, mG, div = out[:3]
@@ -459,7 +475,7 @@ class ShootFn(torch.autograd.Function):
                 # this rank's part of the pair-once VJP, summed over ranks (one all-reduce);
                 # the last step needs gp only when q0 needs no gradient (half the bytes too)
                 want_lq = t > 0 or ctx.needs_input_grad[0]
-                zs_t = Zs[t] if (Zs is not None and t >= 1) else None
+                zs_t = None if Zs is None else Zs[t]
                 g2 = torch.empty((2, M, D), device=dev, dtype=Q.dtype) if want_lq else None
                 gq_l, gp_l = _lib.ode_self_bwd_part(q, p, lq, lp, lc if want_div else None, sigma,
                                                     eta, split.rank, split.world, want_gq=want_lq,
@@ -493,7 +509,7 @@ class ShootFn(torch.autograd.Function):
                 lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lct if want_div else None, sigma, eta,
                                                  dt, None if gQ is None else gQ[t],
                                                  None if gP is None else gP[t], want_lq=want_lq,
-                                                 zs=Zs[t] if (Zs is not None and t >= 1) else None)
+                                                 zs=None if Zs is None else Zs[t])
                 if gC is not None:
                     lc = lc_suffix[t]
                 continue

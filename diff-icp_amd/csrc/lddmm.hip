@@ -673,6 +673,24 @@ extern "C" int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, in
 
 // Ordered forms (rows [row0, row0 + nrows) visited in row_order, or NULL = natural order):
 // the general entry points behind the four above.
+extern "C" int dicp_lddmm_ode_self_fwd_zs_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                              int64_t nrows, int D, double sigma, double eta,
+                                              const int32_t* row_order, float* v, float* mG, float* g,
+                                              float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
+      (nrows > 0 && (!q || !p || !v || !mG || !zs)) || !(sigma > 0)) {
+    set_error("dicp_lddmm_ode_self_fwd_zs_f32: invalid arguments");
+    return DICP_ERR_INVALID;
+  }
+  if (nrows == 0) return DICP_OK;
+  switch (D) {
+    case 2: return ode_self_fwd_d<2>(q, p, M, sigma, eta, make_outs(v, mG, g, nullptr), ws, ws_bytes, st, row0, nrows, row_order, zs);
+    case 3: return ode_self_fwd_d<3>(q, p, M, sigma, eta, make_outs(v, mG, g, nullptr), ws, ws_bytes, st, row0, nrows, row_order, zs);
+    default: set_error("ode_self_fwd_zs: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
 extern "C" int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, int64_t M,
                                                int64_t row0, int64_t nrows, int D, double sigma,
                                                double eta, const int32_t* row_order, float* v,

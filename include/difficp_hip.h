@@ -220,6 +220,14 @@ int dicp_lddmm_euler_step_zs_f32(const float* q, const float* p, int64_t M, int6
                                  float* g, float* zs, void* ws, size_t ws_bytes,
                                  dicp_stream_t stream);
 
+/* dicp_lddmm_ode_self_fwd_ord_f32 with zs (nrows, D) in place of h (the first ODE evaluation of
+ * a shooting: v, mG, g as the plain form, bitwise; H = sum_i p_i.v_i / 2 is then formed by the
+ * caller).  Same requirements as above. */
+int dicp_lddmm_ode_self_fwd_zs_f32(const float* q, const float* p, int64_t M, int64_t row0,
+                                   int64_t nrows, int D, double sigma, double eta,
+                                   const int32_t* row_order, float* v, float* mG, float* g,
+                                   float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream);
+
 /* dicp_lddmm_euler_adjoint_step_f32 given zs (M, D) of the same q (NULL = the plain form).
  * zs needs eta = 0 and the packed symmetric VJP (bwd_alg 3, or lp = NULL). */
 int dicp_lddmm_euler_adjoint_step_zs_f32(const float* q, const float* p, const float* lq,

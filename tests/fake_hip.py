@@ -77,7 +77,10 @@ def _self_terms(q, p, sigma, eta):
     return v, -G, g, h
 
 
-def ode_self_fwd(q, p, sigma, eta, want_div, want_h=False, order=None):
+def ode_self_fwd(q, p, sigma, eta, want_div, want_h=False, order=None, zs_out=None):
+    if zs_out is not None:
+        assert eta == 0 and not want_h
+        _zs_rows(q, 0, q.shape[0], sigma, zs_out)
     v, mG, g, h = _self_terms(_d(q), _d(p), sigma, eta)
     return (_out(v, q), _out(mG, q), _out(g, q) if (want_div or eta != 0) else None,
             _out(h, q) if want_h else None)
@@ -220,7 +223,10 @@ def kernel_ridge_cg(x, v, sigma, alpha, eps=1e-6, maxiter=5000, chunk=32):
     return _out(b, v), {"status": st, "iterations": k, "residual2": 0.0, "threshold": 0.0}
 
 
-def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False, order=None):
+def ode_self_fwd_rows(q, p, row0, nrows, sigma, eta, want_div, want_h=False, order=None, zs_out=None):
+    if zs_out is not None:
+        assert eta == 0 and not want_h
+        _zs_rows(q, row0, nrows, sigma, zs_out)
     v, mG, g, h = ode_self_fwd(q, p, sigma, eta, want_div, want_h)
     sl = slice(row0, row0 + nrows)
     return v[sl].contiguous(), mG[sl].contiguous(), None if g is None else g[sl].contiguous(), \

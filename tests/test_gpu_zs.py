@@ -136,3 +136,21 @@ def test_zs_rejected_where_unsupported(dev):
         L.euler_step(q, p, SIG, 0.02, 0.1, True, zs_out=zs)
     with pytest.raises(RuntimeError):
         L.euler_adjoint_step(q, p, p, p, torch.ones(1, device=dev), SIG, 0.02, 0.1, zs=zs)
+
+
+@pytest.mark.parametrize("M,D", [(1, 3), (300, 2), (20000, 3)])
+def test_first_step_zs(dev, M, D):
+    """dicp_lddmm_ode_self_fwd_zs_f32: v, mG, g bitwise those of the plain pass, zs those of the
+    Euler form, and p.v / 2 the plain pass's h rows (to fp32 rounding)."""
+    L = _lib()
+    q, p, *_ = _case(M, D, 5 * M + D)
+    f = lambda t: t.float().to(dev)
+    zs = torch.empty(M, D, device=dev)
+    v, mG, g, none = L.ode_self_fwd(f(q), f(p), SIG, 0.0, True, zs_out=zs)
+    assert none is None
+    v0, mG0, g0, h0 = L.ode_self_fwd(f(q), f(p), SIG, 0.0, True, want_h=True)
+    assert torch.equal(v, v0) and torch.equal(mG, mG0) and torch.equal(g, g0)
+    zs2 = torch.empty(M, D, device=dev)
+    L.euler_step(f(q), f(p), SIG, 0.0, 0.1, True, zs_out=zs2)
+    assert torch.equal(zs, zs2)
+    assert rel_err(0.5 * (f(p) * v).sum(1), h0) < 1e-6
