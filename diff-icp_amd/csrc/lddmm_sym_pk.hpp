@@ -30,6 +30,26 @@ struct SymBwdPk {
   using S = SymBwd<D>;
   static constexpr int W = GQ ? 2 * D : D;
   static constexpr int kMaxWaves = 4;
+  // LDS record layout (rec_layout): D = 3 puts each D-vector of the record (q', p, a, b, gam p)
+  // in a plane of its own, components x y z, so no broadcast operand sits in a .w slot
+#ifndef DICP_SYMBWD_PK_REC3
+#define DICP_SYMBWD_PK_REC3 1
+#endif
+  static constexpr bool kRec3 = DICP_SYMBWD_PK_REC3 && D == 3;
+  static constexpr int kPlanes = kRec3 ? 5 : S::CW;
+  static constexpr bool kDupW = kRec3;
+  __host__ __device__ static constexpr int slot(int i) { return kRec3 ? (i / 3) * 4 + i % 3 : i; }
+  // the record's floats as broadcast pairs for the packed algebra; with kDupW the z component
+  // of each D-vector is the pair (.z, .w) of its plane -- two registers of one ds_read_b128 --
+  // instead of a splat of .z, which the register allocator materialises with a v_mov
+  __device__ static void colvec(const float* rec, f2* cv) {
+#pragma unroll
+    for (int i = 0; i < 5 * D; ++i) cv[i] = splat(rec[i]);
+    if constexpr (kDupW) {
+#pragma unroll
+      for (int m = 0; m < 5; ++m) cv[3 * m + 2] = f2{rec[3 * m + 2], rec[4 * S::CW + m]};
+    }
+  }
   struct Prm {
     float gt, c;  // gam s1 / alpha, s1 / alpha (SymBwd::Prm)
   };
@@ -54,15 +74,16 @@ struct SymBwdPk {
     f2 z[D], u[D];
     f2 K, w, cKzb;
   };
-  __device__ static void shared_terms(float c, const Row2& r, const float* rec, Shared& t) {
-    const float* pj = rec + D;
-    const float* aj = rec + 2 * D;
-    const float* bj = rec + 3 * D;
-    const float* gpj = rec + 4 * D;
+  __device__ static void shared_terms(float c, const Row2& r, const f2* cv, Shared& t) {
+    const f2* qj = cv;
+    const f2* pj = cv + D;
+    const f2* aj = cv + 2 * D;
+    const f2* bj = cv + 3 * D;
+    const f2* gpj = cv + 4 * D;
     f2 r2 = splat(0.f);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      t.z[d] = r.q[d] - splat(rec[d]);
+      t.z[d] = r.q[d] - qj[d];
       r2 = pk_fma(t.z[d], t.z[d], r2);
     }
     t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
@@ -70,59 +91,61 @@ struct SymBwdPk {
       // b = 0: u = gam (p_i - p_j), zb = 0
       if constexpr (GQ) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) t.u[d] = r.gp[d] - splat(gpj[d]);
+        for (int d = 0; d < D; ++d) t.u[d] = r.gp[d] - gpj[d];
         f2 zu = t.z[0] * t.u[0];
-        f2 iap = pk_fma(r.ia_a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+        f2 iap = pk_fma(r.ia_a[0], pj[0], r.p[0] * aj[0]);
 #pragma unroll
         for (int d = 1; d < D; ++d) {
           zu = pk_fma(t.z[d], t.u[d], zu);
-          iap = pk_fma(r.ia_a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), iap));
+          iap = pk_fma(r.ia_a[d], pj[d], pk_fma(r.p[d], aj[d], iap));
         }
         t.w = pk_fma(splat(kS2), zu, -iap);
       }
       (void)bj;
       (void)c;
     } else if constexpr (GQ) {
-      f2 pp = r.p[0] * splat(pj[0]);
+      f2 pp = r.p[0] * pj[0];
 #pragma unroll
-      for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+      for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], pj[d], pp);
       f2 db[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        db[d] = r.b[d] - splat(bj[d]);
-        t.u[d] = pk_fma(-pp, db[d], r.gp[d] - splat(gpj[d]));
+        db[d] = r.b[d] - bj[d];
+        t.u[d] = pk_fma(-pp, db[d], r.gp[d] - gpj[d]);
       }
       f2 zu = t.z[0] * t.u[0], zb = t.z[0] * db[0];
-      f2 iap = pk_fma(r.ia_a[0], splat(pj[0]), r.p[0] * splat(aj[0]));
+      f2 iap = pk_fma(r.ia_a[0], pj[0], r.p[0] * aj[0]);
 #pragma unroll
       for (int d = 1; d < D; ++d) {
         zu = pk_fma(t.z[d], t.u[d], zu);
         zb = pk_fma(t.z[d], db[d], zb);
-        iap = pk_fma(r.ia_a[d], splat(pj[d]), pk_fma(r.p[d], splat(aj[d]), iap));
+        iap = pk_fma(r.ia_a[d], pj[d], pk_fma(r.p[d], aj[d], iap));
       }
       t.w = pk_fma(splat(kS2), zu, -iap);
       t.cKzb = (splat(c) * zb) * t.K;
     } else {
-      f2 zb = t.z[0] * (r.b[0] - splat(bj[0]));
+      f2 zb = t.z[0] * (r.b[0] - bj[0]);
 #pragma unroll
-      for (int d = 1; d < D; ++d) zb = pk_fma(t.z[d], r.b[d] - splat(bj[d]), zb);
+      for (int d = 1; d < D; ++d) zb = pk_fma(t.z[d], r.b[d] - bj[d], zb);
       t.cKzb = (splat(c) * zb) * t.K;
     }
   }
   // ordered pairs (i, j) of both rows, row side only (diag blocks)
   __device__ static void pair_row(const Prm& prm, const Row2& r, const float* rec, f2* acc) {
     const float gt = prm.gt;
+    f2 cv[5 * D];
+    colvec(rec, cv);
     Shared t;
-    shared_terms(prm.c, r, rec, t);
-    const float* pj = rec + D;
-    const float* aj = rec + 2 * D;
+    shared_terms(prm.c, r, cv, t);
+    const f2* pj = cv + D;
+    const f2* aj = cv + 2 * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const f2 ka = GT ? pk_fma(splat(-gt), t.z[d], splat(aj[d])) : splat(aj[d]);
+      const f2 ka = GT ? pk_fma(splat(-gt), t.z[d], aj[d]) : aj[d];
       if constexpr (B0)
         acc[d] = pk_fma(t.K, ka, acc[d]);
       else
-        acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, ka, acc[d]));
+        acc[d] = pk_fma(t.cKzb, pj[d], pk_fma(t.K, ka, acc[d]));
       if constexpr (GQ) acc[D + d] = pk_fma(t.K, pk_fma(t.w, t.z[d], -t.u[d]), acc[D + d]);
     }
   }
@@ -130,17 +153,19 @@ struct SymBwdPk {
   // into ct (scalars)
   __device__ static void pair_sym(const Prm& prm, const Row2& r, const float* rec, f2* acc, float* ct) {
     const float gt = prm.gt;
+    f2 cv[5 * D];
+    colvec(rec, cv);
     Shared t;
-    shared_terms(prm.c, r, rec, t);
-    const float* pj = rec + D;
-    const float* aj = rec + 2 * D;
+    shared_terms(prm.c, r, cv, t);
+    const f2* pj = cv + D;
+    const f2* aj = cv + 2 * D;
     if constexpr (!GT) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         if constexpr (B0)
-          acc[d] = pk_fma(t.K, splat(aj[d]), acc[d]);
+          acc[d] = pk_fma(t.K, aj[d], acc[d]);
         else
-          acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, splat(aj[d]), acc[d]));
+          acc[d] = pk_fma(t.cKzb, pj[d], pk_fma(t.K, aj[d], acc[d]));
 #if DICP_SYMBWD_SCALAR_CT
         float cg = fmaf(t.K.x, r.ia_a[d].x, t.K.y * r.ia_a[d].y);
         if constexpr (!B0) cg = fmaf(t.cKzb.x, r.p[d].x, fmaf(t.cKzb.y, r.p[d].y, cg));
@@ -167,11 +192,11 @@ struct SymBwdPk {
     for (int d = 0; d < D; ++d) {
       const f2 tt = pk_fma(splat(gt), t.z[d], r.ia_a[d]);
       if constexpr (B0) {
-        acc[d] = pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]);
+        acc[d] = pk_fma(t.K, pk_fma(splat(-gt), t.z[d], aj[d]), acc[d]);
         const f2 cg = t.K * tt;
         ct[d] = cg.x + cg.y;
       } else {
-        acc[d] = pk_fma(t.cKzb, splat(pj[d]), pk_fma(t.K, pk_fma(splat(-gt), t.z[d], splat(aj[d])), acc[d]));
+        acc[d] = pk_fma(t.cKzb, pj[d], pk_fma(t.K, pk_fma(splat(-gt), t.z[d], aj[d]), acc[d]));
         const f2 cg = pk_fma(t.cKzb, r.p[d], t.K * tt);
         ct[d] = cg.x + cg.y;
       }
@@ -185,8 +210,39 @@ struct SymBwdPk {
   }
 };
 
+// LDS layout of the column records in sym_pk_body: record float i lives in plane
+// rec_slot<P>(i) / 4, component rec_slot<P>(i) % 4.  Default: the scalar struct's contiguous
+// float4 planes (S::CW of them); an op may define kPlanes / slot(i) to place its broadcast
+// operands where the packed algebra's op_sel can pick them without a v_mov.
+// kDupW: every plane's .w repeats its .z and is read back as rec[4 S::CW + plane] (see
+// SymBwdPk::colvec).
+template <class P, class = void>
+struct rec_layout {
+  static constexpr int kPlanes = P::S::CW;
+  static constexpr bool kDupW = false;
+  __host__ __device__ static constexpr int slot(int i) { return i; }
+};
+template <class P>
+struct rec_layout<P, std::void_t<decltype(P::kPlanes)>> {
+  static constexpr int kPlanes = P::kPlanes;
+  static constexpr bool kDupW = P::kDupW;
+  __host__ __device__ static constexpr int slot(int i) { return P::slot(i); }
+};
+// live components of plane m (1 + the highest used component, 0 if none)
+template <class P>
+__host__ __device__ constexpr int plane_width(int m) {
+  if (rec_layout<P>::kDupW) return 4;
+  int w = 0;
+  for (int i = 0; i < P::S::kUsed; ++i)
+    if (rec_layout<P>::slot(i) / 4 == m && rec_layout<P>::slot(i) % 4 + 1 > w) w = rec_layout<P>::slot(i) % 4 + 1;
+  return w;
+}
+
 #ifndef DICP_SYMBWD_PK_WMIN
 #define DICP_SYMBWD_PK_WMIN 1
+#endif
+#ifndef DICP_SYMBWD_PK_WMAX
+#define DICP_SYMBWD_PK_WMAX 4
 #endif
 #ifndef DICP_SYMBWD_PK_PREFETCH
 #define DICP_SYMBWD_PK_PREFETCH 0
@@ -202,8 +258,9 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
                                             float* __restrict__ slab, int64_t slot_stride, int qoff,
                                             int qstride) {
   using S = typename P::S;
-  constexpr int CW = S::CW, W = P::W;
-  __shared__ float4 planes[2][CW][kSymG];
+  using LY = rec_layout<P>;
+  constexpr int CW = S::CW, NP = LY::kPlanes, W = P::W;
+  __shared__ float4 planes[2][NP][kSymG];
   __shared__ float colacc[kSymQ][kSymG][W];
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
   const typename P::Prm prm = P::params(a, sc);
@@ -235,34 +292,47 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
   auto stage = [&](int B, int buf) {
     if (tid < kSymG) {
       const int64_t j = (int64_t)B * kSymG + tid;
-      float rec[4 * CW];
+      float rec[4 * CW], ph[4 * NP];
       S::load_col(a, sc, j < M ? j : 0, j < M, rec);
 #pragma unroll
-      for (int m = 0; m < CW; ++m)
-        planes[buf][m][tid] = make_float4(rec[4 * m], rec[4 * m + 1], rec[4 * m + 2], rec[4 * m + 3]);
+      for (int k = 0; k < 4 * NP; ++k) ph[k] = 0.f;
+#pragma unroll
+      for (int i = 0; i < S::kUsed; ++i) ph[LY::slot(i)] = rec[i];
+      if constexpr (LY::kDupW) {
+#pragma unroll
+        for (int m = 0; m < NP; ++m) ph[4 * m + 3] = ph[4 * m + 2];
+      }
+#pragma unroll
+      for (int m = 0; m < NP; ++m)
+        planes[buf][m][tid] = make_float4(ph[4 * m], ph[4 * m + 1], ph[4 * m + 2], ph[4 * m + 3]);
     }
   };
 
   int buf = 0;
   // read a column record: only the S::kUsed live floats (as sym_kernel's ldrec)
   auto ldrec = [&](int col, float* rec) {
-    constexpr int kLast = S::kUsed - 4 * (CW - 1);  // live floats of the last plane (1..4)
+    float ph[4 * NP];
 #pragma unroll
-    for (int m = 0; m < CW; ++m) {
+    for (int m = 0; m < NP; ++m) {
+      const int w = plane_width<P>(m);   // compile-time after unrolling
       const float* src = reinterpret_cast<const float*>(&planes[buf][m][col]);
-      if (m < CW - 1 || kLast == 4) {
+      if (w == 4) {
         const float4 v = *reinterpret_cast<const float4*>(src);
-        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = v.z, rec[4 * m + 3] = v.w;
-      } else if (kLast == 3) {
+        ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = v.z, ph[4 * m + 3] = v.w;
+      } else if (w == 3) {
         const float3 v = *reinterpret_cast<const float3*>(src);
-        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = v.z, rec[4 * m + 3] = 0.f;
-      } else if (kLast == 2) {
+        ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = v.z, ph[4 * m + 3] = 0.f;
+      } else if (w == 2) {
         const float2 v = *reinterpret_cast<const float2*>(src);
-        rec[4 * m] = v.x, rec[4 * m + 1] = v.y, rec[4 * m + 2] = rec[4 * m + 3] = 0.f;
+        ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = ph[4 * m + 3] = 0.f;
       } else {
-        rec[4 * m] = src[0], rec[4 * m + 1] = rec[4 * m + 2] = rec[4 * m + 3] = 0.f;
+        ph[4 * m] = src[0], ph[4 * m + 1] = ph[4 * m + 2] = ph[4 * m + 3] = 0.f;
       }
     }
+#pragma unroll
+    for (int i = 0; i < 4 * CW; ++i) rec[i] = i < S::kUsed ? ph[LY::slot(i)] : 0.f;
+#pragma unroll
+    for (int m = 0; m < NP; ++m) rec[4 * CW + m] = LY::kDupW ? ph[4 * m + 3] : 0.f;
   };
   stage(B0, 0);
   __syncthreads();
@@ -279,11 +349,11 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 #if DICP_SYMBWD_PK_PREFETCH
         // register double-buffer of the column record (as sym_kernel): step k2 + 1's LDS
         // reads are issued before step k2's algebra, so their latency is not exposed
-        float rec[4 * CW];
+        float rec[4 * CW + NP];
         ldrec(h * 64 + (l & 63), rec);
 #pragma unroll DICP_SYMBWD_PK_UNROLL
         for (int k2 = 0; k2 < 64; ++k2) {
-          float nxt[4 * CW];
+          float nxt[4 * CW + NP];
           __builtin_amdgcn_s_waitcnt(kLgkm0);
           ldrec(h * 64 + ((l + k2 + 1) & 63), nxt);  // k2 = 63 wraps to column l: harmless
           __builtin_amdgcn_sched_barrier(0);
@@ -292,13 +362,13 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 #pragma unroll
           for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
 #pragma unroll
-          for (int k = 0; k < 4 * CW; ++k) rec[k] = nxt[k];
+          for (int k = 0; k < 4 * CW + NP; ++k) rec[k] = nxt[k];
         }
 #else
 #pragma unroll DICP_SYMBWD_PK_UNROLL
         for (int k2 = 0; k2 < 64; ++k2) {
           const int col = h * 64 + ((l + k2) & 63);
-          float rec[4 * CW];
+          float rec[4 * CW + NP];
           ldrec(col, rec);
           float ct[W];
           P::pair_sym(prm, row, rec, racc, ct);
@@ -312,15 +382,8 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 #pragma unroll 2
         for (int k2 = 0; k2 < 64; ++k2) {
           const int col = h * 64 + ((l + k2) & 63);
-          float rec[4 * CW];
-#pragma unroll
-          for (int m = 0; m < CW; ++m) {
-            const float4 v = planes[buf][m][col];
-            rec[4 * m] = v.x;
-            rec[4 * m + 1] = v.y;
-            rec[4 * m + 2] = v.z;
-            rec[4 * m + 3] = v.w;
-          }
+          float rec[4 * CW + NP];
+          ldrec(col, rec);
           P::pair_row(prm, row, rec, racc);
         }
       }
@@ -350,7 +413,7 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 }
 
 template <int D, bool GQ, bool B0, bool GT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, 4))) void sym_bwd_pk_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, DICP_SYMBWD_PK_WMAX))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
   sym_pk_body<SymBwdPk<D, GQ, B0, GT>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);

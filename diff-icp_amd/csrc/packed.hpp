@@ -92,8 +92,17 @@ struct OpOdeSelfFwdPk {
   }
 };
 
+// occupancy experiments (tools/ab_libs.py): -DDICP_FWD_PK_WAVES=n asks for n waves per SIMD
+#ifdef DICP_FWD_PK_WAVES
+#define DICP_FWD_PK_ATTR __attribute__((amdgpu_waves_per_eu(DICP_FWD_PK_WAVES, 8)))
+#else
+#define DICP_FWD_PK_ATTR
+#endif
+#ifndef DICP_PK_PAIR_UNROLL
+#define DICP_PK_PAIR_UNROLL DICP_PAIR_UNROLL
+#endif
 template <class Op>
-__global__ __launch_bounds__(kBlock) void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
+__global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
                                                            int64_t chunk, Outs outs) {
   using Base = typename Op::Base;
   constexpr int CW4 = Op::CW4;
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void rowred_pk_kernel(Args args, Scal sc, i
 #pragma unroll
     for (int k = 0; k < NACC; ++k) acc[k] = splat(0.f);
     const float4* tile = lds[buf];
-#pragma unroll DICP_PAIR_UNROLL
+#pragma unroll DICP_PK_PAIR_UNROLL
     for (int t = 0; t < cnt; ++t) {
       float rec[CW4 * 4];
 #pragma unroll

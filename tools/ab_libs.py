@@ -24,7 +24,10 @@ torch.manual_seed(0)
 q = torch.rand(M, 3, device=dev); p = 0.01 * torch.randn(M, 3, device=dev)
 ga = torch.randn(M, 3, device=dev); gb = torch.randn(M, 3, device=dev); gd = torch.ones(1, device=dev)
 w2 = torch.zeros(M, device=dev); mu2 = (q * q).sum(-1)
+zs = torch.empty_like(q)
 fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
+       "step_zs": lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs),
+       "adj_zs": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs),
        "bwd": lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0),
        "estep": lambda: _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True),
        "kred": lambda: _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)}

@@ -1,5 +1,5 @@
 """Launch each hot kernel a few times at the bench's sizes (100k support points, 100k x 100k
-E-step) for rocprofv3 PMC passes, e.g.
+E-step), in the variants the bench's timed steps run, for rocprofv3 PMC passes, e.g.
 
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc -o fetch --output-format csv -- python tools/pmc_probe.py
     rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc -o write --output-format csv -- python tools/pmc_probe.py
@@ -24,9 +24,12 @@ def main():
     gd = torch.ones(1, device=dev)
     mu2 = (q * q).sum(-1)
     w2 = torch.zeros(M, device=dev)
+    zs = torch.empty_like(q)
+    # the variants the bench's timed Euler steps run (shooting.ShootFn, t = 1..nt-2): the fused
+    # forward step writing the divergence rows zs, and the full adjoint step reusing them
     for _ in range(3):
-        _lib.ode_self_fwd(q, p, 0.1, 0.0, True)
-        _lib.ode_self_bwd(q, p, a, a, gd, 0.1, 0.0)
+        _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs)
+        _lib.euler_adjoint_step(q, p, a, a, gd, 0.1, 0.0, 0.1, zs=zs)
         _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True)
     torch.cuda.synchronize()
 
