@@ -1,5 +1,5 @@
 """Row-split of ONE frame over ranks (core/rowsplit.py) on CPU with gloo,
-world sizes 2 and 3 (uneven row slices, padded all-gather).  Kernels are replaced by the
+world sizes 2, 3 and 8 (uneven row slices, padded all-gather; the bench node's 8 ranks).  Kernels are replaced by the
 oracle-backed executable spec (tests/fake_hip.py), so this checks the split / exchange logic
 of the shooting and its adjoint: results must equal the single-process run and be
 bitwise identical on every rank (the replicated L-BFGS must take the same decisions)."""
@@ -84,7 +84,7 @@ def _worker(rank, world, port, q, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "exact"), (3, "verify")])
+@pytest.mark.parametrize("world,mode", [(2, "exact"), (3, "verify"), (8, "verify")])
 def test_rowsplit_matches_single_process(world, mode):
     import numpy as np
     single = {k: v.numpy() for k, v in _run(False).items()}
