@@ -79,7 +79,7 @@ def _worker(rank, world, port, q, K, outliers):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,K,outliers", [(2, 4, False), (3, 2, True)])
+@pytest.mark.parametrize("world,K,outliers", [(2, 4, False), (3, 2, True), (8, 8, True)])
 def test_sharded_atlas_matches_single_process(world, K, outliers):
     import numpy as np
     single = _run(1, 0, None, K, outliers)
