@@ -96,6 +96,41 @@ def cpu_baseline(pair_counts, M_work, budget_s=15.0):
                        "iteration")}
 
 
+def kernel_sum_probe(dev, M, reps=5):
+    """The north_star's "100k x 100k 3D Gaussian kernel sum": KRed (kernel.py:138,
+    X_i = sum_j K(x_i - y_j) b_j) at M x M on this GPU, HIP events on the launch stream, best of
+    `reps`.  Reported beside the compute roofline because the north_star quotes this sum
+    against the HBM roofline: its algorithmic HBM bytes (4 (3M + 6M + 3M)) over the launch are a
+    few GB/s, while the bytes a non-reusing (streaming) evaluation would read, 2 D 4 B per pair,
+    are labelled as "effective pair-stream GB/s" (SURVEY 8(d)), never as HBM."""
+    from difficp_amd import _lib
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.rand(M, 3, generator=g).to(dev)
+    b = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
+    st = torch.cuda.current_stream(dev)
+    _lib.gauss_red(_lib.KRED, x, x, 0.1, b=b)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        _lib.gauss_red(_lib.KRED, x, x, 0.1, b=b)
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    pairs = float(M) * M
+    s = best * 1e-3
+    fl = _lib.FLOPS_PER_PAIR.get("gauss_red", 15)
+    return {"op": "KRed (kernel.py:138) x = y, D = 3, sigma 0.1", "M": M, "ms": round(best, 4),
+            "Tpair_per_s": round(pairs / s / 1e12, 3),
+            "tflops": round(pairs * fl / s / 1e12, 2), "frac_fp32_peak": round(pairs * fl / s / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "alg_hbm_GBps": round(4 * 12 * M / s / 1e9, 3),
+            "effective_pair_stream_GBps": round(pairs * 2 * 3 * 4 / s / 1e9, 1),
+            "note": "compute-bound (15 flop + 1 exp per pair, O(M) bytes): the HBM roofline does not "
+                    "bind; effective pair-stream GB/s = bytes a non-reusing kernel would stream "
+                    "(2 D floats per pair), not HBM traffic"}
+
+
 def load_traffic(kernel_name):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -315,6 +350,12 @@ def _main(out):
                 base = cpu_baseline(pair_counts, min(wl["N"], 50000))
             except Exception as e:  # baseline is informative; never fail the bench on it
                 base = {"error": repr(e)}
+        ksum = None
+        if world == 1 and wl.get("N") == 100000:
+            try:
+                ksum = kernel_sum_probe(dev, wl["N"])
+            except Exception as e:  # informative; never fail the bench on it
+                ksum = {"error": repr(e)}
         tot_ms = sum(v["ms"] for v in summ.values())
         kern_gbps = (round(sum(v["bytes"] for v in summ.values()) / (tot_ms * 1e-3) / 1e9, 3)
                      if tot_ms > 0 else None)
@@ -325,6 +366,7 @@ def _main(out):
             "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": cfg, "roofline": roof, "cpu_baseline": base,
             "kernel_sum_hbm_GBps": kern_gbps,
+            "kernel_sum_100k": ksum,
             "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                             "Gpairs": round(v["pairs"] / 1e9, 3)} for k, v in summ.items()},
         }
