@@ -41,14 +41,20 @@ def main():
         b = torch.randn(M, 3, generator=g).to(dev)
         gd = torch.full((1,), 0.3, device=dev)
         reps = max(2, int(2e10 / (M * M)))
-        full_f = timeit(lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True), reps)
-        full_b = timeit(lambda: _lib.ode_self_bwd(q, p, a, b, gd, 0.1, 0.0), reps)
+        # the variants the timed Euler steps run: forward writing the divergence rows zs, the
+        # adjoint reusing them (shooting.ShootFn)
+        zs = torch.empty_like(q)
+        full_f = timeit(lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs), reps)
+        full_b = timeit(lambda: _lib.euler_adjoint_step(q, p, a, b, gd, 0.1, 0.0, 0.1, zs=zs), reps)
         for W in (2, 4, 8):
             tf, tb = [], []
             for r in range(W):
                 r0, n = rows(M, W, r)
-                tf.append(timeit(lambda: _lib.euler_step_rows(q, p, r0, n, 0.1, 0.0, 0.1, True), reps))
-                tb.append(timeit(lambda: _lib.ode_self_bwd_part(q, p, a, b, gd, 0.1, 0.0, r, W), reps))
+                zl = zs[r0:r0 + n]
+                tf.append(timeit(lambda: _lib.euler_step_rows(q, p, r0, n, 0.1, 0.0, 0.1, True,
+                                                              zs_out=zl), reps))
+                tb.append(timeit(lambda: _lib.ode_self_bwd_part(q, p, a, b, gd, 0.1, 0.0, r, W, zs=zl,
+                                                                zrow0=r0), reps))
             rec = {"M": M, "W": W, "fwd_full_ms": round(full_f, 4), "bwd_full_ms": round(full_b, 4),
                    "fwd_part_max_ms": round(max(tf), 4), "fwd_part_min_ms": round(min(tf), 4),
                    "bwd_part_max_ms": round(max(tb), 4), "bwd_part_min_ms": round(min(tb), 4),
