@@ -1,6 +1,6 @@
 """Headline benchmark: diff-ICP PSR iterations/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload two_set_100k|two_set_50k|two_set_200k|atlas_c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload two_set_100k|two_set_50k|two_set_200k|atlas_c4|c5|c5_alt]
     (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
 
 A "step" is one diff-ICP iteration on the workload -- GMM_opt(max_repeat_GMM=10, tol=1e-3)
@@ -50,6 +50,8 @@ WORKLOADS = {
                               v2p_args={"version": "ridge_keops", "alpha": 1e-3}),
     "atlas_c4": dict(kind="atlas", K_per_rank=4, N=20000, C=512, S=1),
     "c5": dict(kind="atlas", K_per_rank=8, N=7500, C=256, S=4),
+    # SURVEY 8(d) C5, alternative reading: 30k points per structure (120k per frame)
+    "c5_alt": dict(kind="atlas", K_per_rank=8, N=30000, C=256, S=4),
 }
 
 
