@@ -28,6 +28,8 @@ zs = torch.empty_like(q)
 fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
        "step_zs": lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs),
        "adj_zs": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs),
+       "adj_b0": lambda: _lib.euler_adjoint_step(q, p, ga, None, gd, 0.1, 0.0, 0.1, zs=zs),
+       "adj_gp": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, want_lq=False, zs=zs),
        "bwd": lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0),
        "estep": lambda: _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True),
        "kred": lambda: _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)}
