@@ -72,6 +72,7 @@ _SIGNATURES = {
     "dicp_supports_dim": [_INT],
     "dicp_num_splits": [_INT, _I64, _I64],
     "dicp_set_option": [ctypes.c_char_p, _INT],
+    "dicp_get_option": [ctypes.c_char_p, ctypes.POINTER(_INT)],
 }
 _RESTYPES = {"dicp_workspace_bytes": _SZ, "dicp_last_error": ctypes.c_char_p,
              "dicp_version": ctypes.c_char_p}
@@ -114,9 +115,15 @@ def supports_dim(D: int) -> bool:
     return bool(lib().dicp_supports_dim(int(D)))
 
 
-# mirror of the library's algorithm choices that change what an entry accepts (a NULL mG
-# cotangent at eta != 0 needs the packed symmetric VJP, bwd_eta_alg 2 = the library default)
-_OPTIONS = {"bwd_eta_alg": 2, "fwd_alg": 2, "bwd_alg": 3}
+def get_option(name: str) -> int:
+    """The library's current value of a tuning knob (dicp_get_option): the kernel variant an
+    entry point will run is asked from the library, never mirrored on the Python side (a
+    build with other -DDICP_* defaults, or a set_option between a forward and its backward,
+    stays consistent)."""
+    v = _INT(0)
+    _check_rc(lib().dicp_get_option(name.encode(), ctypes.byref(v)), f"get_option({name})")
+    return int(v.value)
+
 
 # divergence-row reuse (dicp_lddmm_*_zs_f32): the forward's per-row sums zs_i = sum_j K z_ij
 # feed the VJP's divergence-cotangent term (env DICP_ZS=0 turns it off, for A/B runs)
@@ -126,7 +133,7 @@ USE_ZS = os.environ.get("DICP_ZS", "1") != "0"
 def zs_ok(eta) -> bool:
     """Whether the fused Euler steps can hand divergence rows from the forward to the VJP
     (eta = 0 with the packed ordered forward and the packed symmetric VJP, the defaults)."""
-    return USE_ZS and eta == 0 and _OPTIONS["fwd_alg"] == 2 and _OPTIONS["bwd_alg"] == 3
+    return USE_ZS and eta == 0 and get_option("fwd_alg") == 2 and get_option("bwd_alg") == 3
 
 
 def _zs_buf(zs, rows, D, dev, name="zs_out"):
@@ -141,14 +148,12 @@ def _zs_buf(zs, rows, D, dev, name="zs_out"):
 def set_option(name: str, value: int):
     """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
     _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")
-    if name in _OPTIONS:
-        _OPTIONS[name] = int(value)
 
 
 def _zero_b_ok(eta) -> bool:
     """Whether a zero mG cotangent may be passed as NULL (the symmetric packed VJPs skip its
     terms); otherwise the caller materialises zeros."""
-    return eta == 0 or _OPTIONS["bwd_eta_alg"] == 2
+    return eta == 0 or get_option("bwd_eta_alg") == 2
 
 
 def _bwd_name(eta, want_gq: bool, zero_b: bool) -> str:

@@ -19,7 +19,7 @@ from ..tools.kernel import GaussKernel, SVDpow
 from ..tools.optim import LBFGS_optimization
 from ..tools.spec import defspec, getspec
 from .shooting import (HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootCache, ShootFn,
-                       complete_p1, skip_p1)
+                       complete_p1, row_order_for, skip_p1)
 
 
 class Shoot(list):
@@ -221,8 +221,14 @@ class LDDMMModel:
     def complete_shoot(self, shoot):
         """Form the final momenta of a shoot made with need_p1=False (no-op otherwise)."""
         if getattr(shoot, "p1_missing", False):
+            # the row visit order the shooting itself used (fwd_alg 3 with row_orders), so the
+            # completed P[nt] is the one a full shooting would have produced
+            split = self._split()
+            order, order_l = row_order_for(getattr(self, "row_orders", None), shoot.Q[0],
+                                           float(self.eta), split, shoot.Q.shape[1])
             complete_p1(shoot.Q, shoot.P, self.Kernel.sigma, float(self.eta),
-                        bool(self.withlogdet), int(self.nt), split=self._split())
+                        bool(self.withlogdet), int(self.nt),
+                        order=order_l if split is not None else order, split=split)
             shoot.p1_missing = False
         return shoot
 

@@ -15,6 +15,7 @@ integrator (up to fp32 rounding); the trajectory (nt+1 states) stays resident in
 from __future__ import annotations
 
 import threading
+from collections import OrderedDict
 
 import torch
 
@@ -50,12 +51,13 @@ def spatial_order(x: torch.Tensor) -> torch.Tensor:
 
 class RowOrderCache:
     """spatial_order of the support points, memoised per tensor (q0 is fixed over an L-BFGS
-    run: every closure reuses the order).  Keyed on (storage pointer, version counter, shape):
-    a stale hit after a free / re-allocation still returns a valid permutation of the same
-    length, so results stay correct (only the grouping could be less compact)."""
+    run: every closure reuses the order).  Keyed on (storage pointer, version counter, shape,
+    slice); each entry holds a strong reference to the keyed tensor, so its storage cannot be
+    freed and handed to another tensor while the entry lives (no stale hit by address reuse).
+    Least-recently-used eviction beyond `maxsize` entries."""
 
     def __init__(self, maxsize=32):
-        self._d = {}
+        self._d = OrderedDict()
         self._lock = threading.Lock()
         self.maxsize = maxsize
 
@@ -69,62 +71,114 @@ class RowOrderCache:
     def __deepcopy__(self, memo):
         return RowOrderCache(self.maxsize)
 
+    def __len__(self):
+        return len(self._d)
+
     def get(self, x: torch.Tensor, row0: int = 0, n: int = None):
         n = x.shape[0] - row0 if n is None else n
         key = (x.data_ptr(), x._version, tuple(x.shape), str(x.device), row0, n)
         with self._lock:
-            o = self._d.get(key)
-        if o is None:
+            e = self._d.get(key)
+            if e is not None:
+                self._d.move_to_end(key)
+        if e is None:
             o = spatial_order(x[row0:row0 + n])
             with self._lock:
-                if len(self._d) >= self.maxsize:
-                    self._d.pop(next(iter(self._d)))
-                self._d[key] = o
-        return o
+                self._d[key] = (x, o)
+                while len(self._d) > self.maxsize:
+                    self._d.popitem(last=False)
+            return o
+        return e[1]
 
 
 # rows per workgroup of the matrix-core forward: at or below it the order cannot matter
 _ORDER_MIN_ROWS = 256
 
 
+def row_order_for(orders, q0, eta, split, M):
+    """The row visit order(s) a shooting of q0 uses: (order of all rows, order of this rank's
+    row slice), either None (no order cache, eta != 0, or too few rows to matter)."""
+    order = order_l = None
+    if orders is not None and eta == 0:
+        if split is not None:
+            r0_, n_, _ = split.rows(M)
+            if n_ > _ORDER_MIN_ROWS:
+                order_l = orders.get(q0, r0_, n_)
+        elif M > _ORDER_MIN_ROWS:
+            order = orders.get(q0)
+    return order, order_l
+
+
+def _nbytes(ts):
+    seen, n = set(), 0
+    for t in ts:
+        if isinstance(t, torch.Tensor):
+            k = (t.untyped_storage().data_ptr(), t.device)
+            if k not in seen:
+                seen.add(k)
+                n += t.untyped_storage().nbytes()
+    return n
+
+
 class ShootCache:
-    """The most recent forward trajectory per support-point tensor q0, to be reused when the
-    same shooting (q0, p0[, x0] and the same model parameters) is asked for again.
+    """Recent forward trajectories keyed by the support-point tensor q0, reused when the same
+    shooting (q0, p0[, x0] and the same model parameters) is asked for again.
 
     Why: DiffPSR.Reg_opt starts every L-BFGS run at the momenta the previous run returned
     (PSR.py:521-569 passes a0[k]); its first closure shoots exactly the trajectory the
     previous run's final shoot computed -- only the data loss changed (new GMM targets), and
     the trajectory does not depend on it.  The kernels are deterministic (no atomics, fixed
     summation order), so a hit returns bitwise the tensors a recomputation would produce;
-    the backward runs the adjoint on them as usual.  One entry per q0 (key: storage pointer,
-    version counter, shape); the inputs are compared bitwise (torch.equal) before reuse."""
+    the backward runs the adjoint on them as usual.
 
-    def __init__(self):
-        self._d = {}
+    Safety: the key is (storage pointer, version counter, shape, device) of q0, and each
+    entry holds a strong reference to that q0, so its storage cannot be freed and reused by a
+    different tensor while the entry lives; before reuse q0, p0 and x0 are compared bitwise
+    (torch.equal) with the cache's own copies of the inputs.  The cache never shares storage
+    with tensors handed to callers (ShootFn returns clones on hits AND misses).  Bounded:
+    least-recently-used eviction beyond `max_entries` entries or `max_bytes` of device memory
+    (one entry per frame is what the Reg_opt reuse needs)."""
+
+    def __init__(self, max_entries=64, max_bytes=8 << 30):
+        self._d = OrderedDict()
         self._lock = threading.Lock()
+        self.max_entries = max_entries
+        self.max_bytes = max_bytes
+        self._bytes = 0
         self.hits = 0
+        self.misses = 0
 
     def __getstate__(self):
-        return {}
+        return {"max_entries": self.max_entries, "max_bytes": self.max_bytes}
 
     def __setstate__(self, state):
-        self.__init__()
+        self.__init__(state.get("max_entries", 64), state.get("max_bytes", 8 << 30))
 
     def __deepcopy__(self, memo):
-        return ShootCache()
+        return ShootCache(self.max_entries, self.max_bytes)
+
+    def __len__(self):
+        return len(self._d)
+
+    @property
+    def nbytes(self):
+        return self._bytes
 
     @staticmethod
     def _key(q0):
         return (q0.data_ptr(), q0._version, tuple(q0.shape), str(q0.device))
 
     def lookup(self, q0, p0, x0, params):
+        key = self._key(q0)
         with self._lock:
-            e = self._d.get(self._key(q0))
-        if e is None or e["params"] != params:
-            return None
-        if not torch.equal(e["p0"], p0):
-            return None
-        if (e["x0"] is None) != (x0 is None) or (x0 is not None and not torch.equal(e["x0"], x0)):
+            e = self._d.get(key)
+            if e is not None:
+                self._d.move_to_end(key)
+        if (e is None or e["params"] != params or not torch.equal(e["q0c"], q0)
+                or not torch.equal(e["p0"], p0)
+                or (e["x0"] is None) != (x0 is None)
+                or (x0 is not None and not torch.equal(e["x0"], x0))):
+            self.misses += 1
             return None
         self.hits += 1
         # the cached tensors may have been produced on another stream (concurrent frames: a
@@ -137,14 +191,25 @@ class ShootCache:
         return e
 
     def store(self, q0, p0, x0, params, outs, saved):
-        e = {"p0": p0.detach().clone(), "x0": None if x0 is None else x0.detach().clone(),
+        e = {"q0": q0, "q0c": outs[0][0], "p0": p0.detach().clone(),
+             "x0": None if x0 is None else x0.detach().clone(),
              "params": params, "outs": outs, "saved": saved}
+        e["nbytes"] = _nbytes(list(outs) + list(saved) + [e["p0"], e["x0"]])
+        key = self._key(q0)
         with self._lock:
-            self._d[self._key(q0)] = e
+            old = self._d.pop(key, None)
+            if old is not None:
+                self._bytes -= old["nbytes"]
+            self._d[key] = e
+            self._bytes += e["nbytes"]
+            while len(self._d) > 1 and (len(self._d) > self.max_entries or self._bytes > self.max_bytes):
+                _, ev = self._d.popitem(last=False)
+                self._bytes -= ev["nbytes"]
 
     def clear(self):
         with self._lock:
             self._d.clear()
+            self._bytes = 0
 
 
 def _h_rows(p, v):
@@ -261,14 +326,7 @@ class ShootFn(torch.autograd.Function):
             X[0].copy_(x0)
         mids = []  # Ralston intermediate states (needed by the adjoint)
         H0 = v0 = mG0 = None
-        order = order_l = None
-        if orders is not None and eta == 0:
-            if split is not None:
-                r0_, n_, _ = split.rows(M)
-                if n_ > _ORDER_MIN_ROWS:
-                    order_l = orders.get(q0, r0_, n_)
-            elif M > _ORDER_MIN_ROWS:
-                order = orders.get(q0)
+        order, order_l = row_order_for(orders, q0, eta, split, M)
         Gd, fused_from = None, None  # fused Euler steps: per-step divergence rows, first step
         Zs = None
         if use_zs:
@@ -427,9 +485,11 @@ class ShootFn(torch.autograd.Function):
         outs = (Q, P, C, X, H0) if has_x else (Q, P, C, H0)
         if cache is not None:
             H0d = H0 if isinstance(H0, torch.Tensor) else torch.as_tensor(H0)
-            cache.store(q0, p0, x0, params, tuple(t.detach() if isinstance(t, torch.Tensor) else t
-                                                  for t in ((Q, P, C, X, H0d) if has_x else (Q, P, C, H0d))),
-                        [t.detach() for t in saved])
+            kept = tuple(t.detach() for t in ((Q, P, C, X, H0d) if has_x else (Q, P, C, H0d)))
+            cache.store(q0, p0, x0, params, kept, [t.detach() for t in saved])
+            # the cache keeps Q, P, ... (and autograd saved them): the caller gets its own
+            # copies, so an in-place write by the caller (complete_shoot) cannot reach them
+            return tuple(t.clone() for t in kept)
         return outs
 
     @staticmethod
@@ -440,6 +500,8 @@ class ShootFn(torch.autograd.Function):
         split = ctx.split
         saved = ctx.saved_tensors
         Zs = saved[-1] if ctx.has_zs else None
+        if Zs is not None and not _lib.zs_ok(eta):
+            Zs = None   # the VJP variant changed since the forward: re-sum the divergence terms
         Q, P, v0, mG0 = saved[:4]
         X = saved[4] if has_x else None
         k = 5 if has_x else 4

@@ -157,6 +157,24 @@ extern "C" int dicp_set_option(const char* name, int value) {
   return DICP_ERR_INVALID;
 }
 
+extern "C" int dicp_get_option(const char* name, int* value) {
+  if (name == nullptr || value == nullptr) {
+    set_error("dicp_get_option: NULL argument");
+    return DICP_ERR_INVALID;
+  }
+  if (!strcmp(name, "split_rounds")) { *value = split_rounds(); return DICP_OK; }
+  if (!strcmp(name, "sym_L")) { *value = sym_L(); return DICP_OK; }
+  if (!strcmp(name, "force_splits")) { *value = force_splits(); return DICP_OK; }
+  if (!strcmp(name, "fwd_alg")) { *value = g_fwd_alg; return DICP_OK; }
+  if (!strcmp(name, "mfma_rmax_x100")) { *value = mfma_rmax_x100(); return DICP_OK; }
+  if (!strcmp(name, "bwd_eta_alg")) { *value = g_bwd_eta_alg; return DICP_OK; }
+  if (!strcmp(name, "bwd_alg")) { *value = g_bwd_alg; return DICP_OK; }
+  if (!strcmp(name, "r_fwd")) { *value = r_fwd(); return DICP_OK; }
+  if (!strcmp(name, "r_bwd")) { *value = r_bwd(); return DICP_OK; }
+  set_error("dicp_get_option: unknown option %s", name);
+  return DICP_ERR_INVALID;
+}
+
 extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float* y, int64_t N,
                                   int D, const float* b, const float* c, double sigma, float* out,
                                   void* ws, size_t ws_bytes, dicp_stream_t stream) {

@@ -330,6 +330,11 @@ int dicp_supports_dim(int D);
  *   "split_rounds", "force_splits", "sym_L"  column-split / symmetric-chunk geometry (0 = auto)
  * Returns DICP_ERR_INVALID for an unknown name or an out-of-range value. */
 int dicp_set_option(const char* name, int value);
+/* Current value of a knob of dicp_set_option (same names; the compile-time defaults until
+ * set), written to *value.  Returns DICP_ERR_INVALID for an unknown name or a NULL value.
+ * No reference counterpart: lets the host binding ask which kernel variant an entry point
+ * will run instead of mirroring the library's defaults. */
+int dicp_get_option(const char* name, int* value);
 /* Number of column splits the library will use for an M x N pass (diagnostics/bench). */
 int dicp_num_splits(int kind, int64_t M, int64_t N);
 

@@ -216,3 +216,15 @@ def test_optimize_final_shoot_complete(dev, version):
     ref = LM.Shoot(q0, p)
     assert torch.equal(shoot.Q, ref.Q) and torch.equal(shoot.P, ref.P)
     assert torch.equal(shoot.C, ref.C)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
+def test_shoot_cache_no_stale_hit_gpu(dev, scheme):
+    """ShootCache on the device (caching allocator: a freed q0's block is handed to the next
+    same-size tensor at once): fresh q0 with equal p0 never hit; a repeated shooting does."""
+    import cache_case
+    from difficp_amd.core.LDDMM import LDDMMModel
+    LM = LDDMMModel(sigma=0.2, D=3, lambd=50.0, version="hybrid", scheme=scheme, nt=5,
+                    spec={"device": dev, "dtype": torch.float32})
+    cache_case.shoot_cache_stale_check(LM, 700, 3, dev)

@@ -5,6 +5,7 @@ of the GPU; the GPU tests pin the kernels."""
 import pytest
 import torch
 
+import cache_case
 import fake_hip
 from conftest import rel_err
 from oracle import torch_ref as R
@@ -339,3 +340,45 @@ def test_optimize_skips_final_momenta_then_completes(fake, version):
     LM.shoot_cache = None
     ref = LM.Shoot(q0, p)
     assert torch.equal(shoot.Q, ref.Q) and torch.equal(shoot.P, ref.P)
+
+
+@pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
+def test_shoot_cache_no_stale_hit_on_reused_address(fake, scheme):
+    """VERDICT r2 / ADVICE: a new q0 at a freed q0's address with equal p0 must not reuse the
+    old trajectory (the cache holds its keyed q0 alive and compares q0 bitwise)."""
+    from difficp_amd.core.LDDMM import LDDMMModel
+    LM = LDDMMModel(sigma=0.3, D=2, lambd=5.0, version="hybrid", scheme=scheme, nt=4, spec=CPU)
+    cache_case.shoot_cache_stale_check(LM, 30, 2, "cpu")
+
+
+def test_shoot_cache_is_bounded(fake):
+    """LRU eviction by entry count and by bytes; entries hold the keyed q0 alive."""
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.shooting import ShootCache
+    LM = LDDMMModel(sigma=0.3, D=2, lambd=5.0, version="hybrid", scheme="Euler", nt=3, spec=CPU)
+    LM.shoot_cache = ShootCache(max_entries=3)
+    keep = [torch.rand(20, 2) for _ in range(5)]
+    for q in keep:
+        LM.Shoot(q, torch.zeros(20, 2))
+    assert len(LM.shoot_cache) == 3
+    LM.Shoot(keep[-1], torch.zeros(20, 2))
+    assert LM.shoot_cache.hits == 1
+    LM.Shoot(keep[0], torch.zeros(20, 2))      # evicted long ago: recomputed
+    assert LM.shoot_cache.hits == 1
+    one = LM.shoot_cache.nbytes / len(LM.shoot_cache)
+    LM.shoot_cache = ShootCache(max_entries=64, max_bytes=int(2.5 * one))
+    for q in keep:
+        LM.Shoot(q, torch.zeros(20, 2))
+    assert len(LM.shoot_cache) == 2 and LM.shoot_cache.nbytes <= 2.5 * one
+
+
+def test_row_order_cache_holds_keyed_tensor():
+    """RowOrderCache entries keep their tensor alive (no address reuse) and are LRU-bounded."""
+    from difficp_amd.core.shooting import RowOrderCache, spatial_order
+    c = RowOrderCache(maxsize=2)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(6):
+        x = torch.rand(400, 3, generator=g)
+        assert torch.equal(c.get(x), spatial_order(x))
+        del x
+    assert len(c) == 2
