@@ -22,7 +22,9 @@ KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRAD
     GRADLAPKSCAL, MIN_SQDIST, MIN_SQDIST_OTHER = range(14)
 # enum dicp_ws_kind
 WS_RED, WS_ODE_SELF_FWD, WS_ODE_SELF_BWD, WS_ODE_EXT_FWD, WS_ODE_EXT_BWD, WS_GMM_ESTEP, \
-    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG, WS_ODE_SELF_FWD_ROWS, WS_ODE_SELF_BWD_PART = range(11)
+    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG, WS_ODE_SELF_FWD_ROWS, WS_ODE_SELF_BWD_PART, WS_GRAD = range(12)
+# enum dicp_grad_kind
+GRAD_HESSW, GRAD_HESSWP, GRAD_ZDOTV, GRAD_HESS3, GRAD_GRADLAP3 = range(5)
 
 _lock = threading.Lock()
 _lib = None
@@ -65,6 +67,7 @@ _SIGNATURES = {
                                              _P, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_bwd_part_zs_f32": [_P, _P, _P, _P, _P, _I64, _INT, _DBL, _DBL, _INT, _INT, _P,
                                             _I64, _I64, _P, _P, _P, _SZ, _P],
+    "dicp_gauss_red_grad_f32": [_INT, _P, _I64, _P, _I64, _INT, _P, _P, _P, _P, _P, _DBL, _P, _P, _SZ, _P],
     "dicp_kernel_ridge_cg_f32": [_P, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _INT, _INT, _P, _SZ, _P],
     "dicp_workspace_bytes": [_INT, _I64, _I64, _INT],
     "dicp_last_error": [],
@@ -312,6 +315,35 @@ def gauss_red(op: int, x, y, sigma: float, b=None, c=None):
                  lambda: lib().dicp_gauss_red_f32(int(op), _ptr(x), M, _ptr(y), N, D, _ptr(b), _ptr(c),
                                   float(sigma), _ptr(out), _ptr(ws), nb, _stream(x.device)))
     _check_rc(rc, f"gauss_red(op={op})")
+    return out
+
+
+def gauss_red_grad(kind: int, x, y, sigma: float, r1=None, r2=None, c1=None, c2=None, cw=None):
+    """One gradient reduction (dicp_gauss_red_grad_f32; include/difficp_hip.h lists the five
+    pair formulas): rows x with optional row vectors r1, r2, columns y with optional column
+    vectors c1, c2 and column scalar cw; None reads as zeros (cw: ones).  Returns (M, D)."""
+    x = _dev(x, "x")
+    y = _dev(y, "y")
+    M, D = x.shape
+    N = y.shape[0]
+    if y.shape[1] != D:
+        raise ValueError("x and y must have the same dimension")
+    r1, r2 = (None if t is None else _dev(t, n) for t, n in ((r1, "r1"), (r2, "r2")))
+    c1, c2 = (None if t is None else _dev(t, n) for t, n in ((c1, "c1"), (c2, "c2")))
+    cw = None if cw is None else _dev(cw, "cw")
+    for t, n, shp in ((r1, "r1", (M, D)), (r2, "r2", (M, D)), (c1, "c1", (N, D)), (c2, "c2", (N, D)),
+                      (cw, "cw", (N,))):
+        if t is not None and tuple(t.shape) != shp:
+            raise ValueError(f"gauss_red_grad: {n} must be shaped {shp}")
+    out = torch.empty((M, D), device=x.device, dtype=torch.float32)
+    if M == 0:
+        return out
+    ws, nb = _workspace(WS_GRAD, M, N, D, x.device)
+    rc = _launch("gauss_red_grad", M * N, 4 * (3 * M * D + 3 * N * D + N),
+                 lambda: lib().dicp_gauss_red_grad_f32(int(kind), _ptr(x), M, _ptr(y), N, D, _ptr(r1), _ptr(r2),
+                                                       _ptr(c1), _ptr(c2), _ptr(cw), float(sigma), _ptr(out),
+                                                       _ptr(ws), nb, _stream(x.device)))
+    _check_rc(rc, f"gauss_red_grad(kind={kind})")
     return out
 
 

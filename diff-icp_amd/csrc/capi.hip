@@ -8,6 +8,7 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D);
 int dicp_lddmm_splits(int kind, int64_t M, int64_t N);
 size_t dicp_gmm_ws(int kind, int64_t M, int64_t N, int D);
 size_t dicp_solve_ws(int kind, int64_t M, int D);
+size_t dicp_grad_ws(int64_t M, int64_t N, int D);
 
 namespace {
 thread_local char g_err[512] = "";
@@ -26,12 +27,14 @@ extern "C" const char* dicp_last_error(void) { return g_err; }
 
 extern "C" const char* dicp_version(void) {
   return "difficp_hip 0.1 (gfx950; ops: gauss_red x13, ode_self fwd/bwd, ode_ext fwd/bwd, "
-         "gmm estep/mstep/targets, kernel ridge CG)";
+         "gmm estep/mstep/targets, kernel ridge CG, reduction gradients x5)";
 }
 
 extern "C" size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D) {
   size_t b = 0;
-  if (kind == DICP_WS_RIDGE_CG)
+  if (kind == DICP_WS_GRAD)
+    b = dicp_grad_ws(M, N, D);
+  else if (kind == DICP_WS_RIDGE_CG)
     b = dicp_solve_ws(kind, M, D);
   else if (kind >= DICP_WS_GMM_ESTEP && kind <= DICP_WS_GMM_TARGETS)
     b = dicp_gmm_ws(kind, M, N, D);

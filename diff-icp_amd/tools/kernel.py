@@ -7,10 +7,11 @@ reached through the C-ABI library (include/difficp_hip.h, dicp_gauss_red_f32).  
 is accepted as an alias of "hip" (this is the backend that replaces KeOps); "torch" is
 mapped to "hip" with a warning -- the product path has no CPU implementation.
 
-Every reduction is differentiable w.r.t. the inputs the LDDMM model differentiates
-(KBase, KRedScal, KRed, GradKRed, LapKRed); the others are forward-only (their backward
-would need third/fourth kernel derivatives that no caller of the reference uses -- the
-LDDMM ODE itself is differentiated through the fused kernels of core/shooting.py).
+Every reduction is differentiable w.r.t. every input, as the reference's are through KeOps /
+torch autodiff: each input gradient is one more tiled HIP reduction (KRed / GradKRed /
+HessKRed forms of the existing pair ops, or the five gradient pair ops of
+dicp_gauss_red_grad_f32 for the second and third kernel derivatives).  The LDDMM ODE itself
+is differentiated through the fused kernels of core/shooting.py.
 """
 from __future__ import annotations
 
@@ -148,21 +149,142 @@ class _LapKRed(torch.autograd.Function):
         return gx, gy, None
 
 
-class _ForwardOnly(torch.autograd.Function):
+# The five reductions below are differentiated by one more tiled row reduction per input
+# gradient (dicp_gauss_red_grad_f32, csrc/grad_ops.hpp; the pair formulas are derived in
+# DESIGN.md section 3): the reference gets these gradients from KeOps / torch autodiff
+# (kernel.py:147-168, :194-207, :284-292).  z = x_i - y_j; g = the output cotangent.
+def _neg(t):
+    return None if t is None else -t
+
+
+class _GradKRedRev(torch.autograd.Function):
+    """Y_j = sum_i gradK(x_i - y_j).d_i  (N,).
+    dx_i = sum_j g_j [s^2 (z.d_i) z - s d_i] K ; dy_j = -g_j sum_i [s^2 (z.d_i) z - s d_i] K ;
+    dd_i = sum_j g_j gradK(z)."""
+
     @staticmethod
-    def forward(ctx, op, name, sigma, x, y, b, c):
-        ctx.name = name
-        return _lib.gauss_red(op, x, y, sigma, b=b, c=c)
+    def forward(ctx, x, y, d, sigma):
+        ctx.sigma = sigma
+        ctx.save_for_backward(x, y, d)
+        return _lib.gauss_red(_lib.GRADK_REV, y, x, sigma, b=d)
 
     @staticmethod
     def backward(ctx, g):
-        raise NotImplementedError(
-            f"{ctx.name}: backward is not provided by the HIP backend (the LDDMM ODE is "
-            "differentiated through the fused kernels of difficp_amd.core.shooting)")
+        x, y, d = ctx.saved_tensors
+        s = ctx.sigma
+        g = g.contiguous()
+        gx = gy = gd = None
+        if ctx.needs_input_grad[0]:
+            gx = _lib.gauss_red_grad(_lib.GRAD_HESSW, x, y, s, r1=d, cw=g)
+        if ctx.needs_input_grad[1]:
+            gy = g[:, None] * _lib.gauss_red_grad(_lib.GRAD_HESSW, y, x, s, c1=d)
+        if ctx.needs_input_grad[2]:
+            gd = _lib.gauss_red(_lib.GRADKSCAL, x, y, s, b=g)
+        return gx, gy, gd, None
 
 
-def _needs_grad(*ts):
-    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+class _DDKRed(torch.autograd.Function):
+    """X_i^d = sum_j -s z^d K b_j^d.  With w = g_i * b_j (elementwise):
+    dx_i = sum_j [s^2 (z.w) z - s w] K ; dy_j = -sum_i [...] ; db_j^d = sum_i s z^d K g_i^d."""
+
+    @staticmethod
+    def forward(ctx, x, y, b, sigma):
+        ctx.sigma = sigma
+        ctx.save_for_backward(x, y, b)
+        return _lib.gauss_red(_lib.DDK, x, y, sigma, b=b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, b = ctx.saved_tensors
+        s = ctx.sigma
+        g = g.contiguous()
+        gx = gy = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = _lib.gauss_red_grad(_lib.GRAD_HESSWP, x, y, s, r1=g, c1=b)
+        if ctx.needs_input_grad[1]:
+            gy = -_lib.gauss_red_grad(_lib.GRAD_HESSWP, y, x, s, r1=b, c1=g)
+        if ctx.needs_input_grad[2]:
+            gb = -_lib.gauss_red(_lib.DDK, y, x, s, b=g)
+        return gx, gy, gb, None
+
+
+class _GenDKRed(torch.autograd.Function):
+    """X_i = sum_j gradK(z) (c_i.b_j).
+    dx_i = sum_j (c_i.b_j) [s^2 (z.g_i) z - s g_i] K ; dy_j = -sum_i (same) ;
+    dc_i = sum_j -s (z.g_i) K b_j ; db_j = sum_i -s (z.g_i) K c_i."""
+
+    @staticmethod
+    def forward(ctx, x, y, b, c, sigma):
+        ctx.sigma = sigma
+        ctx.save_for_backward(x, y, b, c)
+        return _lib.gauss_red(_lib.GENDK, x, y, sigma, b=b, c=c)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, b, c = ctx.saved_tensors
+        s = ctx.sigma
+        g = g.contiguous()
+        gx = gy = gb = gc = None
+        if ctx.needs_input_grad[0]:
+            gx = _lib.gauss_red_grad(_lib.GRAD_HESSW, x, y, s, r1=g, r2=c, c2=b)
+        if ctx.needs_input_grad[1]:
+            gy = _lib.gauss_red_grad(_lib.GRAD_HESSW, y, x, s, c1=g, r2=b, c2=c)
+        if ctx.needs_input_grad[2]:
+            gb = _lib.gauss_red_grad(_lib.GRAD_ZDOTV, y, x, s, c1=_neg(g), c2=c)
+        if ctx.needs_input_grad[3]:
+            gc = _lib.gauss_red_grad(_lib.GRAD_ZDOTV, x, y, s, r1=g, c2=b)
+        return gx, gy, gb, gc, None
+
+
+class _HessKRed(torch.autograd.Function):
+    """X_i = sum_j [s^2 (z.u) z - s u] K, u = c_i - b_j.
+    dx_i = sum_j grad_z{ g_i . [...] K } (third kernel derivative, HESS3) ; dy_j = -sum_i (same);
+    dc_i = sum_j [s^2 (z.g_i) z - s g_i] K ; db_j = -sum_i [...]."""
+
+    @staticmethod
+    def forward(ctx, x, y, b, c, sigma):
+        ctx.sigma = sigma
+        ctx.save_for_backward(x, y, b, c)
+        return _lib.gauss_red(_lib.HESSK, x, y, sigma, b=b, c=c)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y, b, c = ctx.saved_tensors
+        s = ctx.sigma
+        g = g.contiguous()
+        gx = gy = gb = gc = None
+        if ctx.needs_input_grad[0]:
+            gx = _lib.gauss_red_grad(_lib.GRAD_HESS3, x, y, s, r1=c, c1=b, r2=g)
+        if ctx.needs_input_grad[1]:
+            gy = _lib.gauss_red_grad(_lib.GRAD_HESS3, y, x, s, r1=_neg(b), c1=_neg(c), c2=g)
+        if ctx.needs_input_grad[2]:
+            gb = _lib.gauss_red_grad(_lib.GRAD_HESSW, y, x, s, c1=g)
+        if ctx.needs_input_grad[3]:
+            gc = _lib.gauss_red_grad(_lib.GRAD_HESSW, x, y, s, r1=g)
+        return gx, gy, gb, gc, None
+
+
+class _GradLapKRed(torch.autograd.Function):
+    """X_i = sum_j -z (s^3 r2 - (D+2) s^2) K.
+    dx_i = -sum_j K [phi g_i + s^3 (D + 4 - s r2)(g_i.z) z] ; dy_j = -sum_i (same)."""
+
+    @staticmethod
+    def forward(ctx, x, y, sigma):
+        ctx.sigma = sigma
+        ctx.save_for_backward(x, y)
+        return _lib.gauss_red(_lib.GRADLAPK, x, y, sigma)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        s = ctx.sigma
+        g = g.contiguous()
+        gx = gy = None
+        if ctx.needs_input_grad[0]:
+            gx = _lib.gauss_red_grad(_lib.GRAD_GRADLAP3, x, y, s, r1=g)
+        if ctx.needs_input_grad[1]:
+            gy = _lib.gauss_red_grad(_lib.GRAD_GRADLAP3, y, x, s, c1=-g)
+        return gx, gy, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -273,32 +395,31 @@ class GaussKernel(GenKernel):
         getspec(x, y)
         return _GradKRed.apply(x, y, self.sigma)
 
-    def _fwd_only(self, op, name, x, y, b=None, c=None):
-        getspec(x, y, b, c)
-        if _needs_grad(x, y, b, c):
-            return _ForwardOnly.apply(op, name, self.sigma, x, y, b, c)
-        return _lib.gauss_red(op, x, y, self.sigma, b=b, c=c)
-
     def GradKRed_rev_hip(self, x, y, d):
         """Y_j = sum_i sum_d (d_d K)(x_i - y_j) d_i^d, shape (N,) -- column reduction done as
         a row reduction over y (kernel.py:147, :194-195)."""
-        return self._fwd_only(_lib.GRADK_REV, "GradKRed_rev", y, x, b=d)
+        getspec(x, y, d)
+        return _GradKRedRev.apply(x, y, d, self.sigma)
 
     def DDKRed_hip(self, x, y, b):
-        return self._fwd_only(_lib.DDK, "DDKRed", x, y, b=b)
+        getspec(x, y, b)
+        return _DDKRed.apply(x, y, b, self.sigma)
 
     def GenDKRed_hip(self, x, y, b, c):
-        return self._fwd_only(_lib.GENDK, "GenDKRed", x, y, b=b, c=c)
+        getspec(x, y, b, c)
+        return _GenDKRed.apply(x, y, b, c, self.sigma)
 
     def HessKRed_hip(self, x, y, b, c):
-        return self._fwd_only(_lib.HESSK, "HessKRed", x, y, b=b, c=c)
+        getspec(x, y, b, c)
+        return _HessKRed.apply(x, y, b, c, self.sigma)
 
     def LapKRed_hip(self, x, y):
         getspec(x, y)
         return _LapKRed.apply(x, y, self.sigma)
 
     def GradLapKRed_hip(self, x, y):
-        return self._fwd_only(_lib.GRADLAPK, "GradLapKRed", x, y)
+        getspec(x, y)
+        return _GradLapKRed.apply(x, y, self.sigma)
 
     def check_coverage(self, X, Y, Rthreshold):
         """Boolean (N,) mask of points X at distance > Rthreshold*sigma from every Y

@@ -301,6 +301,28 @@ int dicp_kernel_ridge_cg_f32(const float* x, int64_t M, int D, double sigma, dou
                              void* ws, size_t ws_bytes, dicp_stream_t stream);
 
 /* ------------------------------------------------------------------------------------ */
+/* Gradient reductions: the backward passes of GenDKRed, HessKRed, GradLapKRed, DDKRed and
+ * GradKRed_rev, which the reference takes from KeOps / torch autodiff (kernel.py:147-168,
+ * :194-207, :284-292).  Rows x (M, D) with optional row D-vectors r1, r2; columns y (N, D)
+ * with optional column D-vectors c1, c2 and optional column scalar cw (N,).  NULL reads as
+ * zeros (r2 and c2 both NULL: the weight r2.c2 reads as 1; cw NULL reads as 1).
+ * z = x_i - y_j, K = exp(-|z|^2 / (2 sigma^2)), s = 1/sigma^2; out (M, D):
+ *   HESSW    sum_j cw_j (r2_i.c2_j) [s^2 (z.u) z - s u] K,    u = r1_i - c1_j
+ *   HESSWP   sum_j [s^2 (z.u) z - s u] K,                     u = r1_i * c1_j (elementwise)
+ *   ZDOTV    sum_j -s (z.a) K c2_j,                           a = r1_i + c1_j
+ *   HESS3    sum_j K (s^2 [(z.g) u + (z.u) g] - s z [s^2 (z.u)(z.g) - s (u.g)]),
+ *                                                             u = r1_i - c1_j, g = r2_i + c2_j
+ *   GRADLAP3 sum_j -K [(s^3 |z|^2 - (D+2) s^2) g + s^3 (D + 4 - s |z|^2)(g.z) z],  g = r1_i + c1_j
+ * Workspace kind DICP_WS_GRAD. */
+enum dicp_grad_kind {
+  DICP_GRAD_HESSW = 0, DICP_GRAD_HESSWP = 1, DICP_GRAD_ZDOTV = 2, DICP_GRAD_HESS3 = 3,
+  DICP_GRAD_GRADLAP3 = 4
+};
+int dicp_gauss_red_grad_f32(int kind, const float* x, int64_t M, const float* y, int64_t N, int D,
+                            const float* r1, const float* r2, const float* c1, const float* c2,
+                            const float* cw, double sigma, float* out, void* ws, size_t ws_bytes,
+                            dicp_stream_t stream);
+
 /* Scratch bytes needed by entry `kind` (one of the DICP_WS_* below) at these sizes.
  * LDDMM kinds: M = support points, N = columns (RED) or external points (EXT).
  * GMM kinds: M = data points N, N = components C. */
@@ -309,7 +331,8 @@ enum dicp_ws_kind {
   DICP_WS_ODE_EXT_BWD = 4, DICP_WS_GMM_ESTEP = 5, DICP_WS_GMM_MSTEP = 6, DICP_WS_GMM_TARGETS = 7,
   DICP_WS_RIDGE_CG = 8,          /* M = points, N unused */
   DICP_WS_ODE_SELF_FWD_ROWS = 9, /* M = rows of the slice, N = all points (columns) */
-  DICP_WS_ODE_SELF_BWD_PART = 10 /* M = points, N = nparts */
+  DICP_WS_ODE_SELF_BWD_PART = 10, /* M = points, N = nparts */
+  DICP_WS_GRAD = 11              /* dicp_gauss_red_grad_f32: M rows, N columns */
 };
 size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D);
 

@@ -63,6 +63,51 @@ def gauss_red(op, x, y, sigma, b=None, c=None):
     return _out(r, x)
 
 
+def gauss_red_grad(kind, x, y, sigma, r1=None, r2=None, c1=None, c2=None, cw=None):
+    """The five pair formulas of dicp_gauss_red_grad_f32 (include/difficp_hip.h), float64."""
+    from difficp_amd import _lib as L
+    X, Y = _d(x), _d(y)
+    M, D = X.shape
+    N = Y.shape[0]
+    s = 1.0 / sigma ** 2
+    z0 = lambda n: torch.zeros(n, D, dtype=torch.float64)
+    R1 = _d(r1) if r1 is not None else z0(M)
+    C1 = _d(c1) if c1 is not None else z0(N)
+    if kind == L.GRAD_HESSW and r2 is None and c2 is None:
+        R2, C2 = z0(M), z0(N)
+        R2[:, 0] = 1.0
+        C2[:, 0] = 1.0
+    else:
+        R2 = _d(r2) if r2 is not None else z0(M)
+        C2 = _d(c2) if c2 is not None else z0(N)
+    W = _d(cw) if cw is not None else torch.ones(N, dtype=torch.float64)
+    z = X[:, None, :] - Y[None, :, :]
+    r2v = (z * z).sum(-1)
+    K = torch.exp(-0.5 * s * r2v)
+    dot = lambda a, b: (a * b).sum(-1)
+    if kind in (L.GRAD_HESSW, L.GRAD_HESSWP):
+        u = R1[:, None] - C1[None] if kind == L.GRAD_HESSW else R1[:, None] * C1[None]
+        w = K * (W[None] * dot(R2[:, None], C2[None]) if kind == L.GRAD_HESSW else 1.0)
+        out = (w[..., None] * (s * s * dot(z, u)[..., None] * z - s * u)).sum(1)
+    elif kind == L.GRAD_ZDOTV:
+        a = R1[:, None] + C1[None]
+        out = (-s * (K * dot(z, a))[..., None] * C2[None]).sum(1)
+    elif kind == L.GRAD_HESS3:
+        u = R1[:, None] - C1[None]
+        g = R2[:, None] + C2[None]
+        zg, zu, ug = dot(z, g), dot(z, u), dot(u, g)
+        t = s * s * (zg[..., None] * u + zu[..., None] * g) - s * z * (s * s * zu * zg - s * ug)[..., None]
+        out = (K[..., None] * t).sum(1)
+    elif kind == L.GRAD_GRADLAP3:
+        g = R1[:, None] + C1[None]
+        phi = s ** 3 * r2v - (D + 2) * s * s
+        t = phi[..., None] * g + (s ** 3 * (D + 4 - s * r2v) * dot(g, z))[..., None] * z
+        out = -(K[..., None] * t).sum(1)
+    else:
+        raise NotImplementedError(kind)
+    return _out(out, x)
+
+
 def _self_terms(q, p, sigma, eta):
     s = 1.0 / sigma ** 2
     KR = R.KRed(q, q, p, sigma)
@@ -272,7 +317,7 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=Tru
     return (gq if want_gq else None), gp
 
 
-_ENTRIES = ("ode_self_fwd_rows", "euler_step_rows", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+_ENTRIES = ("gauss_red_grad", "ode_self_fwd_rows", "euler_step_rows", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 

@@ -228,3 +228,11 @@ def test_shoot_cache_no_stale_hit_gpu(dev, scheme):
     LM = LDDMMModel(sigma=0.2, D=3, lambd=50.0, version="hybrid", scheme=scheme, nt=5,
                     spec={"device": dev, "dtype": torch.float32})
     cache_case.shoot_cache_stale_check(LM, 700, 3, dev)
+
+
+@pytest.mark.parametrize("D", [2, 3])
+def test_reduction_gradients_gpu(dev, D):
+    """GenDKRed, HessKRed, GradLapKRed, DDKRed, GradKRed_rev differentiable on the device
+    (dicp_gauss_red_grad_f32) w.r.t. every input, against float64 autograd of the oracle."""
+    import grad_case
+    grad_case.check_reduction_grads(dev, D)

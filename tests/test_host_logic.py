@@ -382,3 +382,12 @@ def test_row_order_cache_holds_keyed_tensor():
         assert torch.equal(c.get(x), spatial_order(x))
         del x
     assert len(c) == 2
+
+
+@pytest.mark.parametrize("D", [2, 3])
+def test_reduction_gradients_spec(fake, D):
+    """The gradient wiring of the five reductions that KeOps/torch differentiate in the
+    reference (tools/kernel.py autograd Functions + the pair formulas of
+    dicp_gauss_red_grad_f32 as the CPU spec states them) equals float64 autograd."""
+    import grad_case
+    grad_case.check_reduction_grads("cpu", D, tol_f=1e-6, tol_g=1e-6)
