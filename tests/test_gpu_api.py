@@ -41,8 +41,8 @@ def test_registration_apply_matches_golden_x1(dev):
 @pytest.mark.parametrize("scheme", ["Euler", "Ralston"])
 def test_registration_backward_matches_oracle(dev, version, scheme):
     """backward(Y) = Shoot(q1, -p1, Y)[-1][3] (registrations.py:66-69, 79-87) against the
-    float64 oracle; backward(apply(X)) returns close to X (the flow is reversed up to the
-    integrator's discretisation error)."""
+    float64 oracle; for eta = 0, backward(apply(X)) returns close to X (the flow is reversed up
+    to the integrator's discretisation error)."""
     from difficp_amd.core.LDDMM import LDDMMModel
     from difficp_amd.core.registrations import LDDMMRegistration
     g = torch.Generator().manual_seed(9)
@@ -61,8 +61,12 @@ def test_registration_backward_matches_oracle(dev, version, scheme):
     bw = m.Shoot(fw[-1][0], -fw[-1][1], Y.double().cpu())
     assert rel_err(Y.cpu(), Y64) < 1e-5
     assert rel_err(B.cpu(), bw[-1][3]) < 2e-5
-    disp = float((Y64 - X).norm())
-    assert float((B.double().cpu() - X).norm()) < 0.05 * disp
+    if version != "logdet":
+        # eta = 0: v is odd in p, so shooting from the arrival state with -p1 retraces the
+        # flow; with gradcomponent the -eta GradKRed part of v does not flip (the reference's
+        # backward is then not an inverse) -- only the parity above applies
+        disp = float((Y64 - X).norm())
+        assert float((B.double().cpu() - X).norm()) < 0.05 * disp
     # previous_forwardshoot is reused as given
     sh = reg.shoot(None)
     assert torch.equal(reg.backward(Y, previous_forwardshoot=sh), B)
@@ -97,7 +101,7 @@ def test_v_and_mdivsum_with_autograd(dev, gradcomponent):
         gd64 = torch.autograd.grad(d64, ins64)
         ins = [t.float().to(dev).requires_grad_(True) for t in (x, q, p)]
         d = LM.mdivsum(*ins, rev=rev)
-        assert abs(float(d) - float(d64)) < 1e-5 * abs(float(d64)), rev
+        assert abs(float(d.detach()) - float(d64.detach())) < 1e-5 * abs(float(d64.detach())), rev
         gd = torch.autograd.grad(d, ins)
         for a, b in zip(gd, gd64):
             assert rel_err(a.cpu(), b) < 2e-5, rev
