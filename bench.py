@@ -1,6 +1,7 @@
 """Headline benchmark: diff-ICP PSR iterations/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload two_set_100k|two_set_50k|two_set_200k|atlas_c4|c5|c5_alt]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--workload two_set_100k|two_set_50k|two_set_200k|two_set_50k_exact|atlas_c4|atlas_c4_fixed|c5|c5_alt]
     (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
 
 A "step" is one diff-ICP iteration on the workload -- GMM_opt(max_repeat_GMM=10, tol=1e-3)
@@ -9,7 +10,9 @@ with every point set resident in HBM.  Default workload (the point count BASELIN
 metric names, "100k-pt 3D"; configs[1] is two_set_50k):
 two-point-set 3D match, 100k vs 100k synthetic points, hybrid LDDMM (sigma 0.1, lambda 1e3,
 Euler nt=10, dense support), GMM on xB with sigma optimised.  The atlas workloads shard
-frames over ranks with an RCCL exchange of the GMM sufficient statistics.
+frames over ranks with an RCCL exchange of the GMM sufficient statistics: atlas_c4 / c5 /
+c5_alt keep the frames per rank fixed (weak scaling), atlas_c4_fixed keeps the whole
+32-frame C4 atlas fixed (strong scaling, value = atlas iterations per second).
 
 Rank 0 prints ONE JSON line (value = iterations of all ranks / max-over-ranks time) with a
 "roofline" object for the dominant kernel (algorithmic flop per launch / average launch
@@ -49,6 +52,10 @@ WORKLOADS = {
     "two_set_50k_exact": dict(kind="two_set", N=50000, version="logdet",
                               v2p_args={"version": "ridge_keops", "alpha": 1e-3}),
     "atlas_c4": dict(kind="atlas", K_per_rank=4, N=20000, C=512, S=1),
+    # BASELINE configs[3] as a FIXED workload: 32 frames x 20k whatever the rank count (frames
+    # sharded over the ranks), so the 1 -> 8 GPU lines measure strong scaling of one atlas
+    # (ICP_atlas.py:269-298); value = iterations of the whole 32-frame atlas per second
+    "atlas_c4_fixed": dict(kind="atlas", K_total=32, N=20000, C=512, S=1),
     "c5": dict(kind="atlas", K_per_rank=8, N=7500, C=256, S=4),
     # SURVEY 8(d) C5, alternative reading: 30k points per structure (120k per frame)
     "c5_alt": dict(kind="atlas", K_per_rank=8, N=30000, C=256, S=4),
@@ -59,13 +66,41 @@ def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(pair_counts, M_work, budget_s=15.0):
-    """Time the oracle's C restatement (OpenMP) of the dominant pair kernels on this host on a
-    bounded sample -- repeated ODE-forward / VJP / E-step evaluations at M x M pairs (the
-    workload's size, capped at 50k so one evaluation stays ~1 s) -- then extrapolate to one
+def _pair_kind(name):
+    """CPU-rate class of a live kernel name: the VJP variants (ode_self_bwd*, ode_ext_bwd)
+    are priced at the backward rate, the EM passes at the E-step rate, the rest (forward
+    passes, reductions, CG mat-vecs) at the forward rate."""
+    if name.startswith("ode_self_bwd") or name.startswith("ode_ext_bwd") or name == "gauss_red_grad":
+        return "bwd"
+    if name.startswith("gmm_"):
+        return "em"
+    return "fwd"
+
+
+def _cpu_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+
+
+def _round_robin(calls, budget_s):
+    times = {k: [] for k in calls}
+    t_start = time.perf_counter()
+    while True:  # round-robin until the sample budget is spent (at least one of each)
+        for k, f in calls.items():
+            t0 = time.perf_counter()
+            f()
+            times[k].append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s:
+            break
+    return times, time.perf_counter() - t_start
+
+
+def cpu_baseline_c(pair_counts, M_work, budget_s=15.0):
+    """The oracle's C restatement (OpenMP) of the dominant pair kernels, timed on this host on
+    a bounded sample -- repeated ODE-forward / VJP / E-step evaluations at M x M pairs (the
+    workload's size, capped at 50k so one evaluation stays ~1 s) -- then extrapolated to one
     iteration from the live pair counts (the C kernels' pair rate is flat in M)."""
     from oracle import c_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = _cpu_threads()
     torch.manual_seed(0)
     M = int(M_work)
     q = torch.rand(M, 3)
@@ -76,26 +111,76 @@ def cpu_baseline(pair_counts, M_work, budget_s=15.0):
     calls = {"fwd": lambda: c_ref.ode_self_fwd(q, p, 0.1),
              "bwd": lambda: c_ref.ode_self_bwd(q, p, a, a, 1.0, 0.1),
              "em": lambda: c_ref.gmm_estep(X, X, w0, 0.05)}
-    times = {k: [] for k in calls}
-    t_start = time.perf_counter()
-    while True:  # round-robin until the sample budget is spent (at least one of each)
-        for k, f in calls.items():
-            t0 = time.perf_counter()
-            f()
-            times[k].append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s:
-            break
+    times, took = _round_robin(calls, budget_s)
     rates = {k: M * M / (sum(v) / len(v)) for k, v in times.items()}
-    reps = len(times["fwd"])
-    kind_of = {"ode_self_fwd": "fwd", "ode_self_fwd_eta": "fwd", "ode_ext_fwd": "fwd",
-               "gauss_red": "fwd", "ridge_cg": "fwd", "ode_self_bwd": "bwd", "ode_self_bwd_eta": "bwd", "ode_ext_bwd": "bwd",
-               "gmm_estep": "em", "gmm_mstep": "em", "gmm_targets": "em"}
-    secs = sum(v / rates[kind_of.get(k, "fwd")] for k, v in pair_counts.items())
+    secs = sum(v / rates[_pair_kind(k)] for k, v in pair_counts.items())
     return {"value": 1.0 / secs, "unit": "PSR iterations/sec", "cores": threads, "kind": "port",
-            "sample": (f"oracle/difficp_ref.c (OpenMP, {threads} threads): {reps} x (ODE fwd + VJP + "
-                       f"E-step) at {M}x{M} pairs ({time.perf_counter() - t_start:.1f} s), rates fwd {rates['fwd'] / 1e9:.3f} / bwd {rates['bwd'] / 1e9:.3f} / "
-                       f"EM {rates['em'] / 1e9:.3f} Gpair/s, extrapolated to the live pair counts of one "
-                       "iteration")}
+            "sample": (f"oracle/difficp_ref.c (OpenMP C, {threads} threads): {len(times['fwd'])} x (ODE fwd + VJP + "
+                       f"E-step) at {M}x{M} pairs ({took:.1f} s), rates fwd {rates['fwd'] / 1e9:.3f} / bwd "
+                       f"{rates['bwd'] / 1e9:.3f} / EM {rates['em'] / 1e9:.3f} Gpair/s, extrapolated to the live "
+                       "pair counts of one iteration")}
+
+
+def cpu_baseline_torch(pair_counts, budget_s=15.0, M=4000):
+    """The reference's CPU path as SURVEY 8(d) defines the baseline: the chunked torch
+    restatement of the reference's operators (oracle/torch_ref.py: the torch arithmetic of
+    kernel.py / LDDMM.py / GMM.py, float32, torch.set_num_threads = the host threads), timed on
+    a bounded sample -- one hybrid ODE evaluation (KRed + GenDKRed + GradKRed, LDDMM.py:176-227),
+    the same with its torch-autograd backward (optim.py:46), one torch-path EM step
+    (GMM.py:236-325) at M x M/4 -- and extrapolated to one iteration from the live pair counts.
+    Cross-timed against the imported reference at M <= 4000 in the build container:
+    profiles/r03_cpu_crosstime.json (restatement / reference within 1.2x)."""
+    from oracle import torch_ref as R
+    threads = _cpu_threads()
+    old_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = torch.Generator().manual_seed(0)
+        q = torch.rand(M, 3, generator=g)
+        p = 0.01 * torch.randn(M, 3, generator=g)
+        a = torch.randn(M, 3, generator=g)
+        b = torch.randn(M, 3, generator=g)
+        C = M // 4
+        X = torch.rand(M, 3, generator=g)
+        mu = torch.rand(C, 3, generator=g)
+        w0 = torch.zeros(C)
+        m = R.LDDMM(0.1, 3, 1e3, False, True)
+        c0 = torch.zeros(1)
+        opt = {"mu": True, "w": True, "sigma": True, "eta0": False}
+
+        def fwd_bwd():
+            qq = q.clone().requires_grad_(True)
+            pp = p.clone().requires_grad_(True)
+            v, mG, dc = m.ODE(qq, pp, c0)
+            torch.autograd.grad((a * v).sum() + (b * mG).sum() + dc.sum(), (qq, pp))
+
+        calls = {"fwd": lambda: m.ODE(q, p, c0), "fwd_bwd": fwd_bwd,
+                 "em": lambda: R.em_step(X, mu, w0, 0.05, opt)}
+        times, took = _round_robin(calls, budget_s)
+    finally:
+        torch.set_num_threads(old_threads)
+    avg = {k: sum(v) / len(v) for k, v in times.items()}
+    rates = {"fwd": M * M / avg["fwd"], "bwd": M * M / max(avg["fwd_bwd"] - avg["fwd"], 1e-9),
+             "em": M * C / avg["em"]}
+    secs = sum(v / rates[_pair_kind(k)] for k, v in pair_counts.items())
+    return {"value": 1.0 / secs, "unit": "PSR iterations/sec", "cores": threads, "kind": "port",
+            "sample": (f"oracle/torch_ref.py (the reference's torch arithmetic, float32, {threads} threads): "
+                       f"{len(times['fwd'])} x (hybrid ODE eval, ODE eval + autograd backward, EM step) at "
+                       f"{M} points ({took:.1f} s); rates fwd {rates['fwd'] / 1e9:.4f} / bwd {rates['bwd'] / 1e9:.4f} / "
+                       f"EM {rates['em'] / 1e9:.4f} Gpair/s, extrapolated to the live pair counts of one "
+                       "iteration; cross-timed vs the imported reference within 1.2x at N <= 4000 "
+                       "(profiles/r03_cpu_crosstime.json)")}
+
+
+def cpu_baseline(pair_counts, M_work):
+    """cpu_baseline object of the bench line: the reference-path torch restatement (SURVEY
+    8(d)) as the value, the faster OpenMP C restatement beside it."""
+    base = cpu_baseline_torch(pair_counts)
+    try:
+        base["c_openmp"] = cpu_baseline_c(pair_counts, M_work, budget_s=10.0)
+    except Exception as e:  # informative only
+        base["c_openmp"] = {"error": repr(e)}
+    return base
 
 
 def kernel_sum_probe(dev, M, reps=5):
@@ -226,16 +311,18 @@ def _main(out):
                                else f"replicas x{world}")}
         scaling = "strong" if split else "weak"
     else:
-        K = wl["K_per_rank"] * world
+        fixed = "K_total" in wl
+        K = wl["K_total"] if fixed else wl["K_per_rank"] * world
         comm = True if world > 1 else None
         psr = workloads.build_atlas(K, wl["N"], wl["C"], dev, comm=comm, seed=0, S=wl["S"])
         psr.concurrent_frames = args.concurrent_frames
         cfg = {"workload": f"groupwise atlas {K} frames x {wl['S']} structures x {wl['N']} 3D points, "
-                           f"C={wl['C']} per structure", "frames_per_rank": wl["K_per_rank"],
+                           f"C={wl['C']} per structure" + (" (BASELINE configs[3], fixed)" if fixed else ""),
+               "frames_per_rank": (f"{K // world}-{-(-K // world)}" if fixed else wl["K_per_rank"]),
                "lddmm": "hybrid sigma=0.1 lambda=1e3 Euler nt=10 dense", "max_repeat_GMM": 10,
                "tol": 1e-3, "parallelism": f"frame-sharded dp{world} (RCCL suff-stat exchange)",
                "concurrent_frames": args.concurrent_frames or "auto"}
-        scaling = "weak"
+        scaling = "strong" if fixed else "weak"
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s")
 
@@ -297,7 +384,8 @@ def _main(out):
         prof_iters = 1
 
     if rank == 0:
-        # row-split: all ranks advance the SAME match; replicas / atlas: every rank's own work
+        # row-split two-set / fixed atlas: all ranks advance the SAME problem; replicas /
+        # per-rank atlas: every rank's own work
         iters = args.steps * (1 if scaling == "strong" else world)
         value = iters / elapsed
         summ = prof.summary() if prof is not None else {}
