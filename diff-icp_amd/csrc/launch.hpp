@@ -200,6 +200,20 @@ int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, in
   return DICP_OK;
 }
 
+// Centred-expansion reductions (centred.hpp / centred.hip).  red_alg: 0 = never (generic
+// skeleton), 1 = automatic (large enough passes), 2 = always; cx_rho_x100: sub-tile radius (in
+// scaled units x 100) up to which the expanded exponent is used.
+int& red_alg();
+int& cx_rho_x100();
+bool cx_eligible(int64_t M, int64_t N);
+bool cx_has_op(int op);
+int cx_gauss_red(int op, const float* x, int64_t M, const float* y, int64_t N, int D, const float* b,
+                 double sigma, float* out, void* ws, size_t wsb, hipStream_t st);
+int cx_ext_fwd(const float* x, int64_t N, const float* q, const float* p, int64_t M, int D, double sigma,
+               double eta, float* vx, float* gx, void* ws, size_t wsb, hipStream_t st);
+size_t cx_red_ws(int64_t M, int64_t N, int D);
+size_t cx_ext_ws(int64_t N, int64_t M, int D);
+
 inline Scal make_scal(double sigma, double eta) {
   Scal sc;
   const double s = 1.0 / (sigma * sigma);

@@ -150,6 +150,16 @@ extern "C" int dicp_set_option(const char* name, int value) {
     g_bwd_alg = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "red_alg")) {
+    if (value < 0 || value > 2) return DICP_ERR_INVALID;
+    red_alg() = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "cx_rho_x100")) {
+    if (value < 0 || value > 100000) return DICP_ERR_INVALID;
+    cx_rho_x100() = value;
+    return DICP_OK;
+  }
   if (value != 1 && value != 2 && value != 4) return DICP_ERR_INVALID;
   if (!strcmp(name, "r_fwd")) { g_r_fwd = value; return DICP_OK; }
   if (!strcmp(name, "r_bwd")) { g_r_bwd = value; return DICP_OK; }
@@ -169,6 +179,8 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "mfma_rmax_x100")) { *value = mfma_rmax_x100(); return DICP_OK; }
   if (!strcmp(name, "bwd_eta_alg")) { *value = g_bwd_eta_alg; return DICP_OK; }
   if (!strcmp(name, "bwd_alg")) { *value = g_bwd_alg; return DICP_OK; }
+  if (!strcmp(name, "red_alg")) { *value = red_alg(); return DICP_OK; }
+  if (!strcmp(name, "cx_rho_x100")) { *value = cx_rho_x100(); return DICP_OK; }
   if (!strcmp(name, "r_fwd")) { *value = r_fwd(); return DICP_OK; }
   if (!strcmp(name, "r_bwd")) { *value = r_bwd(); return DICP_OK; }
   set_error("dicp_get_option: unknown option %s", name);
@@ -193,6 +205,8 @@ extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float
     set_error("dicp_gauss_red_f32: op %d needs b%s", op, needc ? " and c" : "");
     return DICP_ERR_INVALID;
   }
+  if (cx_has_op(op) && (D == 2 || D == 3) && cx_eligible(M, N))
+    return cx_gauss_red(op, x, M, y, N, D, b, sigma, out, ws, ws_bytes, st);
   switch (op) {
     case DICP_KBASE: return red_dispatch<OpKBase>("KBase", D, a, sc, M, N, out, ws, ws_bytes, st);
     case DICP_KREDSCAL: return red_dispatch<OpKRedScal>("KRedScal", D, a, sc, M, N, out, ws, ws_bytes, st);
@@ -448,6 +462,7 @@ template <int D>
 int ode_ext_fwd_d(const float* x, int64_t N, const float* q, const float* p, int64_t M,
                   double sigma, double eta, float* vx, float* gx, void* ws, size_t wsb,
                   hipStream_t st) {
+  if (cx_eligible(N, M)) return cx_ext_fwd(x, N, q, p, M, D, sigma, eta, vx, gx, ws, wsb, st);
   const Args a = {x, nullptr, nullptr, nullptr, q, p, nullptr, nullptr};
   const Scal sc = make_scal(sigma, eta);
   const Outs o = make_outs(vx, gx);
@@ -467,6 +482,10 @@ size_t ode_ext_fwd_ws(int64_t N, int64_t M) {
                    rowred_ws_bytes<OpOdeExtFwd<D, false, true>, kR>(N, M),
                    rowred_ws_bytes<OpOdeExtFwd<D, false, false>, kR>(N, M)})
     m = v > m ? v : m;
+  if (cx_eligible(N, M)) {
+    const size_t c = cx_ext_ws(N, M, D);
+    m = c > m ? c : m;
+  }
   return m;
 }
 
@@ -808,6 +827,10 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
                     red_ws<OpGradLapKScal>(D, M, N), red_ws<OpMinSqDistOther>(D, M, N),
                     red_ws<OpRadiusCount>(D, M, N)};
       for (size_t v : c) m = v > m ? v : m;
+      if (cx_eligible(M, N)) {
+        const size_t v = cx_red_ws(M, N, D);
+        m = v > m ? v : m;
+      }
       return m;
     }
     case DICP_WS_ODE_SELF_FWD: return D == 2 ? ode_self_fwd_ws<2>(M) : ode_self_fwd_ws<3>(M);

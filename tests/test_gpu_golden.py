@@ -32,8 +32,21 @@ def spec(dev):
     return {"device": dev, "dtype": torch.float32}
 
 
+@pytest.mark.parametrize("red_alg", [1, 2, 0])
 @pytest.mark.parametrize("fname", ["reductions", "reductions_large"])
-def test_reductions_golden(dev, fname):
+def test_reductions_golden(dev, fname, red_alg):
+    """red_alg 1: the library's automatic choice; 2: the centred-expansion path forced on
+    (KBase, KRedScal, KRed, GradKRed); 0: the generic skeleton only."""
+    from difficp_amd import _lib
+    old = _lib.get_option("red_alg")
+    _lib.set_option("red_alg", red_alg)
+    try:
+        _reductions_golden(dev, fname)
+    finally:
+        _lib.set_option("red_alg", old)
+
+
+def _reductions_golden(dev, fname):
     from difficp_amd.tools.kernel import GaussKernel
     z = load(fname)
     for key in keys(z, "/KRed"):
