@@ -86,7 +86,9 @@ int& red_alg() {
 bool cx_eligible(int64_t M, int64_t N) {
   if (red_alg() == 0) return false;
   if (red_alg() == 2) return M > 0 && N > 0;
-  return N >= 2048 && (double)M * (double)N >= 4.0e6;
+  // the prep pass (bounding box, Morton codes, radix sort, records) costs ~40-60 us: measured
+  // break-even between 20k x 20k (0.8x) and 50k x 50k (1.09x) (tools/cx_ab.py)
+  return N >= 16384 && (double)M * (double)N >= 2.0e9;
 }
 
 // Launch the centred reduction Op over rows x (M, D) and columns (y, fields in a.c1..) (N).

@@ -5,18 +5,21 @@
 // for r2 = |x - y|^2, a multiply by -log2(e)/(2 sigma^2), the exp and 3 fma.  Here the
 // columns are visited in a spatial (Morton) order and grouped into sub-tiles of 64 (one
 // wave's worth, built by one wave in the prep pass); each sub-tile t has a centre c_t, and in
-// scaled coordinates (X = alpha x - c_t, Y = alpha y - c_t, alpha = sqrt(log2 e / (2 sigma^2)))
+// scaled coordinates (X = alpha (x - c_t), Y = alpha (y - c_t), alpha = sqrt(log2 e / (2 sigma^2)))
 //     K = exp2(-|X - Y|^2) = exp2(2 X.Y - |Y|^2 - |X|^2)
 // where 2Y and -|Y|^2 are stored in the column record and -|X|^2 is formed once per
 // (row, sub-tile): the exponent costs 1 add + 3 fma, the whole KRed pair 7 VALU + 1 exp.
 // Terms linear in z = x - y are summed as X sum K - sum K Y (per sub-tile, then folded into
 // the row's totals), so GradKRed costs 8 VALU + exp and the external-point forward 8-12.
 //
-// Accuracy: the cancellation error of the expanded exponent is ~eps (|X|^2 + |Y|^2), small
+// Accuracy: X and Y are formed from RAW differences (x - c_t, y - c_t, then scaled), so their
+// rounding is relative to the distance from the sub-tile centre, not to the coordinates'
+// magnitude; the cancellation error of the expanded exponent is ~eps (|X|^2 + |Y|^2), small
 // where K matters (|X - Y| = O(1) and |Y| <= rho_t, the sub-tile radius).  A sub-tile whose
 // radius exceeds rho_max (cx_rho_x100 / 100 scaled units, default 1.5) is summed in the
-// difference form z = X - Y (same records, same centre), so the error never exceeds that of
-// a cloud of rho_max radius: checked against float64 in tests/test_gpu_centred.py.
+// difference form on the raw coordinates, z = alpha (x - y) (the record also carries y), with
+// the z-linear terms accumulated directly -- the generic skeleton's arithmetic.  Checked
+// against float64 in tests/test_gpu_centred.py (compact, wide and offset clouds).
 // Deterministic: the sort is a stable radix sort of Morton codes, summation order fixed.
 #pragma once
 #include "launch.hpp"
@@ -26,7 +29,11 @@ namespace dicp {
 
 constexpr int kSub = 64;  // columns per centred sub-tile (one wave64 in the prep pass)
 
-// ---- ops: record = [2Y (D) | -|Y|^2 | fields...] ------------------------------------------
+// ---- ops: record = [2Y (D) | -|Y|^2 | fields... | y (D, raw)] ------------------------------
+// pair(K, e, rec, acc): compact sub-tiles (expanded exponent e); pair_z(K, e, z, rec, acc):
+// wide sub-tiles, z = alpha (x - y) from raw coordinates, the z-linear sums accumulated
+// directly in the slots the compact form uses for its Y sums; fold(X, acc, tot, compact) adds a
+// sub-tile's partial sums into the row's totals (X terms only for compact sub-tiles).
 template <int D>
 struct CxBase {
   static constexpr int kPre = D + 1;
@@ -35,29 +42,34 @@ struct CxBase {
 // KBase: sum_j K                                                     kernel.py:131 / :178
 template <int D>
 struct CxKBase : CxBase<D> {
-  static constexpr int RW4 = cw4(D + 1), NACC = 1, NTOT = 1, kNOut = 1;
+  static constexpr int kRaw = D + 1;
+  static constexpr int RW4 = cw4(2 * D + 1), NACC = 1, NTOT = 1, kNOut = 1;
   static constexpr int kOutW[4] = {1, 0, 0, 0};
   __device__ static void build(const Args&, int64_t, const float*, float*) {}
   __device__ static void pair(float K, float, const float*, float* acc) { acc[0] += K; }
-  __device__ static void fold(const float*, const float* acc, float* tot) { tot[0] += acc[0]; }
+  __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
+  __device__ static void fold(const float*, const float* acc, float* tot, bool) { tot[0] += acc[0]; }
   __device__ static void store(const Scal&, float, const float* t, float* v) { v[0] = t[0]; }
 };
 
 // KRedScal: sum_j K d_j                                              kernel.py:135 / :182
 template <int D>
 struct CxKRedScal : CxBase<D> {
-  static constexpr int RW4 = cw4(D + 2), NACC = 1, NTOT = 1, kNOut = 1;
+  static constexpr int kRaw = D + 2;
+  static constexpr int RW4 = cw4(2 * D + 2), NACC = 1, NTOT = 1, kNOut = 1;
   static constexpr int kOutW[4] = {1, 0, 0, 0};
   __device__ static void build(const Args& a, int64_t o, const float*, float* rec) { rec[D + 1] = a.c1[o]; }
   __device__ static void pair(float K, float, const float* rec, float* acc) { acc[0] = fmaf(K, rec[D + 1], acc[0]); }
-  __device__ static void fold(const float*, const float* acc, float* tot) { tot[0] += acc[0]; }
+  __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
+  __device__ static void fold(const float*, const float* acc, float* tot, bool) { tot[0] += acc[0]; }
   __device__ static void store(const Scal&, float, const float* t, float* v) { v[0] = t[0]; }
 };
 
 // KRed: sum_j K b_j  (the velocity field, LDDMM.py:114)             kernel.py:138 / :186
 template <int D>
 struct CxKRed : CxBase<D> {
-  static constexpr int RW4 = cw4(2 * D + 1), NACC = D, NTOT = D, kNOut = 1;
+  static constexpr int kRaw = 2 * D + 1;
+  static constexpr int RW4 = cw4(3 * D + 1), NACC = D, NTOT = D, kNOut = 1;
   static constexpr int kOutW[4] = {D, 0, 0, 0};
   __device__ static void build(const Args& a, int64_t o, const float*, float* rec) {
 #pragma unroll
@@ -67,7 +79,8 @@ struct CxKRed : CxBase<D> {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + 1 + d], acc[d]);
   }
-  __device__ static void fold(const float*, const float* acc, float* tot) {
+  __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
+  __device__ static void fold(const float*, const float* acc, float* tot, bool) {
 #pragma unroll
     for (int d = 0; d < D; ++d) tot[d] += acc[d];
   }
@@ -78,9 +91,11 @@ struct CxKRed : CxBase<D> {
 };
 
 // GradKRed: -s sum_j K z = -(s/alpha) (X sum K - sum K Y)           kernel.py:142 / :190
+// (wide sub-tiles: -(s/alpha) sum K z' accumulated directly)
 template <int D>
 struct CxGradK : CxBase<D> {
-  static constexpr int RW4 = cw4(D + 1), NACC = D + 1, NTOT = D, kNOut = 1;
+  static constexpr int kRaw = D + 1;
+  static constexpr int RW4 = cw4(2 * D + 1), NACC = D + 1, NTOT = D, kNOut = 1;
   static constexpr int kOutW[4] = {D, 0, 0, 0};
   __device__ static void build(const Args&, int64_t, const float*, float*) {}
   __device__ static void pair(float K, float, const float* rec, float* acc) {
@@ -88,9 +103,13 @@ struct CxGradK : CxBase<D> {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[1 + d] = fmaf(K, rec[d], acc[1 + d]);  // sum K 2Y
   }
-  __device__ static void fold(const float* X, const float* acc, float* tot) {
+  __device__ static void pair_z(float K, float, const float* z, const float*, float* acc) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) tot[d] += fmaf(X[d], acc[0], -0.5f * acc[1 + d]);
+    for (int d = 0; d < D; ++d) acc[1 + d] = fmaf(K, z[d], acc[1 + d]);    // sum K z
+  }
+  __device__ static void fold(const float* X, const float* acc, float* tot, bool compact) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) tot[d] += compact ? fmaf(X[d], acc[0], -0.5f * acc[1 + d]) : acc[1 + d];
   }
   __device__ static void store(const Scal& sc, float sa, const float* t, float* v) {
 #pragma unroll
@@ -105,8 +124,9 @@ struct CxGradK : CxBase<D> {
 template <int D, bool ETA, bool DIV>
 struct CxExtFwd : CxBase<D> {
   static constexpr int kW = 2 * D + 1;                       // w_j slot
-  static constexpr int RW4 = cw4(2 * D + 1 + (DIV ? 1 : 0));
-  // acc: V (D) | W | K, K2Y (D), Ke
+  static constexpr int kRaw = 2 * D + 1 + (DIV ? 1 : 0);
+  static constexpr int RW4 = cw4(kRaw + D);
+  // acc: V (D) | W | K, K2Y (D), Ke  (wide sub-tiles: W <- sum K (z.p), K2Y <- sum K z)
   static constexpr int oW = D, oK = D + (DIV ? 1 : 0);
   static constexpr int NACC = oK + (ETA ? D + 2 : 0);
   // tot: V (D) | G | Z (D), L
@@ -135,18 +155,32 @@ struct CxExtFwd : CxBase<D> {
       acc[oK + 1 + D] = fmaf(K, e, acc[oK + 1 + D]);
     }
   }
-  __device__ static void fold(const float* X, const float* acc, float* tot) {
+  __device__ static void pair_z(float K, float e, const float* z, const float* rec, float* acc) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + 1 + d], acc[d]);
+    if (DIV) acc[oW] = fmaf(K, dot<D>(z, rec + D + 1), acc[oW]);
+    if (ETA) {
+      acc[oK] += K;
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[oK + 1 + d] = fmaf(K, z[d], acc[oK + 1 + d]);
+      acc[oK + 1 + D] = fmaf(K, e, acc[oK + 1 + D]);
+    }
+  }
+  __device__ static void fold(const float* X, const float* acc, float* tot, bool compact) {
 #pragma unroll
     for (int d = 0; d < D; ++d) tot[d] += acc[d];
     if (DIV) {
-      float g = -acc[oW];
+      float g = compact ? -acc[oW] : acc[oW];
+      if (compact) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) g = fmaf(X[d], acc[d], g);
+        for (int d = 0; d < D; ++d) g = fmaf(X[d], acc[d], g);
+      }
       tot[tG] += g;
     }
     if (ETA) {
 #pragma unroll
-      for (int d = 0; d < D; ++d) tot[tZ + d] += fmaf(X[d], acc[oK], -0.5f * acc[oK + 1 + d]);
+      for (int d = 0; d < D; ++d)
+        tot[tZ + d] += compact ? fmaf(X[d], acc[oK], -0.5f * acc[oK + 1 + d]) : acc[oK + 1 + d];
       tot[tZ + D] += fmaf(-kS2, acc[oK + 1 + D], -(float)D * acc[oK]);
     }
   }
@@ -242,7 +276,7 @@ __global__ __launch_bounds__(256) void cx_codes_kernel(const float* __restrict__
 
 // One wave per sub-tile of 64 sorted columns: the sub-tile centre (mid-range of its scaled
 // coordinates), its radius, and the column records [2Y | -|Y|^2 | fields] relative to it.
-// meta[t] = (centre (D), 1 if the sub-tile is compact (radius^2 <= rho2max) else 0).
+// meta[t] = (raw centre (D), 1 if the sub-tile is compact (scaled radius^2 <= rho2max) else 0).
 template <int D, class Op>
 __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float alpha, float rho2max,
                                                        const int32_t* __restrict__ order, float4* recs,
@@ -254,12 +288,12 @@ __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float 
   const int64_t j = t * kSub + lane;
   const bool valid = j < N;
   const int64_t o = valid ? order[j] : 0;
-  float Y[D], lo[D], hi[D];
+  float y[D], lo[D], hi[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    Y[d] = alpha * a.c0[o * D + d];
-    lo[d] = valid ? Y[d] : __builtin_huge_valf();
-    hi[d] = valid ? Y[d] : -__builtin_huge_valf();
+    y[d] = a.c0[o * D + d];
+    lo[d] = valid ? y[d] : __builtin_huge_valf();
+    hi[d] = valid ? y[d] : -__builtin_huge_valf();
   }
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -270,8 +304,8 @@ __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float 
   float c[D], Yc[D], r2 = 0.f;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    c[d] = 0.5f * (lo[d] + hi[d]);
-    Yc[d] = Y[d] - c[d];
+    c[d] = 0.5f * (lo[d] + hi[d]);          // raw centre of the sub-tile
+    Yc[d] = alpha * (y[d] - c[d]);          // scaled, relative to it
     r2 = fmaf(Yc[d], Yc[d], r2);
   }
   float rmax = valid ? r2 : 0.f;
@@ -281,7 +315,10 @@ __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float 
 #pragma unroll
     for (int k = 0; k < Op::RW4 * 4; ++k) rec[k] = 0.f;
 #pragma unroll
-    for (int d = 0; d < D; ++d) rec[d] = 2.f * Yc[d];
+    for (int d = 0; d < D; ++d) {
+      rec[d] = 2.f * Yc[d];
+      rec[Op::kRaw + d] = y[d];
+    }
     rec[D] = -r2;
     Op::build(a, o, Yc, rec);
 #pragma unroll
@@ -309,13 +346,13 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
   __shared__ float4 lmeta[2][NSUB];
   const int tid = threadIdx.x;
   const int64_t ibase = (int64_t)blockIdx.x * (kBlock * R) + tid;
-  float xs[R][D];
+  float xs[R][D];  // raw coordinates of the thread's rows
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     int64_t i = ibase + (int64_t)r * kBlock;
     if (i >= M) i = M - 1;
 #pragma unroll
-    for (int d = 0; d < D; ++d) xs[r][d] = alpha * x[i * D + d];
+    for (int d = 0; d < D; ++d) xs[r][d] = x[i * D + d];
   }
   float tot[R][Op::NTOT];
 #pragma unroll
@@ -357,7 +394,7 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
         float a2 = 0.f;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-          X[r][d] = xs[r][d] - cm[d];
+          X[r][d] = alpha * (xs[r][d] - cm[d]);
           a2 = fmaf(X[r][d], X[r][d], a2);
         }
         A[r] = -a2;
@@ -382,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
             Op::pair(fast_exp2(e), e, rec, acc[r]);
           }
         }
-      } else {  // wide sub-tile: difference form on the same records (Y = rec / 2)
+      } else {  // wide sub-tile: difference form on the raw coordinates (the generic arithmetic)
 #pragma unroll 2
         for (int t = 0; t < n; ++t) {
           float rec[RW4 * 4];
@@ -393,18 +430,18 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
           }
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            float e = 0.f;
+            float z[D], e = 0.f;
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-              const float z = fmaf(-0.5f, rec[d], X[r][d]);
-              e = fmaf(-z, z, e);
+              z[d] = alpha * (xs[r][d] - rec[Op::kRaw + d]);
+              e = fmaf(-z[d], z[d], e);
             }
-            Op::pair(fast_exp2(e), e, rec, acc[r]);
+            Op::pair_z(fast_exp2(e), e, z, rec, acc[r]);
           }
         }
       }
 #pragma unroll
-      for (int r = 0; r < R; ++r) Op::fold(X[r], acc[r], tot[r]);
+      for (int r = 0; r < R; ++r) Op::fold(X[r], acc[r], tot[r], m.w != 0.f);
     }
     __syncthreads();
     buf ^= 1;
