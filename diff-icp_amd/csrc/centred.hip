@@ -35,7 +35,7 @@ CxLayout cx_layout(int64_t N, int rw4, int64_t slab_floats) {
   CxLayout L;
   const int64_t nsub = (N + kSub - 1) / kSub;
   size_t o = 0;
-  L.box = o; o += align256(64);
+  L.box = o; o += align256((size_t)kBoxBlocks * 8 * sizeof(float));
   L.keys0 = o; o += align256((size_t)N * 4);
   L.keys1 = o; o += align256((size_t)N * 4);
   L.vals0 = o; o += align256((size_t)N * 4);
@@ -116,12 +116,15 @@ int launch_cx(const char* name, const float* x, int64_t M, Args a, int64_t N, do
   const double alpha = std::sqrt(1.4426950408889634 / (2.0 * sigma * sigma));
   Scal sc = make_scal(sigma, eta);
   sc.aux1 = (float)(1.0 / (sigma * sigma) / alpha);
-  const float rho = cx_rho_x100() / 100.f;
+  float rho = cx_rho_x100() / 100.f;
+  if (rho > kCxRhoCap) rho = kCxRhoCap;   // the factored exponent's range (centred.hpp)
   // prep: sort the columns along a Morton curve, build the sub-tile records
-  cx_bbox_kernel<D><<<1, 1024, 0, st>>>(a.c0, N, box);
+  int64_t nparts = (N + 1023) / 1024;
+  if (nparts > kBoxBlocks) nparts = kBoxBlocks;
+  cx_bbox_kernel<D><<<(unsigned)nparts, 256, 0, st>>>(a.c0, N, box);
   int rc = check_launch(name);
   if (rc) return rc;
-  cx_codes_kernel<D><<<(unsigned)((N + 255) / 256), 256, 0, st>>>(a.c0, N, box, k0, v0);
+  cx_codes_kernel<D><<<(unsigned)((N + 255) / 256), 256, 0, st>>>(a.c0, N, box, (int)nparts, k0, v0);
   if ((rc = check_launch(name))) return rc;
   size_t tb = sort_temp_bytes(N);
   if (rocprim::radix_sort_pairs(base + L.sort, tb, k0, k1, v0, v1, (unsigned int)N, 0, 30, st) != hipSuccess) {
@@ -165,7 +168,10 @@ int launch_cx(const char* name, const float* x, int64_t M, Args a, int64_t N, do
   return DICP_OK;
 }
 
-constexpr int kCxR = 2;  // rows per thread
+#ifndef DICP_CX_R
+#define DICP_CX_R 2
+#endif
+constexpr int kCxR = DICP_CX_R;  // rows per thread
 
 template <int D>
 int cx_gauss_red_d(int op, const float* x, int64_t M, const float* y, int64_t N, const float* b,

@@ -6,11 +6,17 @@
 // columns are visited in a spatial (Morton) order and grouped into sub-tiles of 64 (one
 // wave's worth, built by one wave in the prep pass); each sub-tile t has a centre c_t, and in
 // scaled coordinates (X = alpha (x - c_t), Y = alpha (y - c_t), alpha = sqrt(log2 e / (2 sigma^2)))
-//     K = exp2(-|X - Y|^2) = exp2(2 X.Y - |Y|^2 - |X|^2)
-// where 2Y and -|Y|^2 are stored in the column record and -|X|^2 is formed once per
-// (row, sub-tile): the exponent costs 1 add + 3 fma, the whole KRed pair 7 VALU + 1 exp.
-// Terms linear in z = x - y are summed as X sum K - sum K Y (per sub-tile, then folded into
-// the row's totals), so GradKRed costs 8 VALU + exp and the external-point forward 8-12.
+//     K = exp2(-|X - Y|^2) = exp2(m - |X|^2) * exp2(2 X.Y - |Y|^2 - m)
+// where 2Y and -|Y|^2 - m are stored in the column record and the row factor
+// F = exp2(m - |X|^2) is formed once per (row, sub-tile) and applied to the sub-tile's partial
+// sums: the exponent costs 3 fma, the whole KRed pair 6 VALU + 1 exp (the generic skeleton:
+// 10).  Terms linear in z = x - y are summed as X sum K - sum K Y (per sub-tile, then folded
+// into the row's totals), so GradKRed costs 7 VALU + exp and the external-point forward 7-11.
+// Range (m = 16, sub-tile radius rho <= 4): 2 X.Y - |Y|^2 - m <= 2 rho |X| - m stays finite
+// for |X| <= 14, and rows farther than 14 scaled units from a sub-tile (F = 0 in float32) are
+// clamped to |X| = 14 -- their contributions from it are below 2^-140 and vanish either way;
+// F itself underflows (below 2^-126) only for rows more than ~12 scaled units (~14 sigma)
+// from the sub-tile, whose contributions are below 2^-(12 - rho)^2.
 //
 // Accuracy: X and Y are formed from RAW differences (x - c_t, y - c_t, then scaled), so their
 // rounding is relative to the distance from the sub-tile centre, not to the coordinates'
@@ -28,12 +34,16 @@
 namespace dicp {
 
 constexpr int kSub = 64;  // columns per centred sub-tile (one wave64 in the prep pass)
+constexpr float kCxShift = 16.f;     // m: exponent shift between the row factor and the pair term
+constexpr float kCxClamp = 14.f;     // |X| clamp (see above); needs rho <= kCxRhoCap
+constexpr float kCxRhoCap = 4.f;     // largest sub-tile radius the expanded form accepts
 
 // ---- ops: record = [2Y (D) | -|Y|^2 | fields... | y (D, raw)] ------------------------------
-// pair(K, e, rec, acc): compact sub-tiles (expanded exponent e); pair_z(K, e, z, rec, acc):
-// wide sub-tiles, z = alpha (x - y) from raw coordinates, the z-linear sums accumulated
-// directly in the slots the compact form uses for its Y sums; fold(X, acc, tot, compact) adds a
-// sub-tile's partial sums into the row's totals (X terms only for compact sub-tiles).
+// pair(K, e, rec, acc): compact sub-tiles (K without the row factor F, e its exponent);
+// pair_z(K, e, z, rec, acc): wide sub-tiles, z = alpha (x - y) from raw coordinates, the
+// z-linear sums accumulated directly in the slots the compact form uses for its Y sums;
+// fold(X, acc, tot, compact, F, Es) adds a sub-tile's partial sums into the row's totals
+// (compact: times F = exp2(Es), with the X terms; wide: as they are).
 template <int D>
 struct CxBase {
   static constexpr int kPre = D + 1;
@@ -48,7 +58,9 @@ struct CxKBase : CxBase<D> {
   __device__ static void build(const Args&, int64_t, const float*, float*) {}
   __device__ static void pair(float K, float, const float*, float* acc) { acc[0] += K; }
   __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
-  __device__ static void fold(const float*, const float* acc, float* tot, bool) { tot[0] += acc[0]; }
+  __device__ static void fold(const float*, const float* acc, float* tot, bool c, float F, float) {
+    tot[0] = fmaf(c ? F : 1.f, acc[0], tot[0]);
+  }
   __device__ static void store(const Scal&, float, const float* t, float* v) { v[0] = t[0]; }
 };
 
@@ -61,7 +73,9 @@ struct CxKRedScal : CxBase<D> {
   __device__ static void build(const Args& a, int64_t o, const float*, float* rec) { rec[D + 1] = a.c1[o]; }
   __device__ static void pair(float K, float, const float* rec, float* acc) { acc[0] = fmaf(K, rec[D + 1], acc[0]); }
   __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
-  __device__ static void fold(const float*, const float* acc, float* tot, bool) { tot[0] += acc[0]; }
+  __device__ static void fold(const float*, const float* acc, float* tot, bool c, float F, float) {
+    tot[0] = fmaf(c ? F : 1.f, acc[0], tot[0]);
+  }
   __device__ static void store(const Scal&, float, const float* t, float* v) { v[0] = t[0]; }
 };
 
@@ -80,9 +94,10 @@ struct CxKRed : CxBase<D> {
     for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + 1 + d], acc[d]);
   }
   __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
-  __device__ static void fold(const float*, const float* acc, float* tot, bool) {
+  __device__ static void fold(const float*, const float* acc, float* tot, bool c, float F, float) {
+    const float f = c ? F : 1.f;
 #pragma unroll
-    for (int d = 0; d < D; ++d) tot[d] += acc[d];
+    for (int d = 0; d < D; ++d) tot[d] = fmaf(f, acc[d], tot[d]);
   }
   __device__ static void store(const Scal&, float, const float* t, float* v) {
 #pragma unroll
@@ -107,9 +122,10 @@ struct CxGradK : CxBase<D> {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[1 + d] = fmaf(K, z[d], acc[1 + d]);    // sum K z
   }
-  __device__ static void fold(const float* X, const float* acc, float* tot, bool compact) {
+  __device__ static void fold(const float* X, const float* acc, float* tot, bool compact, float F, float) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) tot[d] += compact ? fmaf(X[d], acc[0], -0.5f * acc[1 + d]) : acc[1 + d];
+    for (int d = 0; d < D; ++d)
+      tot[d] += compact ? F * fmaf(X[d], acc[0], -0.5f * acc[1 + d]) : acc[1 + d];
   }
   __device__ static void store(const Scal& sc, float sa, const float* t, float* v) {
 #pragma unroll
@@ -166,22 +182,25 @@ struct CxExtFwd : CxBase<D> {
       acc[oK + 1 + D] = fmaf(K, e, acc[oK + 1 + D]);
     }
   }
-  __device__ static void fold(const float* X, const float* acc, float* tot, bool compact) {
+  __device__ static void fold(const float* X, const float* acc, float* tot, bool compact, float F, float Es) {
+    const float f = compact ? F : 1.f;
 #pragma unroll
-    for (int d = 0; d < D; ++d) tot[d] += acc[d];
+    for (int d = 0; d < D; ++d) tot[d] = fmaf(f, acc[d], tot[d]);
     if (DIV) {
       float g = compact ? -acc[oW] : acc[oW];
       if (compact) {
 #pragma unroll
         for (int d = 0; d < D; ++d) g = fmaf(X[d], acc[d], g);
       }
-      tot[tG] += g;
+      tot[tG] = fmaf(f, g, tot[tG]);
     }
     if (ETA) {
 #pragma unroll
       for (int d = 0; d < D; ++d)
-        tot[tZ + d] += compact ? fmaf(X[d], acc[oK], -0.5f * acc[oK + 1 + d]) : acc[oK + 1 + d];
-      tot[tZ + D] += fmaf(-kS2, acc[oK + 1 + D], -(float)D * acc[oK]);
+        tot[tZ + d] += compact ? F * fmaf(X[d], acc[oK], -0.5f * acc[oK + 1 + d]) : acc[oK + 1 + d];
+      // sum K e over the true exponents: compact pairs carry e - Es
+      const float Ke = compact ? fmaf(Es, acc[oK], acc[oK + 1 + D]) : acc[oK + 1 + D];
+      tot[tZ + D] += f * fmaf(-kS2, Ke, -(float)D * acc[oK]);
     }
   }
   __device__ static void store(const Scal& sc, float sa, const float* t, float* v) {
@@ -195,17 +214,19 @@ struct CxExtFwd : CxBase<D> {
 };
 
 // ---- prep pass ----------------------------------------------------------------------------
-// bounding box of the columns (one workgroup of 1024 threads; box = lo[D], hi[D])
+// bounding box of the columns, stage 1: each workgroup reduces a grid-strided share of the
+// columns to (lo[D], hi[D]) in part[blockIdx.x]; the codes kernel reduces the parts (stage 2)
+constexpr int kBoxBlocks = 256;
 template <int D>
-__global__ __launch_bounds__(1024) void cx_bbox_kernel(const float* __restrict__ y, int64_t N, float* box) {
-  __shared__ float red[2 * D][16];
+__global__ __launch_bounds__(256) void cx_bbox_kernel(const float* __restrict__ y, int64_t N, float* part) {
+  __shared__ float red[2 * D][4];
   float lo[D], hi[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     lo[d] = __builtin_huge_valf();
     hi[d] = -__builtin_huge_valf();
   }
-  for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < N; j += (int64_t)gridDim.x * blockDim.x) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float v = y[j * D + d];
@@ -232,8 +253,8 @@ __global__ __launch_bounds__(1024) void cx_bbox_kernel(const float* __restrict__
   if (threadIdx.x < 2 * D) {
     const int k = threadIdx.x;
     float v = red[k][0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) v = k < D ? fminf(v, red[k][i]) : fmaxf(v, red[k][i]);
-    box[k] = v;
+    for (int i = 1; i < 4; ++i) v = k < D ? fminf(v, red[k][i]) : fmaxf(v, red[k][i]);
+    part[blockIdx.x * 2 * D + k] = v;
   }
 }
 
@@ -253,11 +274,42 @@ __device__ __forceinline__ uint32_t spread2(uint32_t c) {  // 15 bits -> every s
   return c;
 }
 
-// Morton code of each column over the bounding box (30 bits), value = column index
+// Morton code of each column over the bounding box (30 bits), value = column index; every
+// workgroup first reduces the nparts bounding-box parts of cx_bbox_kernel (first wave)
 template <int D>
 __global__ __launch_bounds__(256) void cx_codes_kernel(const float* __restrict__ y, int64_t N,
-                                                       const float* __restrict__ box, uint32_t* keys,
-                                                       int32_t* vals) {
+                                                       const float* __restrict__ part, int nparts,
+                                                       uint32_t* keys, int32_t* vals) {
+  __shared__ float box[2 * D];
+  if (threadIdx.x < 64) {
+    float lo[D], hi[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      lo[d] = __builtin_huge_valf();
+      hi[d] = -__builtin_huge_valf();
+    }
+    for (int b = threadIdx.x; b < nparts; b += 64) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        lo[d] = fminf(lo[d], part[b * 2 * D + d]);
+        hi[d] = fmaxf(hi[d], part[b * 2 * D + D + d]);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      for (int off = 32; off > 0; off >>= 1) {
+        lo[d] = fminf(lo[d], __shfl_xor(lo[d], off, 64));
+        hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off, 64));
+      }
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        box[d] = lo[d];
+        box[D + d] = hi[d];
+      }
+    }
+  }
+  __syncthreads();
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= N) return;
   constexpr uint32_t kMax = D == 3 ? 1023u : 32767u;
@@ -319,7 +371,7 @@ __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float 
       rec[d] = 2.f * Yc[d];
       rec[Op::kRaw + d] = y[d];
     }
-    rec[D] = -r2;
+    rec[D] = -r2 - kCxShift;
     Op::build(a, o, Yc, rec);
 #pragma unroll
     for (int k = 0; k < Op::RW4; ++k)
@@ -388,7 +440,8 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
       const int n = (cnt - b0) < kSub ? (cnt - b0) : kSub;
       const float4 m = lmeta[buf][sb];
       const float cm[3] = {m.x, m.y, m.z};
-      float X[R][D], A[R], acc[R][Op::NACC];
+      const bool compact = m.w != 0.f;
+      float X[R][D], F[R], Es[R], acc[R][Op::NACC];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         float a2 = 0.f;
@@ -397,12 +450,18 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
           X[r][d] = alpha * (xs[r][d] - cm[d]);
           a2 = fmaf(X[r][d], X[r][d], a2);
         }
-        A[r] = -a2;
+        Es[r] = kCxShift - a2;                 // row factor F = exp2(m - |X|^2)
+        F[r] = fast_exp2(Es[r]);
+        if (a2 > kCxClamp * kCxClamp) {        // F = 0: keep the pair exponents finite
+          const float f = kCxClamp * __builtin_amdgcn_rsqf(a2);
+#pragma unroll
+          for (int d = 0; d < D; ++d) X[r][d] *= f;
+        }
 #pragma unroll
         for (int k = 0; k < Op::NACC; ++k) acc[r][k] = 0.f;
       }
       const float4* tile = lds[buf] + b0 * RW4;
-      if (m.w != 0.f) {  // compact sub-tile: expanded exponent, 1 add + D fma
+      if (compact) {  // compact sub-tile: expanded exponent, D fma
 #pragma unroll 2
         for (int t = 0; t < n; ++t) {
           float rec[RW4 * 4];
@@ -413,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
           }
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            float e = A[r] + rec[D];
+            float e = rec[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) e = fmaf(X[r][d], rec[d], e);
             Op::pair(fast_exp2(e), e, rec, acc[r]);
@@ -441,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
         }
       }
 #pragma unroll
-      for (int r = 0; r < R; ++r) Op::fold(X[r], acc[r], tot[r], m.w != 0.f);
+      for (int r = 0; r < R; ++r) Op::fold(X[r], acc[r], tot[r], compact, F[r], Es[r]);
     }
     __syncthreads();
     buf ^= 1;

@@ -73,9 +73,9 @@ def test_centred_reductions_match_oracle(dev, D, M, N, sig, ext):
 
 @pytest.mark.parametrize("D", [2, 3])
 def test_centred_fallback_and_compact_agree(dev, D):
-    """rho_max 0 (every sub-tile in the difference form) vs the default vs a huge rho_max
-    (every sub-tile expanded, even wide ones): all within the criterion on a cloud whose
-    extent is ~30 sigma, so the expanded form's cancellation is exercised."""
+    """rho_max 0 (every sub-tile in the difference form) vs the default vs the largest rho_max
+    the factored exponent accepts (4 scaled units, kCxRhoCap): all within the criterion on a
+    cloud whose extent is ~30 sigma, so the expanded form's cancellation is exercised."""
     from difficp_amd import _lib as L
     g = torch.Generator().manual_seed(3 + D)
     M, N, sig = 6000, 9000, 0.1
@@ -84,7 +84,7 @@ def test_centred_fallback_and_compact_agree(dev, D):
     b = torch.randn(N, D, generator=g, dtype=torch.float64)
     f = lambda t: t.float().to(dev).contiguous()
     ref = R.KRed(x, y, b, sig)
-    for rho in (0, 150, 100000):
+    for rho in (0, 150, 100000):       # 100000 is capped at 400 by the library
         with red_alg(2, rho):
             out = L.gauss_red(L.KRED, f(x), f(y), sig, b=f(b))
         assert rel_err(out.cpu(), ref) < 1e-5, (rho, rel_err(out.cpu(), ref))
