@@ -16,7 +16,6 @@ keep their initial values there (x1, y, a0 are only meaningful on the owning ran
 from __future__ import annotations
 
 import copy
-import warnings
 
 import numpy as np
 import torch
@@ -25,8 +24,8 @@ from .GMM import GaussianMixtureUnif, _comm_active, _gather_rows, _sum_ranks
 from .LDDMM import LDDMMModel
 from .registrations import LDDMMRegistration
 from ..tools.in_out import read_point_sets
-from ..tools.point_sets import decimate
 from ..tools.spec import defspec
+from .support import decimated_points, grid_points, merged_v2p_args, warn_uncovered
 
 
 def _rank_world(comm):
@@ -250,40 +249,26 @@ class DiffPSR(MultiPSR):
             self.a0[k] = self.LMi.v2p(self.q0[k], v0, **v2p_args)
 
     def update_a0(self, q0_prev, a0_prev=None, **v2p_args):
-        if self.v2p_args and not v2p_args.get("version"):
-            v2p_args = {**self.v2p_args, **{k: v for k, v in v2p_args.items() if k != "rcond"}}
+        """Momenta on the current support giving the previous velocity field (PSR.py:415-425)."""
+        v2p_args = merged_v2p_args(self.v2p_args, v2p_args)
         if a0_prev is None:
             a0_prev = self.a0
         for k in range(self.K):
             v0 = self.LMi.v(self.q0[k], q0_prev[k], a0_prev[k])
             self.a0[k] = self.LMi.v2p(self.q0[k], v0, **v2p_args)
 
-    def set_support_scheme(self, scheme="decim", rho=1.0, xticks=None, yticks=None, q0=None):
+    def set_support_scheme(self, scheme="decim", rho=1.0, xticks=None, yticks=None, q0=None, zticks=None):
         """Support points (PSR.py:430-493): "decim" (greedy covering decimation of each
-        structure, point_sets.py:102-133, device kernels), "grid" (2D, :472-482) or
-        "custom" (:484-487)."""
+        structure, point_sets.py:102-133, device kernels), "grid" (the reference's 2D grid, and
+        its 3D extension: core/support.py grid_points; zticks for the third axis) or "custom"
+        (:484-487)."""
         self.rho = rho
         Rcover = rho * self.LMi.Kernel.sigma
         self.support_scheme = scheme
         q0_prev = self.q0
         if scheme == "grid":
-            if self.D != 2:
-                raise ValueError("grid support scheme is 2D only (as in the reference)")
-            if xticks is None or yticks is None:
-                # get_bounds(*allx0, relmargin=0.1) (visualization/visu.py:35-50), same float32 ops
-                xs = [a.detach().cpu() for a in self.allx0 if len(a) > 0]
-                mins = torch.cat(tuple(a.min(0).values.reshape(1, 2) for a in xs), 0).min(0).values.numpy()
-                maxs = torch.cat(tuple(a.max(0).values.reshape(1, 2) for a in xs), 0).max(0).values.numpy()
-                gmin = (1 + 0.1) * mins - 0.1 * maxs
-                gmax = (1 + 0.1) * maxs - 0.1 * mins
-                xmin, xmax, ymin, ymax = gmin[0], gmax[0], gmin[1], gmax[1]
-            if xticks is None:
-                xticks = np.arange(xmin - Rcover / 2, xmax + Rcover / 2, Rcover)
-            if yticks is None:
-                yticks = np.arange(ymin - Rcover / 2, ymax + Rcover / 2, Rcover)
-            gp = np.stack(np.meshgrid(xticks, yticks), axis=2)
-            gp = torch.tensor(gp.reshape((-1, 2), order="F"), **self.compspec).contiguous()
-            self.q0 = [gp] * self.K
+            ticks = (xticks, yticks) if self.D == 2 else (xticks, yticks, zticks)
+            self.q0 = [grid_points(self.allx0, Rcover, self.D, self.compspec, ticks)] * self.K
         elif scheme == "custom":
             assert q0 is not None, "For a custom support scheme, please specify argument q0"
             self.q0 = [q0.clone().detach().to(**self.compspec).contiguous()] * self.K
@@ -292,14 +277,13 @@ class DiffPSR(MultiPSR):
             self.supp_ids = np.array([[None] * self.S] * self.K, dtype=object)
             self.q0 = [None] * self.K
             for k in range(self.K):
+                self.q0[k], ids = decimated_points(list(self.x0[k, :]), Rcover, self.compspec)
                 for s in range(self.S):
-                    self.supp_ids[k, s], _ = decimate(self.x0[k, s].to(**self.compspec), Rcover)
-                Ndecim = sum(len(self.supp_ids[k, s]) for s in range(self.S))
+                    self.supp_ids[k, s] = ids[s]
                 if self.printstuff:
+                    Ndecim = self.q0[k].shape[0]
                     Pdecim = Ndecim / sum(int(self.N[k, s]) for s in range(self.S))
                     print(f"Decimation, frame {k} : {Ndecim} support points ({Pdecim:.0%} of original sets)")
-                self.q0[k] = torch.cat(tuple(self.x0[k, s][self.supp_ids[k, s]] for s in range(self.S)),
-                                       dim=0).to(**self.compspec).contiguous()
         else:
             raise ValueError(f"Unknown value of support point scheme : {scheme}.")
         self.update_a0(q0_prev, rcond=1e-1)
@@ -372,15 +356,7 @@ class DiffPSR(MultiPSR):
             for s in range(self.S):
                 self.update_quadloss(k, s)
             if self.support_scheme is not None:
-                Rw = 2.0
-                for t in range(len(self.shoot[k])):
-                    qk, xk = self.shoot[k][t][0], self.shoot[k][t][-1]
-                    unc = self.LMi.Kernel.check_coverage(xk, qk, Rw)
-                    if unc.any():
-                        print(f"WARNING : shooting, time step {t} : {unc.sum()} uncovered points "
-                              f"({unc.sum() / xk.shape[0]:.2%})")
-                        warnings.warn("Uncovered points during LDDMM shooting. Choose a smaller rho "
-                                      "when defining the support scheme.", RuntimeWarning)
+                warn_uncovered(self.LMi.Kernel, self.shoot[k])
             chg = change if isinstance(change, str) else f"{change:.4}"
             msg = f"Frame {k} : {isteps} optim steps, loss={self.regloss[k] + datal:.4}, change={chg}."
             if self.world == 1:

@@ -1,21 +1,21 @@
-"""Standard (Glaunes-style) point-set registration with template estimation: mirror of
-diffICP/core/PSR_standard.py on the HIP path.
+"""Standard (Glaunes-style) point-set registration with template estimation on the HIP path
+(SURVEY 8(f) f4): the API of diffICP/core/PSR_standard.py (`data_distance` :37-58,
+`MultiPSR_std` :67-357, `DiffPSR_std` :364-566), built on this package's own pieces:
 
-The data attachment is the RKHS distance between point clouds seen as signed measures
-(`data_distance`, PSR_standard.py:37-58), built from the KBase / KRedScal reductions
-(dicp_gauss_red_f32, differentiable through tools/kernel.py); the registrations are the
-fused LDDMM shootings (core/shooting.py) -- dense support: warped template = q1; other
-support schemes: the template is carried as external points (x).  `MultiPSR_std` /
-`DiffPSR_std` keep the reference's attributes (y0, y1, x, Nx, Ny, w0, a0, q0, shoot,
-regloss, dataloss, E), call order and energy bookkeeping.  AffinePSR_std (affine
-registrations, not on the kernel hot path) is out of scope.
+  * the data attachment is the RKHS distance between point clouds seen as measures,
+    assembled from the KBase / KRedScal reductions (dicp_gauss_red_f32, differentiable
+    through tools/kernel.py, centred-expansion kernels at scale);
+  * each frame's registration is the fused LDDMM shooting of core/shooting.py (dense
+    support: the warped template is q1; other supports carry the template as external points);
+  * support schemes, momentum re-projection, coverage warnings and row splitting are the
+    helpers shared with core/PSR.py (core/support.py) -- including the 3D grid.
 
-Reference quirks kept or fixed:
-  * the loss accumulators of Reg_opt / Template_opt start from `torch.tensor([0.0])`, a
-    float32 CPU tensor (PSR_standard.py:235, :519): their sums are float32 in the reference,
-    kept float32 here but created on the computation device (the reference's breaks on GPU);
-  * data_distance(x, x) terms do not depend on the optimised variables; they are still
-    evaluated (same values, same energy), once per call as in the reference.
+Energy bookkeeping follows the reference: E = sum_k regloss_k + sum_{k,s} dataloss_{k,s}, with
+dataloss = data_distance / noise_std^2; the L-BFGS losses of Reg_opt and Template_opt are
+accumulated in a float32 one-element tensor as the reference's `torch.tensor([0.0])`
+(PSR_standard.py:235, :519), created on the computation device (the reference's is on the CPU,
+which breaks its GPU path).  AffinePSR_std (affine registrations, no pair kernels) is out of
+scope.
 """
 from __future__ import annotations
 
@@ -27,75 +27,99 @@ import torch
 from ..tools.in_out import read_point_sets
 from ..tools.kernel import GenKernel
 from ..tools.optim import LBFGS_optimization
-from ..tools.point_sets import decimate
 from ..tools.spec import defspec
 from .LDDMM import LDDMMModel
 from .registrations import LDDMMRegistration
+from .support import decimated_points, grid_points, merged_v2p_args, split_rows, warn_uncovered
 
 
 def data_distance(Kernel: GenKernel, x, y, w=None):
-    """RKHS distance between the data cloud x (weights 1/Nx) and the template y (weights 1/Ny,
-    or -w) -- PSR_standard.py:37-58:
-        L = sum_ij c_i c_j K(X_i, X_j),  X = (y, x)."""
+    """Squared RKHS distance between the data cloud x (mass 1/Nx per point) and the template
+    y (mass 1/Ny per point, or the weights w) -- PSR_standard.py:37-58:
+        |mu_x - mu_y|^2 = <mu_x, mu_x> + <mu_y, mu_y> - 2 <mu_y, mu_x>."""
     KB = Kernel.KBase
-    Nx = x.shape[0]
-    Ny = y.shape[0]
+    nx, ny = x.shape[0], y.shape[0]
+    xx = KB(x, x).sum() / nx ** 2
     if w is None:
-        return KB(x, x).sum() / Nx ** 2 + KB(y, y).sum() / Ny ** 2 - 2 * KB(y, x).sum() / (Nx * Ny)
-    KRS = Kernel.KRedScal
-    return (KB(x, x).sum() / Nx ** 2 + (KRS(y, y, w).flatten() * w).sum()
-            - 2 * (KB(y, x).flatten() * w).sum() / Nx)
+        return xx + KB(y, y).sum() / ny ** 2 - 2 * KB(y, x).sum() / (nx * ny)
+    yy = (Kernel.KRedScal(y, y, w).flatten() * w).sum()
+    return xx + yy - 2 * (KB(y, x).flatten() * w).sum() / nx
 
 
-def _acc_zero(spec):
-    # torch.tensor([0.0]) of the reference: float32, here on the computation device
+def _loss_acc(spec):
+    """The float32 one-element loss accumulator of the reference (torch.tensor([0.0]))."""
     return torch.zeros(1, dtype=torch.float32, device=spec["device"])
 
 
+def _per_structure(v, S, what):
+    """A value given once for every structure, or as a list of S values."""
+    if isinstance(v, list):
+        if len(v) != S:
+            raise ValueError(f"{what}: expected one entry per structure ({S}), got {len(v)}")
+        return list(v)
+    return [v] * S
+
+
 class MultiPSR_std:
-    """Base class (PSR_standard.py:67-357)."""
+    """K frames x S structures registered to S templates (PSR_standard.py:67-357).
+
+    Attributes (the reference's): x[k, s] data, y0[s] templates, y1[k, s] warped templates,
+    Nx, Ny, w0[s] template weights (or None), noise_std[s], shoot[k], regloss[k],
+    dataloss[k, s], E, ally0 (templates concatenated)."""
 
     def __init__(self, x, y_template, noise_std, DataKernel: GenKernel, template_weights=False,
                  dataspec=defspec, compspec=defspec):
         self.dataspec, self.compspec = dataspec, compspec
         self.DataKernel = DataKernel
         self.printstuff = True
-        x, self.K, self.S, self.D = read_point_sets(x)
-        if isinstance(y_template, torch.Tensor):
-            self.y0 = [y_template.clone().contiguous().detach().to(**self.dataspec) for _ in range(self.S)]
-        else:
-            if not isinstance(y_template, list) or len(y_template) != self.S:
-                raise ValueError("y_template should be a single point set (torch tensor), or a list with S point sets")
-            self.y0 = [y.clone().contiguous().detach().to(**self.dataspec) for y in y_template]
-        self.noise_std = noise_std if isinstance(noise_std, list) else [noise_std] * self.S
-        assert len(self.noise_std) == self.S
-        self.y1 = np.empty((self.K, self.S), dtype=object)
+        frames, self.K, self.S, self.D = read_point_sets(x)
+        if not isinstance(y_template, (torch.Tensor, list)):
+            raise ValueError("y_template: a point set (tensor) or a list of S point sets")
+        tpl = _per_structure(y_template, self.S, "y_template")
+        self.y0 = [t.detach().clone().contiguous().to(**dataspec) for t in tpl]
+        self.noise_std = _per_structure(noise_std, self.S, "noise_std")
         self.x = np.empty((self.K, self.S), dtype=object)
-        for s in range(self.S):
-            for k in range(self.K):
-                self.x[k, s] = x[k][s].contiguous().detach().to(**self.dataspec)
-                self.y1[k, s] = self.y0[s].clone().contiguous().detach().to(**self.dataspec)
-        self.Nx = np.array([[self.x[k, s].shape[0] for s in range(self.S)] for k in range(self.K)])
-        self.Ny = np.array([self.y0[s].shape[0] for s in range(self.S)])
-        self.ally0 = torch.cat(tuple(self.y0), dim=0).clone().to(**self.compspec).detach().contiguous()
+        self.y1 = np.empty((self.K, self.S), dtype=object)
+        for k in range(self.K):
+            for s in range(self.S):
+                self.x[k, s] = frames[k][s].detach().contiguous().to(**dataspec)
+                self.y1[k, s] = self.y0[s].clone()
+        self.Nx = np.array([[len(self.x[k, s]) for s in range(self.S)] for k in range(self.K)])
+        self.Ny = np.array([len(t) for t in self.y0])
+        self._refresh_ally0()
         self.template_weights = template_weights
-        if self.template_weights:
-            self.w0 = [torch.ones(int(self.Ny[s]), **self.compspec) / int(self.Ny[s]) for s in range(self.S)]
-        else:
-            self.w0 = [None] * self.S
+        self.w0 = ([torch.ones(int(n), **compspec) / int(n) for n in self.Ny] if template_weights
+                   else [None] * self.S)
         self.shoot = [None] * self.K
         self.regloss = [0] * self.K
         self.dataloss = np.zeros((self.K, self.S))
         for k in range(self.K):
             for s in range(self.S):
-                self.dataloss[k, s] = float(data_distance(self.DataKernel, self.x[k, s], self.y0[s],
-                                                          self.w0[s])) / self.noise_std[s] ** 2
-        self.E = sum(float(r) for r in self.regloss) + self.dataloss.sum().item()
+                self.dataloss[k, s] = self._data_term(k, s, self.y0[s])
+        self.E = self._energy()
 
     def __setstate__(self, state):
         self.__dict__.update(state)
         self.dataspec = defspec
         self.compspec = defspec
+
+    # ---- small pieces ---------------------------------------------------------------------
+    def _refresh_ally0(self):
+        self.ally0 = torch.cat(tuple(self.y0), dim=0).detach().clone().to(**self.compspec).contiguous()
+
+    def _data_term(self, k, s, y):
+        """dataloss[k, s] for the warped template y (a float)."""
+        return float(data_distance(self.DataKernel, self.x[k, s], y, self.w0[s])) / self.noise_std[s] ** 2
+
+    def _energy(self):
+        return sum(float(r) for r in self.regloss) + self.dataloss.sum().item()
+
+    def _set_energy(self, E):
+        if self.E is not None and E > self.E:
+            msg = "WARNING: measured increase in optimization energy ! Should not happen."
+            warnings.warn(msg)
+            print(msg)
+        self.E = E
 
     def get_template(self, s=0):
         return self.y0[s]
@@ -112,27 +136,25 @@ class MultiPSR_std:
             return LDDMMRegistration(self.LMi, self.q0, self.a0[k])
         raise NotImplementedError("AffinePSR_std is out of scope of difficp_amd")
 
+    # ---- optimisation steps ---------------------------------------------------------------
     def Template_opt(self, nmax=10, tol=1e-3, errthresh=1e8):
-        """Optimise each template y0[s] (and its weights) through all frames' registrations
-        (PSR_standard.py:226-257)."""
+        """Each template y0[s] (and its weights) optimised through all frames' registrations
+        (PSR_standard.py:226-257): loss = sum_k data_distance(x[k, s], phi_k(y0[s]), w0[s])."""
         for s in range(self.S):
+            regs = [self.Registration(k) for k in range(self.K)]
 
-            def lossfunc(y0s, ws):
-                L = _acc_zero(self.compspec)
-                for k in range(self.K):
-                    L += data_distance(self.DataKernel, self.x[k, s], self.Registration(k).apply(y0s), ws)
+            def loss(y0s, ws=None, s=s, regs=regs):
+                L = _loss_acc(self.compspec)
+                for k, reg in enumerate(regs):
+                    L += data_distance(self.DataKernel, self.x[k, s], reg.apply(y0s), ws)
                 return L
 
+            params = [self.y0[s], self.w0[s]] if self.template_weights else [self.y0[s]]
+            p, L, nsteps, change = LBFGS_optimization(params, loss, nmax=nmax, tol=tol, errthresh=errthresh)
+            self.y0[s] = p[0]
             if self.template_weights:
-                p, L, nsteps, change = LBFGS_optimization([self.y0[s], self.w0[s]], lossfunc, nmax=nmax,
-                                                          tol=tol, errthresh=errthresh)
-                self.y0[s] = p[0]
                 self.w0[s] = p[1]
-            else:
-                p, L, nsteps, change = LBFGS_optimization([self.y0[s]], lambda y0s: lossfunc(y0s, None),
-                                                          nmax=nmax, tol=tol, errthresh=errthresh)
-                self.y0[s] = p[0]
-            self.update_state(s=s, caller=self.Template_opt)
+            self.update_state(s=s, caller="Template_opt")
             if self.printstuff:
                 print(f"Template {s} : {nsteps} optim steps, loss={L:.4}, change={change:.4}.".ljust(70)
                       + f"Total energy = {self.E:.8}")
@@ -141,143 +163,110 @@ class MultiPSR_std:
         raise NotImplementedError("function Reg_opt must be written in derived classes.")
 
     def update_state(self, k=None, s=None, caller=None):
-        """Recompute warped templates, data losses, regloss, support points and E
-        (PSR_standard.py:269-318)."""
-        klist = range(self.K) if k is None else [k]
-        slist = range(self.S) if s is None else [s]
-        for kk in klist:
-            for ss in slist:
-                if caller != self.Reg_opt:
-                    self.y1[kk, ss] = self.Registration(kk).apply(self.y0[ss]).detach()
-                self.dataloss[kk, ss] = float(data_distance(self.DataKernel, self.x[kk, ss], self.y1[kk, ss],
-                                                            self.w0[ss])) / self.noise_std[ss] ** 2
+        """Bring y1, dataloss, regloss, the support and E up to date after a change
+        (PSR_standard.py:269-318).  caller: None (everything), "Reg_opt" (y1 already set by
+        the registration) or "Template_opt" (templates changed: support and momenta follow);
+        the reference's bound methods are accepted too."""
+        caller = getattr(caller, "__name__", caller)
+        ks = range(self.K) if k is None else [k]
+        ss = range(self.S) if s is None else [s]
+        for kk in ks:
+            for sn in ss:
+                if caller != "Reg_opt":
+                    self.y1[kk, sn] = self.Registration(kk).apply(self.y0[sn]).detach()
+                self.dataloss[kk, sn] = self._data_term(kk, sn, self.y1[kk, sn])
         if caller is None and isinstance(self, DiffPSR_std):
-            for kk in klist:
+            for kk in ks:
                 self.regloss[kk] = float(self.LMi.trajloss(self.Registration(kk).shoot(None)))
-        if caller == self.Template_opt:
-            self.ally0 = torch.cat(tuple(self.y0), dim=0).clone().to(**self.compspec).detach().contiguous()
+        if caller == "Template_opt":
+            self._refresh_ally0()
             if isinstance(self, DiffPSR_std):
-                q0_prev = self.q0
-                if self.support_scheme is None:
-                    self.q0 = self.ally0
-                    self.update_a0(q0_prev, rcond=1e-1)
-                elif self.support_scheme == "decim":
-                    self.set_support_scheme("decim", self.rho)
-        E = sum(float(r) for r in self.regloss) + self.dataloss.sum().item()
-        if self.E is not None and E > self.E:
-            warnings.warn("WARNING: measured increase in optimization energy ! Should not happen.")
-            print("WARNING: measured increase in optimization energy ! Should not happen.")
-        self.E = E
+                self._templates_moved()
+        self._set_energy(self._energy())
 
 
 class DiffPSR_std(MultiPSR_std):
-    """MultiPSR_std with LDDMM registrations (PSR_standard.py:364-566)."""
+    """MultiPSR_std with LDDMM registrations (PSR_standard.py:364-566): one support q0 for all
+    frames (the templates, or a scheme built from them), momenta a0[k] per frame."""
 
     def __init__(self, x, y_template, noise_std, LMi: LDDMMModel, DataKernel: GenKernel,
                  template_weights=False, dataspec=defspec, compspec=defspec, v2p_args=None):
         super().__init__(x, y_template, noise_std, DataKernel=DataKernel, template_weights=template_weights,
                          dataspec=dataspec, compspec=compspec)
         if LMi.Kernel.spec != compspec:
-            raise ValueError("Spec (dtype+device) error : LDDMMmodel 'spec' and diffPSR 'compspec' "
-                             "attributes should be the same")
+            raise ValueError("Spec (dtype+device) error : the LDDMM model's spec and compspec differ")
         self.LMi = LMi
-        self.v2p_args = dict(v2p_args or {})   # as DiffPSR (core/PSR.py): None = reference defaults
+        self.v2p_args = dict(v2p_args or {})   # as core/PSR.DiffPSR: None = the reference's v2p defaults
         self.support_scheme = None
+        self.rho = None
         self.q0 = self.ally0
         self.a0 = [None] * self.K
         self.initialize_a0()
 
     def initialize_a0(self, **v2p_args):
-        """a0 at zero speeds (PSR_standard.py:422-428)."""
-        v2p_args = v2p_args or self.v2p_args
-        for k in range(self.K):
-            v0 = torch.zeros(self.q0.shape, **self.compspec)
-            self.a0[k] = self.LMi.v2p(self.q0, v0, **v2p_args)
+        """Momenta of zero initial speed (PSR_standard.py:422-428)."""
+        args = v2p_args or self.v2p_args
+        zero = torch.zeros(self.q0.shape, **self.compspec)
+        self.a0 = [self.LMi.v2p(self.q0, zero, **args) for _ in range(self.K)]
 
     def update_a0(self, q0_prev, a0_prev=None, **v2p_args):
-        """Project the previous field on the new support (PSR_standard.py:430-443)."""
-        if self.v2p_args and not v2p_args.get("version"):
-            v2p_args = {**self.v2p_args, **{k: v for k, v in v2p_args.items() if k != "rcond"}}
-        if a0_prev is None:
-            a0_prev = self.a0
-        for k in range(self.K):
-            v0 = self.LMi.v(self.q0, q0_prev, a0_prev[k])
-            self.a0[k] = self.LMi.v2p(self.q0, v0, **v2p_args)
+        """Momenta on the current support that keep each frame's initial velocity field
+        (PSR_standard.py:430-443)."""
+        args = merged_v2p_args(self.v2p_args, v2p_args)
+        prev = self.a0 if a0_prev is None else a0_prev
+        self.a0 = [self.LMi.v2p(self.q0, self.LMi.v(self.q0, q0_prev, a), **args) for a in prev]
 
-    def set_support_scheme(self, scheme="decim", rho=1.0, xticks=None, yticks=None, q0=None):
-        """Support points of the template (PSR_standard.py:445-503): "decim" (device greedy
-        decimation, point_sets.py:102-133), "grid" (2D) or "custom"."""
-        self.rho = rho
+    def _templates_moved(self):
+        """After Template_opt: the dense support follows the templates; a decimated one is
+        rebuilt from them (PSR_standard.py:305-313)."""
+        if self.support_scheme is None:
+            q0_prev, self.q0 = self.q0, self.ally0
+            self.update_a0(q0_prev, rcond=1e-1)
+        elif self.support_scheme == "decim":
+            self.set_support_scheme("decim", self.rho)
+
+    def set_support_scheme(self, scheme="decim", rho=1.0, xticks=None, yticks=None, q0=None, zticks=None):
+        """Support points built from the templates (PSR_standard.py:445-503): "decim", "grid"
+        (2D as the reference, and 3D; core/support.py) or "custom"."""
         Rcover = rho * self.LMi.Kernel.sigma
-        self.support_scheme = scheme
-        q0_prev = self.q0
         if scheme == "decim":
-            supp_ids = [decimate(self.y0[s].to(**self.compspec), Rcover)[0] for s in range(self.S)]
-            Ndecim = sum(len(i) for i in supp_ids)
+            q_new, ids = decimated_points(self.y0, Rcover, self.compspec)
             if self.printstuff:
-                print(f"Decimation : {Ndecim} support points ({Ndecim / sum(self.Ny):.0%} of original sets)")
-            self.q0 = torch.cat(tuple(self.y0[s][supp_ids[s]] for s in range(self.S)),
-                                dim=0).to(**self.compspec).contiguous()
+                n = sum(len(i) for i in ids)
+                print(f"Decimation : {n} support points ({n / sum(self.Ny):.0%} of original sets)")
         elif scheme == "grid":
-            if self.D != 2:
-                raise ValueError("grid support scheme is 2D only (as in the reference)")
-            if xticks is None or yticks is None:
-                # get_bounds(*y0, relmargin=0.1) (visualization/visu.py:35-50)
-                ys = [a.detach().cpu() for a in self.y0 if len(a) > 0]
-                mins = torch.cat(tuple(a.min(0).values.reshape(1, 2) for a in ys), 0).min(0).values.numpy()
-                maxs = torch.cat(tuple(a.max(0).values.reshape(1, 2) for a in ys), 0).max(0).values.numpy()
-                gmin = (1 + 0.1) * mins - 0.1 * maxs
-                gmax = (1 + 0.1) * maxs - 0.1 * mins
-                xmin, xmax, ymin, ymax = gmin[0], gmax[0], gmin[1], gmax[1]
-            if xticks is None:
-                xticks = np.arange(xmin - Rcover / 2, xmax + Rcover / 2, Rcover)
-            if yticks is None:
-                yticks = np.arange(ymin - Rcover / 2, ymax + Rcover / 2, Rcover)
-            gp = np.stack(np.meshgrid(xticks, yticks), axis=2)
-            self.q0 = torch.tensor(gp.reshape((-1, 2), order="F"), **self.compspec).contiguous()
+            ticks = (xticks, yticks) if self.D == 2 else (xticks, yticks, zticks)
+            q_new = grid_points(self.y0, Rcover, self.D, self.compspec, ticks)
         elif scheme == "custom":
             assert q0 is not None, "For a custom support scheme, please specify argument q0"
-            self.q0 = q0.clone().detach().to(**self.compspec).contiguous()
+            q_new = q0.detach().clone().to(**self.compspec).contiguous()
         else:
-            raise ValueError(f"Unknown value of support point scheme : {scheme}. Only values available "
-                             "are 'decim', 'grid' and 'custom'.")
+            raise ValueError(f"Unknown support point scheme {scheme!r} (available: 'decim', 'grid', 'custom')")
+        self.rho, self.support_scheme = rho, scheme
+        q0_prev, self.q0 = self.q0, q_new
         self.update_a0(q0_prev, rcond=1e-2)
 
     def Reg_opt(self, nmax=10, tol=1e-3):
-        """LDDMM registration of the template to each frame (PSR_standard.py:507-566)."""
+        """Each frame's LDDMM registration of the templates (PSR_standard.py:507-566):
+        loss = sum_s data_distance(x[k, s], y1 rows of structure s, w0[s]) / noise_std[s]^2."""
         for k in range(self.K):
 
-            def dataloss_func(y):
-                L = _acc_zero(self.compspec)
-                last = 0
-                for s in range(self.S):
-                    first, last = last, last + int(self.Ny[s])
-                    L += data_distance(self.DataKernel, self.x[k, s], y[first:last], self.w0[s]) / self.noise_std[s] ** 2
+            def dataloss(y, k=k):
+                L = _loss_acc(self.compspec)
+                for s, ys in enumerate(split_rows(y, self.Ny)):
+                    L += data_distance(self.DataKernel, self.x[k, s], ys, self.w0[s]) / self.noise_std[s] ** 2
                 return L
 
-            if self.support_scheme is None:
-                self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
-                    self.LMi.Optimize(dataloss_func, self.q0, self.a0[k], tol=tol, nmax=nmax)
-                ally1k = self.shoot[k][-1][0]
-            else:
-                self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
-                    self.LMi.Optimize(dataloss_func, self.q0, self.a0[k], self.ally0, tol=tol, nmax=nmax)
-                ally1k = self.shoot[k][-1][-1]
-            last = 0
-            for s in range(self.S):
-                first, last = last, last + int(self.Ny[s])
-                self.y1[k, s] = ally1k[first:last].to(**self.dataspec)
-            if self.support_scheme is not None:
-                Rcoverwarning = 2.0
-                for t in range(len(self.shoot[k])):
-                    qk, yk = self.shoot[k][t][0], self.shoot[k][t][-1]
-                    unc = self.LMi.Kernel.check_coverage(yk, qk, Rcoverwarning)
-                    if unc.any():
-                        print(f"WARNING : shooting, time step {t} : {unc.sum()} uncovered points "
-                              f"({unc.sum() / yk.shape[0]:.2%})")
-                        warnings.warn("Uncovered points during LDDMM shooting. Choose a smaller rho when "
-                                      "defining the support scheme.", RuntimeWarning)
-            self.update_state(k=k, caller=self.Reg_opt)
+            dense = self.support_scheme is None
+            extra = () if dense else (self.ally0,)
+            self.a0[k], self.shoot[k], self.regloss[k], datal, isteps, change = \
+                self.LMi.Optimize(dataloss, self.q0, self.a0[k], *extra, tol=tol, nmax=nmax)
+            warped = self.shoot[k][-1][0] if dense else self.shoot[k][-1][-1]
+            for s, ys in enumerate(split_rows(warped, self.Ny)):
+                self.y1[k, s] = ys.to(**self.dataspec)
+            if not dense:
+                warn_uncovered(self.LMi.Kernel, self.shoot[k])
+            self.update_state(k=k, caller="Reg_opt")
             if self.printstuff:
                 print(f"Frame {k} : {isteps} optim steps, loss={float(self.regloss[k]) + float(datal):.4}, "
                       f"change={change:.4}.".ljust(70) + f"Total energy = {self.E:.8}")

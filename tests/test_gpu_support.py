@@ -1,0 +1,88 @@
+"""Support schemes on the device: the 3D grid support of DiffPSR (the
+reference's grid is 2D only, PSR.py:472-482 -- parity-unpinned: support-point count, coverage,
+free-energy monotonicity and bitwise determinism are checked), and DiffPSR_std with
+decimated / grid supports and template weights (PSR_standard.py:445-503; the reference's
+golden trace covers the dense support only)."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _grid_run(dev):
+    from difficp_amd import workloads
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    spec = {"device": dev, "dtype": torch.float32}
+    x = [f.to(dev) for f in workloads.atlas_frames(3, 3000, seed=5)]
+    G = GaussianMixtureUnif(torch.zeros(64, 3), spec=spec)
+    G.to_optimize = {"mu": True, "sigma": True, "w": True, "eta0": False}
+    LM = LDDMMModel(sigma=0.1, D=3, lambd=1e3, version="hybrid", scheme="Euler", nt=10, spec=spec)
+    torch.manual_seed(0)
+    P = DiffPSR(x, G, LM, dataspec=spec, compspec=spec)
+    P.printstuff = False
+    P.reinitialize_GMM()
+    P.set_support_scheme("grid", rho=1.0)
+    fes = [P.FE]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)        # uncovered points would raise
+        for _ in range(2):
+            P.GMM_opt(max_iterations=10, tol=1e-3)
+            fes.append(P.FE)
+            P.Reg_opt(nmax=1, tol=1e-3)
+            fes.append(P.FE)
+    return P, fes
+
+
+def test_grid_support_3d_diffpsr(dev):
+    from difficp_amd.core.support import bounds_with_margin
+    P, fes = _grid_run(dev)
+    lo, hi = bounds_with_margin(P.allx0, 3)
+    R = 0.1
+    n = np.prod([len(np.arange(lo[d] - R / 2, hi[d] + R / 2, R)) for d in range(3)])
+    assert P.q0[0].shape == (n, 3)
+    for f0, f1 in zip(fes[:-1], fes[1:]):
+        assert f1 <= f0 + 1e-6 * abs(f0), fes
+    P2, fes2 = _grid_run(dev)
+    assert fes2 == fes
+    for k in range(3):
+        assert torch.equal(P.a0[k], P2.a0[k]) and torch.equal(P.x1[k, 0], P2.x1[k, 0])
+
+
+@pytest.mark.parametrize("scheme", ["decim", "grid"])
+@pytest.mark.parametrize("weights", [False, True])
+def test_psr_std_support_schemes(dev, scheme, weights):
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR_standard import DiffPSR_std
+    from difficp_amd.tools.kernel import GaussKernel
+    from difficp_amd.tools.point_sets import decimate
+    spec = {"device": dev, "dtype": torch.float32}
+    g = torch.Generator().manual_seed(13)
+    t = torch.linspace(0, 2 * np.pi, 121)[:-1]
+    y0 = torch.stack([0.5 + 0.3 * torch.cos(t), 0.5 + 0.2 * torch.sin(t)], 1)
+    xs = []
+    for k in range(3):
+        tk = torch.rand(200, generator=g) * 2 * np.pi
+        xs.append((torch.stack([0.5 + (0.3 + 0.03 * k) * torch.cos(tk), 0.5 + (0.2 - 0.02 * k) * torch.sin(tk)], 1)
+                   + 0.01 * torch.randn(200, 2, generator=g)).to(dev))
+    DK = GaussKernel(0.1, 2, spec=spec)
+    LM = LDDMMModel(sigma=0.2, D=2, lambd=2.0, version="classic", scheme="Euler", nt=10, spec=spec)
+    P = DiffPSR_std(xs, y0.to(dev), 0.05, LM, DK, template_weights=weights, dataspec=spec, compspec=spec)
+    P.printstuff = False
+    P.set_support_scheme(scheme, rho=1.0)
+    if scheme == "decim":
+        assert P.q0.shape[0] == len(decimate(y0.to(dev), 0.2)[0])
+    Es = [P.E]
+    for _ in range(2):
+        P.Reg_opt(nmax=2, tol=1e-4)
+        Es.append(P.E)
+        P.Template_opt(nmax=2, tol=1e-4)
+        Es.append(P.E)
+    assert Es[-1] < Es[0]
+    assert all(np.isfinite(Es))
+    if weights:
+        assert P.w0[0].shape == (120,)
