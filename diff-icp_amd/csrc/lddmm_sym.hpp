@@ -69,7 +69,10 @@ inline SymGeom sym_geom(int64_t M, int nparts = 1) {
   g.nQ = (g.nG + kSymQ - 1) / kSymQ;
   int L = sym_L();
   if (L <= 0) {
-    L = 4;
+    // L = 8 where the chip stays full with >= 4096 workgroups (100k points: 9.6k): time
+    // within 0.3% of L = 4 (r02_ab_vjp_symL_100k.json) and ~25% fewer partial slots written
+    // and merged; otherwise L = 4, halved until a launch has >= 2048 workgroups
+    L = (double)g.nQ * g.nG / (2.0 * 8 * nparts) >= 4096.0 ? 8 : 4;
     while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0) L /= 2;
   }
   g.L = L;

@@ -16,6 +16,8 @@ from difficp_amd import _lib  # noqa: E402
 
 def main():
     M = int(os.environ.get("PMC_M", "100000"))
+    if os.environ.get("PMC_SYM_L"):   # A/B of the VJP's column groups per workgroup
+        _lib.set_option("sym_L", int(os.environ["PMC_SYM_L"]))
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     q = torch.rand(M, 3, device=dev)
