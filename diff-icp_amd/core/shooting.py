@@ -174,10 +174,17 @@ class ShootCache:
             e = self._d.get(key)
             if e is not None:
                 self._d.move_to_end(key)
-        if (e is None or e["params"] != params or not torch.equal(e["q0c"], q0)
+        # p0 first: it is what differs between the closures of one L-BFGS run (each
+        # torch.equal is a device round trip).  The L-BFGS parameter is updated in place, so
+        # the same storage at a newer version is a miss without comparing (at worst a false
+        # miss -- a recomputation -- never a stale hit)
+        if e is not None and p0.data_ptr() == e["p0src"][0] and p0._version != e["p0src"][1]:
+            self.misses += 1
+            return None
+        if (e is None or e["params"] != params or (e["x0"] is None) != (x0 is None)
                 or not torch.equal(e["p0"], p0)
-                or (e["x0"] is None) != (x0 is None)
-                or (x0 is not None and not torch.equal(e["x0"], x0))):
+                or (x0 is not None and not torch.equal(e["x0"], x0))
+                or not torch.equal(e["q0c"], q0)):
             self.misses += 1
             return None
         self.hits += 1
@@ -191,7 +198,7 @@ class ShootCache:
         return e
 
     def store(self, q0, p0, x0, params, outs, saved):
-        e = {"q0": q0, "q0c": outs[0][0], "p0": p0.detach().clone(),
+        e = {"q0": q0, "q0c": outs[0][0], "p0": p0.detach().clone(), "p0src": (p0.data_ptr(), p0._version),
              "x0": None if x0 is None else x0.detach().clone(),
              "params": params, "outs": outs, "saved": saved}
         e["nbytes"] = _nbytes(list(outs) + list(saved) + [e["p0"], e["x0"]])

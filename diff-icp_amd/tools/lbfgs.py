@@ -20,11 +20,25 @@ D = diag(S^T Y).  Per iteration: one stacked GEMV [S; Y] v, two m x m triangular
 pair).  Results equal torch's two-loop up to floating-point rounding.  The "GEMVs" are torch
 elementwise products + reductions, not BLAS calls: rocBLAS allows atomics by default, and the
 row-split multi-GPU mode needs bitwise-identical iterates on every rank.
+
+Host round trips.  torch's step and `_strong_wolfe` keep the line-search scalars (gtd, the
+step t after an interpolation, the gradient / step norms) as 0-d device tensors, so every
+comparison is a device-to-host synchronisation -- ~9-10 per L-BFGS iteration, each leaving
+the GPU idle while the host decides (profiles/r03_timeline_summary.json).  Here the same
+control flow runs on host scalars: the values torch keeps as 0-d tensors are numpy scalars
+of the parameters' dtype (numpy's weak-Python-scalar promotion, NEP 50, is torch's), the
+loss values Python floats as in torch, so every decision and step length is bit-identical to
+torch.optim.LBFGS's.  Each function evaluation reads (loss, g.d, max|g|) in ONE transfer, an
+iteration adds one read of (y.s, y.y) and one of (g.d, max|d| [, sum|g|]) -- 3 round trips per
+iteration.  The loss of every evaluation is passed to `on_loss(loss)` (if set) while the
+parameters still hold the evaluated point (tools/optim.py tracks the best point with it).
 """
 from __future__ import annotations
 
+import math
+
+import numpy as np
 import torch
-from torch.optim.lbfgs import _strong_wolfe
 
 
 def _rowdots(A, v):
@@ -89,6 +103,132 @@ class CompactLBFGS(torch.optim.LBFGS):
         return v * gamma + (SY_ * coef[:, None]).sum(0)
 
     # ------------------------------------------------------------------------------
+    on_loss = None   # callback(loss: float) after every function evaluation
+
+    def _read(self, *ts):
+        """Device scalars -> host floats in one transfer (float64: exact for either dtype)."""
+        return torch.stack([t.detach().reshape(()).to(torch.float64) for t in ts]).tolist()
+
+    def _dt(self, *vals):
+        """Host stand-ins of torch's 0-d tensors: numpy scalars of the parameters' dtype."""
+        dt = np.float32 if self._params[0].dtype == torch.float32 else np.float64
+        return [dt(v) for v in vals]
+
+    def _evaluate(self, closure, d=None):
+        """One function evaluation at the current parameters: (loss, flat_grad, g.d, max|g|);
+        g.d is None without d."""
+        L = closure()
+        flat_grad = self._gather_flat_grad()
+        if d is None:
+            loss, gmax = self._read(L, flat_grad.abs().max())
+            gtd = None
+            (gmax,) = self._dt(gmax)
+        else:
+            loss, gtd, gmax = self._read(L, flat_grad.dot(d), flat_grad.abs().max())
+            gtd, gmax = self._dt(gtd, gmax)
+        if self.on_loss is not None:
+            self.on_loss(loss)
+        return loss, flat_grad, gtd, gmax
+
+    def _directional_eval(self, closure, x, t, d):
+        self._add_grad(float(t), d)
+        out = self._evaluate(closure, d)
+        self._set_param(x)
+        return out
+
+    @staticmethod
+    def _cubic_interpolate(x1, f1, g1, x2, f2, g2, bounds=None):
+        """torch.optim.lbfgs._cubic_interpolate on host scalars: the same expression, with
+        numpy scalars where torch has 0-d tensors (and Python floats where it has them)."""
+        if bounds is not None:
+            xmin_bound, xmax_bound = bounds
+        else:
+            xmin_bound, xmax_bound = (x1, x2) if x1 <= x2 else (x2, x1)
+        with np.errstate(all="ignore"):
+            d1 = g1 + g2 - 3 * (f1 - f2) / (x1 - x2)
+            d2_square = d1 ** 2 - g1 * g2
+            if d2_square >= 0:
+                d2 = np.sqrt(d2_square)
+                if x1 <= x2:
+                    min_pos = x2 - (x2 - x1) * ((g2 + d2 - d1) / (g2 - g1 + 2 * d2))
+                else:
+                    min_pos = x1 - (x1 - x2) * ((g1 + d2 - d1) / (g1 - g2 + 2 * d2))
+                return min(max(min_pos, xmin_bound), xmax_bound)
+            return (xmin_bound + xmax_bound) / 2.0
+
+    def _strong_wolfe(self, closure, x, t, d, f, g, gtd, gmax, d_norm, c1=1e-4, c2=0.9,
+                      tolerance_change=1e-9, max_ls=25):
+        """torch.optim.lbfgs._strong_wolfe (same bracketing / zoom control flow) on host
+        scalars; returns (f, g, t, evaluations, max|g|) of the accepted point."""
+        interp = self._cubic_interpolate
+        g = g.clone(memory_format=torch.contiguous_format)
+        f_new, g_new, gtd_new, gmax_new = self._directional_eval(closure, x, t, d)
+        ls_func_evals = 1
+        t_prev, f_prev, g_prev, gtd_prev, gmax_prev = 0, f, g, gtd, gmax
+        done = False
+        ls_iter = 0
+        while ls_iter < max_ls:
+            if f_new > (f + c1 * t * gtd) or (ls_iter > 1 and f_new >= f_prev):
+                bracket, bracket_f = [t_prev, t], [f_prev, f_new]
+                bracket_g = [g_prev, g_new.clone(memory_format=torch.contiguous_format)]
+                bracket_gtd, bracket_gmax = [gtd_prev, gtd_new], [gmax_prev, gmax_new]
+                break
+            if abs(gtd_new) <= -c2 * gtd:
+                bracket, bracket_f, bracket_g, bracket_gmax = [t], [f_new], [g_new], [gmax_new]
+                done = True
+                break
+            if gtd_new >= 0:
+                bracket, bracket_f = [t_prev, t], [f_prev, f_new]
+                bracket_g = [g_prev, g_new.clone(memory_format=torch.contiguous_format)]
+                bracket_gtd, bracket_gmax = [gtd_prev, gtd_new], [gmax_prev, gmax_new]
+                break
+            min_step = t + 0.01 * (t - t_prev)
+            max_step = t * 10
+            tmp = t
+            t = interp(t_prev, f_prev, gtd_prev, t, f_new, gtd_new, bounds=(min_step, max_step))
+            t_prev, f_prev, gtd_prev, gmax_prev = tmp, f_new, gtd_new, gmax_new
+            g_prev = g_new.clone(memory_format=torch.contiguous_format)
+            f_new, g_new, gtd_new, gmax_new = self._directional_eval(closure, x, t, d)
+            ls_func_evals += 1
+            ls_iter += 1
+        if ls_iter == max_ls:
+            bracket, bracket_f, bracket_g, bracket_gmax = [0, t], [f, f_new], [g, g_new], [gmax, gmax_new]
+        insuf_progress = False
+        low_pos, high_pos = (0, 1) if bracket_f[0] <= bracket_f[-1] else (1, 0)
+        while not done and ls_iter < max_ls:
+            if abs(bracket[1] - bracket[0]) * d_norm < tolerance_change:
+                break
+            t = interp(bracket[0], bracket_f[0], bracket_gtd[0], bracket[1], bracket_f[1], bracket_gtd[1])
+            eps = 0.1 * (max(bracket) - min(bracket))
+            if min(max(bracket) - t, t - min(bracket)) < eps:
+                if insuf_progress or t >= max(bracket) or t <= min(bracket):
+                    t = max(bracket) - eps if abs(t - max(bracket)) < abs(t - min(bracket)) else min(bracket) + eps
+                    insuf_progress = False
+                else:
+                    insuf_progress = True
+            else:
+                insuf_progress = False
+            f_new, g_new, gtd_new, gmax_new = self._directional_eval(closure, x, t, d)
+            ls_func_evals += 1
+            ls_iter += 1
+            if f_new > (f + c1 * t * gtd) or f_new >= bracket_f[low_pos]:
+                bracket[high_pos], bracket_f[high_pos] = t, f_new
+                bracket_g[high_pos] = g_new.clone(memory_format=torch.contiguous_format)
+                bracket_gtd[high_pos], bracket_gmax[high_pos] = gtd_new, gmax_new
+                low_pos, high_pos = (0, 1) if bracket_f[0] <= bracket_f[1] else (1, 0)
+            else:
+                if abs(gtd_new) <= -c2 * gtd:
+                    done = True
+                elif gtd_new * (bracket[high_pos] - bracket[low_pos]) >= 0:
+                    bracket[high_pos], bracket_f[high_pos] = bracket[low_pos], bracket_f[low_pos]
+                    bracket_g[high_pos], bracket_gtd[high_pos] = bracket_g[low_pos], bracket_gtd[low_pos]
+                    bracket_gmax[high_pos] = bracket_gmax[low_pos]
+                bracket[low_pos], bracket_f[low_pos] = t, f_new
+                bracket_g[low_pos] = g_new.clone(memory_format=torch.contiguous_format)
+                bracket_gtd[low_pos], bracket_gmax[low_pos] = gtd_new, gmax_new
+        return (bracket_f[low_pos], bracket_g[low_pos], bracket[low_pos], ls_func_evals,
+                bracket_gmax[low_pos])
+
     @torch.no_grad()
     def step(self, closure):  # noqa: C901 -- mirrors torch.optim.LBFGS.step
         if len(self.param_groups) != 1:
@@ -101,19 +241,18 @@ class CompactLBFGS(torch.optim.LBFGS):
         tolerance_grad = group["tolerance_grad"]
         tolerance_change = group["tolerance_change"]
         line_search_fn = group["line_search_fn"]
+        if line_search_fn not in (None, "strong_wolfe"):
+            raise RuntimeError("only 'strong_wolfe' is supported")
 
         state = self.state[self._params[0]]
         state.setdefault("func_evals", 0)
         state.setdefault("n_iter", 0)
 
-        orig_loss = closure()
-        loss = float(orig_loss)
+        loss, flat_grad, _, gmax = self._evaluate(closure)
+        orig_loss = loss
         current_evals = 1
         state["func_evals"] += 1
-
-        flat_grad = self._gather_flat_grad()
-        opt_cond = flat_grad.abs().max() <= tolerance_grad
-        if opt_cond:
+        if gmax <= tolerance_grad:
             return orig_loss
 
         d = state.get("d")
@@ -134,11 +273,11 @@ class CompactLBFGS(torch.optim.LBFGS):
             else:
                 y = flat_grad.sub(prev_flat_grad)
                 s = d.mul(t)
-                ys = y.dot(s)
+                ys, yy = self._dt(*self._read(y.dot(s), y.dot(y)))
                 if ys > 1e-10:
                     self._hist_push(s, y)
-                    H_diag = ys / y.dot(y)
-                d = self._hist_apply(flat_grad.neg(), H_diag)
+                    H_diag = ys / yy
+                d = self._hist_apply(flat_grad.neg(), H_diag if isinstance(H_diag, int) else float(H_diag))
 
             if prev_flat_grad is None:
                 prev_flat_grad = flat_grad.clone(memory_format=torch.contiguous_format)
@@ -146,36 +285,30 @@ class CompactLBFGS(torch.optim.LBFGS):
                 prev_flat_grad.copy_(flat_grad)
             prev_loss = loss
 
-            if state["n_iter"] == 1:
-                t = min(1.0, 1.0 / flat_grad.abs().sum()) * lr
+            first = state["n_iter"] == 1
+            if first:
+                gtd, d_norm, gsum = self._dt(*self._read(flat_grad.dot(d), d.abs().max(),
+                                                         flat_grad.abs().sum()))
+                t = min(1.0, 1.0 / gsum) * lr
             else:
+                gtd, d_norm = self._dt(*self._read(flat_grad.dot(d), d.abs().max()))
                 t = lr
-
-            gtd = flat_grad.dot(d)
             if gtd > -tolerance_change:
                 break
 
             ls_func_evals = 0
             if line_search_fn is not None:
-                if line_search_fn != "strong_wolfe":
-                    raise RuntimeError("only 'strong_wolfe' is supported")
                 x_init = self._clone_param()
-
-                def obj_func(x, t, d):
-                    return self._directional_evaluate(closure, x, t, d)
-
-                loss, flat_grad, t, ls_func_evals = _strong_wolfe(
-                    obj_func, x_init, t, d, loss, flat_grad, gtd, max_ls=max_eval - current_evals)
-                self._add_grad(t, d)
-                opt_cond = flat_grad.abs().max() <= tolerance_grad
+                loss, flat_grad, t, ls_func_evals, gmax = self._strong_wolfe(
+                    closure, x_init, t, d, loss, flat_grad, gtd, gmax, d_norm, max_ls=max_eval - current_evals)
+                self._add_grad(float(t), d)
+                opt_cond = gmax <= tolerance_grad
             else:
-                self._add_grad(t, d)
+                self._add_grad(float(t), d)
+                opt_cond = False
                 if n_iter != max_iter:
-                    with torch.enable_grad():
-                        loss = closure()
-                    loss = float(loss)
-                    flat_grad = self._gather_flat_grad()
-                    opt_cond = flat_grad.abs().max() <= tolerance_grad
+                    loss, flat_grad, _, gmax = self._evaluate(closure)
+                    opt_cond = gmax <= tolerance_grad
                     ls_func_evals = 1
 
             current_evals += ls_func_evals
@@ -187,7 +320,8 @@ class CompactLBFGS(torch.optim.LBFGS):
                 break
             if opt_cond:
                 break
-            if d.mul(t).abs().max() <= tolerance_change:
+            # max|t d| = |t| max|d| in the parameters' dtype (rounding is monotone)
+            if abs(self._dt(t)[0]) * d_norm <= tolerance_change:
                 break
             if abs(loss - prev_loss) < tolerance_change:
                 break

@@ -31,22 +31,26 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator
     optimizer = CompactLBFGS(p, max_iter=20, max_eval=100, history_size=100,
                              line_search_fn="strong_wolfe")
     iter_L, best_L, best_p = [], math.inf, None
+    optimizer.on_loss = lambda Ld: record(Ld)
 
     def closure():
-        nonlocal best_L, best_p
         optimizer.zero_grad()
         L = lossfunc(*p)
         # backward is queued BEFORE the host reads the loss (optim.py:41-47 reads it first): the
         # gradient does not depend on the read and p is not modified by backward, so results are
         # unchanged, but the host no longer drains the stream between the forward shooting and
-        # its adjoint -- the backward's host-side setup overlaps the forward's kernels
+        # its adjoint.  The loss itself is read by the optimizer together with the line
+        # search's scalars (one transfer) and handed to record() below.
         L.backward()
-        Ld = L.detach().item()
+        return L
+
+    def record(Ld):
+        # optim.py:39-45 (iter_L, best_p), while p still holds the evaluated point
+        nonlocal best_L, best_p
         iter_L.append(Ld)
         if Ld < best_L:
             best_L = Ld
             best_p = [a.clone().detach() for a in p]
-        return L
 
     i, keepOn, L = 0, True, math.inf
     change = None
@@ -81,6 +85,7 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator
             p = [a.detach().requires_grad_(True) for a in p]
             optimizer = CompactLBFGS(p, max_iter=20, max_eval=100, history_size=100,
                                      line_search_fn=None)
+            optimizer.on_loss = lambda Ld: record(Ld)
         else:
             changes = [((a - a_prev) ** 2).mean().sqrt().detach().cpu().numpy()
                        for a, a_prev in zip(p, p_prev)]

@@ -38,6 +38,27 @@ def main():
            "span_ms": round((t1 - t0) / 1e6, 1), "device_busy_ms": round(busy / 1e6, 1),
            "hot_kernels_ms": round(hot / 1e6, 1), "other_kernels_ms": round((busy - hot) / 1e6, 1),
            "idle_gaps_ms": round(gaps / 1e6, 1), "kernels": len(win)}
+    # where the idle time is: gap histogram and the kernel boundaries of the largest gaps
+    gl, last, prev = [], t0, "(window start)"
+    for s, e, n in win:
+        if s > last:
+            gl.append((s - last, prev, n))
+        if e > last:
+            last, prev = e, n
+    short = lambda n: n.split("(")[0][-60:]
+    edges = [(0, 10e3), (10e3, 50e3), (50e3, 200e3), (200e3, 1e6), (1e6, 1e12)]
+    out["gap_histogram_ns"] = {f"{int(a)}-{int(b) if b < 1e12 else 'inf'}": {
+        "count": sum(1 for g, _, _ in gl if a <= g < b),
+        "ms": round(sum(g for g, _, _ in gl if a <= g < b) / 1e6, 2)} for a, b in edges}
+    ctx = {}
+    for g, p, n in gl:
+        if g >= 50e3:
+            k = f"{short(p)} -> {short(n)}"
+            c = ctx.setdefault(k, [0, 0.0])
+            c[0] += 1
+            c[1] += g / 1e6
+    out["gaps_over_50us_by_boundary"] = {k: {"count": v[0], "ms": round(v[1], 2)}
+                                         for k, v in sorted(ctx.items(), key=lambda kv: -kv[1][1])[:15]}
     print(json.dumps(out, indent=1))
 
 
