@@ -129,3 +129,51 @@ def test_rowsplit_two_set_on_gpu(dev):
         assert np.abs(x1 - single["x1"].numpy()).max() < 1e-3
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])
+
+
+def _worker_rccl(port, q):
+    """World-1 RCCL ("nccl") group on cuda:0: the collective helpers of the row split and of the
+    GMM statistics exchange run through RCCL itself (a 1-GPU box cannot host two RCCL ranks),
+    then a two-set iteration inside the RCCL group (the split disengages at W = 1)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from difficp_amd.core.rowsplit import RowSplit
+        from difficp_amd.core import GMM
+        rs = RowSplit()
+        assert rs._gather_base and rs.world == 1
+        t = torch.arange(12, dtype=torch.float32, device="cuda:0").view(4, 3)
+        checks = {
+            "all_gather": torch.equal(rs.all_gather(t.view(-1)), t.view(-1)),
+            "sum_ordered": torch.equal(rs.sum_ordered(t), t),
+            "all_reduce": torch.equal(rs.all_reduce_(t.clone()), t),
+            "gather_into": torch.equal(rs.gather_into(torch.empty_like(t), t), t),
+            "check_identical": rs.check_identical(t) is None and rs.verified_calls == 1,
+            "gather_rows": torch.equal(rs.gather_rows([t], 4)[0][0], t),
+            "gmm_gather": torch.equal(GMM._gather_rows(t, True)[0], t),
+            "comm_device": GMM._comm_device().type == "cuda",
+        }
+        res = _two_set(True)
+        q.put((checks, res["FE"], res["x1"].numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rowsplit_rccl_world1(dev):
+    """The RCCL code paths (all_gather_into_tensor, all_reduce, the verify checksum) execute on
+    the device, and an iteration run inside an RCCL group matches the plain one."""
+    import numpy as np
+    single = _two_set(False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl, args=(_free_port(), q))
+    p.start()
+    checks, fe, x1 = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert all(checks.values()), checks
+    assert abs(fe - single["FE"]) < 1e-5 * abs(single["FE"]), (fe, single["FE"])
+    assert np.abs(x1 - single["x1"].numpy()).max() < 1e-3

@@ -18,7 +18,8 @@ import sys
 NAMES = {"sym_bwd_pk_kernel": "ode_self_bwd", "sym_bwd_kernel": "ode_self_bwd", "sym_merge_kernel": "sym_merge",
          "OpOdeSelfBwd": "ode_self_bwd_ordered", "OpOdeSelfFwd": "ode_self_fwd",
          "OpGmmE": "gmm_estep", "OpGmmM": "gmm_mstep", "OpGmmTargets": "gmm_targets",
-         "merge_slabs": "merge_slabs", "lse_finalize": "lse_finalize"}
+         "merge_slabs": "merge_slabs", "lse_finalize": "lse_finalize",
+         "cx_kernel": "centred_reduction"}
 
 
 def short(kname):
