@@ -83,11 +83,16 @@ int& red_alg() {
   return v;
 }
 
-bool cx_eligible(int64_t M, int64_t N) {
+bool cx_eligible(int64_t M, int64_t N, bool ext) {
   if (red_alg() == 0) return false;
   if (red_alg() == 2) return M > 0 && N > 0;
   // the prep pass (bounding box, Morton codes, radix sort, records) costs ~40-60 us: measured
-  // break-even between 20k x 20k (0.8x) and 50k x 50k (1.09x) (tools/cx_ab.py)
+  // break-even against the generic reductions between 20k x 20k (0.8x) and 50k x 50k (1.09x),
+  // at 100k rows x 20k columns (1.04x) (tools/cx_ab.py, profiles/r03_ab_centred_shapes.json).
+  // The external-point forward has a packed scaled-coordinate kernel below these sizes
+  // (ext_pk.hpp, 1.2x the generic one), which the centred form only beats from ~50k x 50k on
+  // (tools/ext_ab.py, profiles/r03_ab_ext_packed.json).
+  if (ext) return N >= 32768 && (double)M * (double)N >= 2.5e9;
   return N >= 16384 && (double)M * (double)N >= 2.0e9;
 }
 

@@ -205,7 +205,8 @@ int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, in
 // scaled units x 100) up to which the expanded exponent is used.
 int& red_alg();
 int& cx_rho_x100();
-bool cx_eligible(int64_t M, int64_t N);
+// rows M, columns N; ext: the external-point forward (its non-centred kernel is the packed one)
+bool cx_eligible(int64_t M, int64_t N, bool ext = false);
 bool cx_has_op(int op);
 int cx_gauss_red(int op, const float* x, int64_t M, const float* y, int64_t N, int D, const float* b,
                  double sigma, float* out, void* ws, size_t wsb, hipStream_t st);

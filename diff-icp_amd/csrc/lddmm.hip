@@ -6,6 +6,7 @@
 #include "packed.hpp"
 #include "lddmm_sym_pk.hpp"
 #include "mfma_fwd.hpp"
+#include "ext_pk.hpp"
 
 #include <stdlib.h>
 
@@ -41,6 +42,10 @@ int g_bwd_alg = 3;
 #define DICP_BWD_ETA_ALG 2
 #endif
 int g_bwd_eta_alg = DICP_BWD_ETA_ALG;
+// external-point passes below the centred path's sizes: 0 = generic scalar rows in original
+// units (OpOdeExtFwd / OpOdeExtBwdX / OpOdeExtBwdQ), 1 = packed-FP32 rows in scaled
+// coordinates (ext_pk.hpp; the VJP only for eta = 0)
+int g_ext_alg = 1;
 // eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
 // (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair instead of 20 + 1, but 3-5%
 // slower: issue-stalled on its rotating column sums), 2 = packed-FP32 rows (packed.hpp: the
@@ -155,6 +160,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     red_alg() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "ext_alg")) {
+    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    g_ext_alg = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "cx_rho_x100")) {
     if (value < 0 || value > 100000) return DICP_ERR_INVALID;
     cx_rho_x100() = value;
@@ -181,6 +191,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "bwd_alg")) { *value = g_bwd_alg; return DICP_OK; }
   if (!strcmp(name, "red_alg")) { *value = red_alg(); return DICP_OK; }
   if (!strcmp(name, "cx_rho_x100")) { *value = cx_rho_x100(); return DICP_OK; }
+  if (!strcmp(name, "ext_alg")) { *value = g_ext_alg; return DICP_OK; }
   if (!strcmp(name, "r_fwd")) { *value = r_fwd(); return DICP_OK; }
   if (!strcmp(name, "r_bwd")) { *value = r_bwd(); return DICP_OK; }
   set_error("dicp_get_option: unknown option %s", name);
@@ -462,10 +473,20 @@ template <int D>
 int ode_ext_fwd_d(const float* x, int64_t N, const float* q, const float* p, int64_t M,
                   double sigma, double eta, float* vx, float* gx, void* ws, size_t wsb,
                   hipStream_t st) {
-  if (cx_eligible(N, M)) return cx_ext_fwd(x, N, q, p, M, D, sigma, eta, vx, gx, ws, wsb, st);
+  if (cx_eligible(N, M, true)) return cx_ext_fwd(x, N, q, p, M, D, sigma, eta, vx, gx, ws, wsb, st);
+  const Outs o = make_outs(vx, gx);
+  if (g_ext_alg == 1) {
+    Args a = {x, nullptr, nullptr, nullptr, q, p, nullptr, nullptr};
+    Scal sc = make_scal(sigma, eta);
+    scale_coords(a, sc, sigma);
+    if (eta != 0.0)
+      return gx ? launch_rowred_pk<OpExtFwdPk<D, true, true>>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st)
+                : launch_rowred_pk<OpExtFwdPk<D, true, false>>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st);
+    return gx ? launch_rowred_pk<OpExtFwdPk<D, false, true>>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st)
+              : launch_rowred_pk<OpExtFwdPk<D, false, false>>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st);
+  }
   const Args a = {x, nullptr, nullptr, nullptr, q, p, nullptr, nullptr};
   const Scal sc = make_scal(sigma, eta);
-  const Outs o = make_outs(vx, gx);
   if (eta != 0.0) {
     if (gx) return launch_rowred<OpOdeExtFwd<D, true, true>, kR>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st);
     return launch_rowred<OpOdeExtFwd<D, true, false>, kR>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st);
@@ -480,9 +501,13 @@ size_t ode_ext_fwd_ws(int64_t N, int64_t M) {
   for (size_t v : {rowred_ws_bytes<OpOdeExtFwd<D, true, true>, kR>(N, M),
                    rowred_ws_bytes<OpOdeExtFwd<D, true, false>, kR>(N, M),
                    rowred_ws_bytes<OpOdeExtFwd<D, false, true>, kR>(N, M),
-                   rowred_ws_bytes<OpOdeExtFwd<D, false, false>, kR>(N, M)})
+                   rowred_ws_bytes<OpOdeExtFwd<D, false, false>, kR>(N, M),
+                   rowred_pk_ws_bytes<OpExtFwdPk<D, true, true>>(N, M),
+                   rowred_pk_ws_bytes<OpExtFwdPk<D, true, false>>(N, M),
+                   rowred_pk_ws_bytes<OpExtFwdPk<D, false, true>>(N, M),
+                   rowred_pk_ws_bytes<OpExtFwdPk<D, false, false>>(N, M)})
     m = v > m ? v : m;
-  if (cx_eligible(N, M)) {
+  if (cx_eligible(N, M, true)) {
     const size_t c = cx_ext_ws(N, M, D);
     m = c > m ? c : m;
   }
@@ -493,6 +518,19 @@ template <int D>
 int ode_ext_bwd_d(const float* x, int64_t N, const float* q, const float* p, int64_t M,
                   double sigma, double eta, const float* gvx, const float* gdiv, float* gxo,
                   float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
+  if (g_ext_alg == 1 && eta == 0.0) {
+    Args a = {x, gvx, nullptr, nullptr, q, p, nullptr, nullptr};
+    Scal sc = make_scal(sigma, 0.0);
+    scale_coords(a, sc, sigma);
+    sc.dev0 = gdiv;
+    int rc = launch_rowred_pk<OpExtBwdXPk<D>>("ode_ext_bwd_x", a, sc, N, M, make_outs(gxo), ws, wsb, st);
+    if (rc) return rc;
+    Args b = {q, p, nullptr, nullptr, x, gvx, nullptr, nullptr};
+    b.scale = a.scale;
+    Outs o = make_outs(gq, gp);
+    o.accumulate[0] = o.accumulate[1] = 1;
+    return launch_rowred_pk<OpExtBwdQPk<D>>("ode_ext_bwd_q", b, sc, M, N, o, ws, wsb, st);
+  }
   Scal sc = make_scal(sigma, eta);
   sc.dev0 = gdiv;
   // rows x: gradient w.r.t. the carried points
@@ -520,7 +558,8 @@ size_t ode_ext_bwd_ws(int64_t N, int64_t M) {
   size_t m = 0;
   for (size_t v : {rowred_ws_bytes<OpOdeExtBwdX<D>, kR>(N, M), rowred_ws_bytes<OpOdeExtBwdQ<D>, kR>(M, N),
                    rowred_ws_bytes<OpOdeExtBwdXEta<D>, kR>(N, M),
-                   rowred_ws_bytes<OpOdeExtBwdQEta<D>, kR>(M, N)})
+                   rowred_ws_bytes<OpOdeExtBwdQEta<D>, kR>(M, N),
+                   rowred_pk_ws_bytes<OpExtBwdXPk<D>>(N, M), rowred_pk_ws_bytes<OpExtBwdQPk<D>>(M, N)})
     m = v > m ? v : m;
   return m;
 }

@@ -101,6 +101,13 @@ struct OpOdeSelfFwdPk {
 #ifndef DICP_PK_PAIR_UNROLL
 #define DICP_PK_PAIR_UNROLL DICP_PAIR_UNROLL
 #endif
+// packed ops may define load_rows_s, which also sees the launch scalars (row constants such
+// as a cotangent scale read from device memory at kernel start)
+template <class T, class = void>
+struct has_rows_s : std::false_type {};
+template <class T>
+struct has_rows_s<T, std::void_t<decltype(&T::load_rows_s)>> : std::true_type {};
+
 template <class Op>
 __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
                                                            int64_t chunk, Outs outs) {
@@ -115,7 +122,10 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
   int64_t i0 = ibase, i1 = ibase + kBlock;
   typename Base::Row brow[2];
   typename Op::Row2 row;
-  Op::load_rows(args, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row, brow[0], brow[1]);
+  if constexpr (has_rows_s<Op>::value)
+    Op::load_rows_s(args, sc, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row, brow[0], brow[1]);
+  else
+    Op::load_rows(args, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row, brow[0], brow[1]);
 
   f2 tot[NACC];
 #pragma unroll

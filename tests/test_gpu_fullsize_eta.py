@@ -112,9 +112,16 @@ def test_bwd_zs_fullsize_subset(pts, dev):
 
 
 @pytest.mark.parametrize("eta", [0.0, 1e-3])
-def test_ext_fwd_fullsize_subset_eta(pts, eta):
+@pytest.mark.parametrize("red_alg,ext_alg", [(1, 1), (0, 1), (0, 0)])   # centred / packed / generic
+def test_ext_fwd_fullsize_subset_eta(pts, eta, red_alg, ext_alg):
     from difficp_amd import _lib
-    vx, gx = _lib.ode_ext_fwd(pts["xf"], pts["qf"], pts["pf"], SIG, eta, True)
+    _lib.set_option("red_alg", red_alg)
+    _lib.set_option("ext_alg", ext_alg)
+    try:
+        vx, gx = _lib.ode_ext_fwd(pts["xf"], pts["qf"], pts["pf"], SIG, eta, True)
+    finally:
+        _lib.set_option("red_alg", 1)
+        _lib.set_option("ext_alg", 1)
     s = pts["sub"]
     v64, g64 = F.ext_terms(pts["x"][s], pts["q"], pts["p"], SIG, eta)
     assert rel_err(vx[s], v64) < 1e-5
@@ -122,7 +129,8 @@ def test_ext_fwd_fullsize_subset_eta(pts, eta):
 
 
 @pytest.mark.parametrize("eta", [0.0, 1e-3])
-def test_ext_bwd_fullsize_subset(pts, eta, dev):
+@pytest.mark.parametrize("ext_alg", [1, 0])   # packed (eta = 0) / generic
+def test_ext_bwd_fullsize_subset(pts, eta, dev, ext_alg):
     """ode_ext_bwd: gx rows (x side) and the gq, gp accumulated into the caller's buffers
     (support side, a column reduction over the 50k external points)."""
     from difficp_amd import _lib
@@ -130,8 +138,12 @@ def test_ext_bwd_fullsize_subset(pts, eta, dev):
     q, p = pts["qf"], pts["pf"]
     gq0 = torch.randn_like(q)
     gq, gp = gq0.clone(), torch.zeros_like(q)
-    gx = _lib.ode_ext_bwd(pts["xf"], q, p, pts["axf"], torch.full((1,), gam, device=dev), SIG, eta,
-                          gq, gp)
+    _lib.set_option("ext_alg", ext_alg)
+    try:
+        gx = _lib.ode_ext_bwd(pts["xf"], q, p, pts["axf"], torch.full((1,), gam, device=dev), SIG,
+                              eta, gq, gp)
+    finally:
+        _lib.set_option("ext_alg", 1)
     s = pts["sub"]
     gx64, gq64, gp64 = F.ext_vjp_subset(pts["x"], pts["q"], pts["p"], pts["ax"], gam, s, s, SIG, eta)
     assert rel_err(gx[s], gx64) < 2e-5
