@@ -42,9 +42,9 @@ int g_bwd_alg = 3;
 #define DICP_BWD_ETA_ALG 2
 #endif
 int g_bwd_eta_alg = DICP_BWD_ETA_ALG;
-// external-point passes below the centred path's sizes: 0 = generic scalar rows in original
-// units (OpOdeExtFwd / OpOdeExtBwdX / OpOdeExtBwdQ), 1 = packed-FP32 rows in scaled
-// coordinates (ext_pk.hpp; the VJP only for eta = 0)
+// external-point passes and KRed below the centred path's sizes: 0 = generic scalar rows in
+// original units (OpOdeExtFwd / OpOdeExtBwdX / OpOdeExtBwdQ / OpKRed), 1 = packed-FP32 rows in
+// scaled coordinates (ext_pk.hpp; the external-point VJP only for eta = 0)
 int g_ext_alg = 1;
 // eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
 // (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair instead of 20 + 1, but 3-5%
@@ -218,6 +218,15 @@ extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float
   }
   if (cx_has_op(op) && (D == 2 || D == 3) && cx_eligible(M, N))
     return cx_gauss_red(op, x, M, y, N, D, b, sigma, out, ws, ws_bytes, st);
+  if (op == DICP_KRED && g_ext_alg == 1 && (D == 2 || D == 3) && N > 0) {
+    // KRed = the external-point forward's velocity sum: the packed scaled-coordinate kernel
+    Args ak = {x, nullptr, nullptr, nullptr, y, b, nullptr, nullptr};
+    Scal sk = make_scal(sigma, 0.0);
+    scale_coords(ak, sk, sigma);
+    const Outs o = make_outs(out);
+    return D == 2 ? launch_rowred_pk<OpExtFwdPk<2, false, false>>("KRed", ak, sk, M, N, o, ws, ws_bytes, st)
+                  : launch_rowred_pk<OpExtFwdPk<3, false, false>>("KRed", ak, sk, M, N, o, ws, ws_bytes, st);
+  }
   switch (op) {
     case DICP_KBASE: return red_dispatch<OpKBase>("KBase", D, a, sc, M, N, out, ws, ws_bytes, st);
     case DICP_KREDSCAL: return red_dispatch<OpKRedScal>("KRedScal", D, a, sc, M, N, out, ws, ws_bytes, st);
@@ -864,7 +873,9 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
                     red_ws<OpMinSqDist>(D, M, N), red_ws<OpZDotB>(D, M, N),
                     red_ws<OpDDK>(D, M, N), red_ws<OpKRedScal>(D, M, N),
                     red_ws<OpGradLapKScal>(D, M, N), red_ws<OpMinSqDistOther>(D, M, N),
-                    red_ws<OpRadiusCount>(D, M, N)};
+                    red_ws<OpRadiusCount>(D, M, N),
+                    D == 2 ? rowred_pk_ws_bytes<OpExtFwdPk<2, false, false>>(M, N)
+                           : rowred_pk_ws_bytes<OpExtFwdPk<3, false, false>>(M, N)};
       for (size_t v : c) m = v > m ? v : m;
       if (cx_eligible(M, N)) {
         const size_t v = cx_red_ws(M, N, D);

@@ -104,3 +104,18 @@ def test_ext_packed_default_and_deterministic(dev):
     g1 = _lib.ode_ext_bwd(x, q, p, a, gd, SIG, 0.0, gq, gp)
     g2 = _lib.ode_ext_bwd(x, q, p, a, gd, SIG, 0.0, gq2, gp2)
     assert torch.equal(g1, g2) and torch.equal(gq, gq2) and torch.equal(gp, gp2)
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
+@pytest.mark.parametrize("N,M", SHAPES)
+@pytest.mark.parametrize("D", [2, 3])
+def test_kred_paths(dev, path, N, M, D):
+    """KRed (kernel.py:138, :186-187) on the packed scaled-coordinate kernel (ext_alg 1 below the
+    centred sizes), the generic kernel and the centred one."""
+    from difficp_amd import _lib
+    x, y, b, _ = _case(N, M, D, N * 13 + M + D, dev)
+    xf, yf, bf = x.float(), y.float(), b.float()
+    with options(**PATHS[path]):
+        out = _lib.gauss_red(_lib.KRED, xf, yf, SIG, b=bf)
+    ref, _ = F.ext_terms(xf.double(), yf.double(), bf.double(), SIG, 0.0)
+    assert rel_err(out, ref) < 1e-5
