@@ -252,6 +252,26 @@ class LDDMMModel:
             H0 = self.Hamiltonian(q0, p0)
         return self.lam * H0 + cost
 
+    # extent of the support, in units of sigma, beyond which the fused shooting kernels'
+    # scaled coordinates (q' = alpha (q - q_0), csrc/common.hpp ld_coord) can no longer
+    # guarantee the parity criterion (1e-5 norm-wise against float64): measured 2.8e-6 at
+    # 100 sigma, 1.3e-5 at 300 sigma (profiles/r03_extent_precision.jsonl)
+    EXTENT_WARN_SIGMA = 200.0
+
+    def _check_extent(self, q0):
+        """Warn once per model when the support spans more than EXTENT_WARN_SIGMA sigma (one
+        small device read per Optimize call)."""
+        if getattr(self, "_extent_warned", False) or q0.numel() == 0 or q0.device.type != "cuda":
+            return
+        ext = float((q0.amax(0) - q0.amin(0)).norm()) / float(self.Kernel.sigma)
+        if ext > self.EXTENT_WARN_SIGMA:
+            import warnings
+            self._extent_warned = True
+            warnings.warn(f"LDDMM support spans {ext:.0f} sigma: beyond ~{self.EXTENT_WARN_SIGMA:.0f} sigma "
+                          "the scaled-coordinate shooting kernels lose float32 digits against the "
+                          "reference arithmetic (relative error > 1e-5); rescale the problem or use "
+                          "a larger sigma", RuntimeWarning)
+
     def Optimize(self, dataloss, q0, p0, x0=None, nmax=10, tol=1e-3, errthresh=1e8):
         """min_p0 trajloss + dataloss(q1 or x1) with L-BFGS (LDDMM.py:338-398).
         Returns (p0, shoot, trajl, datal, nsteps, change)."""
@@ -260,6 +280,7 @@ class LDDMMModel:
         q0 = q0.detach()
         if is_x:
             x0 = x0.detach()
+        self._check_extent(q0)
 
         last_eval = {}
 

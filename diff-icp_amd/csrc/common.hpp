@@ -68,7 +68,26 @@ struct Args {
   // coordinate pre-scale alpha = sqrt(log2(e) / (2 sigma^2)) for ops that work in scaled
   // coordinates (K = exp2(-|alpha z|^2) needs no per-pair multiply); 0 when unused
   float scale;
+  // origin of the scaled coordinates q' = alpha (q - shift): a device D-vector (the first
+  // support point) or NULL (0).  Pair terms only see differences, so the shift changes no
+  // result in exact arithmetic; it keeps |q'| at the cloud's extent over sigma whatever the
+  // offset of the coordinates, so the rounding of q' does not grow with that offset.
+  const float* shift;
 };
+
+template <int D>
+__device__ __forceinline__ void load_shift(const Args& a, float* c) {
+#pragma unroll
+  for (int d = 0; d < D; ++d) c[d] = a.shift ? a.shift[d] : 0.f;
+}
+// scaled coordinates of point i of p (D floats): alpha (p_i - shift)
+template <int D>
+__device__ __forceinline__ void ld_coord(const Args& a, const float* __restrict__ p, int64_t i, float* dst) {
+  float c[D];
+  load_shift<D>(a, c);
+#pragma unroll
+  for (int d = 0; d < D; ++d) dst[d] = a.scale * (p[i * D + d] - c[d]);
+}
 
 // Output descriptor: up to 4 output arrays, each (rows, width) row-major.
 // In split mode the kernel writes partial slab `blockIdx.y` of each output at

@@ -108,9 +108,12 @@ bool supported_dim(int D) { return D == 2 || D == 3; }
 
 // Scaled-coordinate ops (OpOdeSelfFwd / OpOdeSelfBwd): alpha = sqrt(log2 e / (2 sigma^2)),
 // aux1 = s / alpha.
+// The coordinate origin is the first column point (a.c0: the support q of the self ops, the
+// support of the external-point x pass, y of KRed), the same for rows and columns.
 void scale_coords(Args& a, Scal& sc, double sigma) {
   const double alpha = std::sqrt(1.4426950408889634 / (2.0 * sigma * sigma));
   a.scale = (float)alpha;
+  a.shift = a.c0;
   sc.aux1 = (float)(1.0 / (sigma * sigma) / alpha);
 }
 
@@ -220,9 +223,8 @@ extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float
     return cx_gauss_red(op, x, M, y, N, D, b, sigma, out, ws, ws_bytes, st);
   if (op == DICP_KRED && g_ext_alg == 1 && (D == 2 || D == 3) && N > 0) {
     // KRed = the external-point forward's velocity sum: the packed scaled-coordinate kernel
-    Args ak = {x, nullptr, nullptr, nullptr, y, b, nullptr, nullptr};
-    Scal sk = make_scal(sigma, 0.0);
-    scale_coords(ak, sk, sigma);
+    const Args ak = {x, nullptr, nullptr, nullptr, y, b, nullptr, nullptr};
+    const Scal sk = make_scal(sigma, 0.0);
     const Outs o = make_outs(out);
     return D == 2 ? launch_rowred_pk<OpExtFwdPk<2, false, false>>("KRed", ak, sk, M, N, o, ws, ws_bytes, st)
                   : launch_rowred_pk<OpExtFwdPk<3, false, false>>("KRed", ak, sk, M, N, o, ws, ws_bytes, st);
@@ -485,9 +487,8 @@ int ode_ext_fwd_d(const float* x, int64_t N, const float* q, const float* p, int
   if (cx_eligible(N, M, true)) return cx_ext_fwd(x, N, q, p, M, D, sigma, eta, vx, gx, ws, wsb, st);
   const Outs o = make_outs(vx, gx);
   if (g_ext_alg == 1) {
-    Args a = {x, nullptr, nullptr, nullptr, q, p, nullptr, nullptr};
-    Scal sc = make_scal(sigma, eta);
-    scale_coords(a, sc, sigma);
+    const Args a = {x, nullptr, nullptr, nullptr, q, p, nullptr, nullptr};
+    const Scal sc = make_scal(sigma, eta);
     if (eta != 0.0)
       return gx ? launch_rowred_pk<OpExtFwdPk<D, true, true>>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st)
                 : launch_rowred_pk<OpExtFwdPk<D, true, false>>("ode_ext_fwd", a, sc, N, M, o, ws, wsb, st);
@@ -528,14 +529,12 @@ int ode_ext_bwd_d(const float* x, int64_t N, const float* q, const float* p, int
                   double sigma, double eta, const float* gvx, const float* gdiv, float* gxo,
                   float* gq, float* gp, void* ws, size_t wsb, hipStream_t st) {
   if (g_ext_alg == 1 && eta == 0.0) {
-    Args a = {x, gvx, nullptr, nullptr, q, p, nullptr, nullptr};
+    const Args a = {x, gvx, nullptr, nullptr, q, p, nullptr, nullptr};
     Scal sc = make_scal(sigma, 0.0);
-    scale_coords(a, sc, sigma);
     sc.dev0 = gdiv;
     int rc = launch_rowred_pk<OpExtBwdXPk<D>>("ode_ext_bwd_x", a, sc, N, M, make_outs(gxo), ws, wsb, st);
     if (rc) return rc;
-    Args b = {q, p, nullptr, nullptr, x, gvx, nullptr, nullptr};
-    b.scale = a.scale;
+    const Args b = {q, p, nullptr, nullptr, x, gvx, nullptr, nullptr};
     Outs o = make_outs(gq, gp);
     o.accumulate[0] = o.accumulate[1] = 1;
     return launch_rowred_pk<OpExtBwdQPk<D>>("ode_ext_bwd_q", b, sc, M, N, o, ws, wsb, st);

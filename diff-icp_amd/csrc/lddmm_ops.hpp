@@ -414,11 +414,11 @@ struct OpOdeSelfFwd {
   static constexpr bool kMin = false;
   struct Row { float q[D]; float p[D]; };
   __device__ static void load_row(const Args& a, int64_t i, Row& r) {
-    ld_scaled<D>(a.r0, i, a.scale, r.q);
+    ld_coord<D>(a, a.r0, i, r.q);
     ld<D>(a.r1, i, r.p);
   }
   __device__ static void load_col(const Args& a, int64_t j, float* rec) {
-    ld_scaled<D>(a.c0, j, a.scale, rec);
+    ld_coord<D>(a, a.c0, j, rec);
     ld<D>(a.c1, j, rec + D);
   }
   __device__ static void pair(const Scal& sc, const Row& r, const float* rec, float* acc) {
@@ -518,7 +518,7 @@ struct OpOdeSelfBwd {
   // ap is evaluated with the row's a, p pre-multiplied by 1/alpha (ia_a, ia_p)
   struct Row { float q[D]; float p[D]; float b[D]; float ia_a[D]; float ia_p[D]; };
   __device__ static void load_row(const Args& a, int64_t i, Row& r) {
-    ld_scaled<D>(a.r0, i, a.scale, r.q);
+    ld_coord<D>(a, a.r0, i, r.q);
     ld<D>(a.r1, i, r.p);
     ld<D>(a.r3, i, r.b);
     const float ia = 1.0f / a.scale;
@@ -527,7 +527,7 @@ struct OpOdeSelfBwd {
     for (int d = 0; d < D; ++d) r.ia_p[d] = ia * r.p[d];
   }
   __device__ static void load_col(const Args& a, int64_t j, float* rec) {
-    ld_scaled<D>(a.c0, j, a.scale, rec);
+    ld_coord<D>(a, a.c0, j, rec);
     ld<D>(a.c1, j, rec + D);
     ld<D>(a.c2, j, rec + 2 * D);
     ld<D>(a.c3, j, rec + 3 * D);
@@ -584,7 +584,7 @@ struct OpOdeSelfBwd2 {
   static constexpr bool kMin = false;
   struct Row { float q[D]; float p[D]; float b[D]; float ia_a[D]; float sia_p[D]; float gp[D]; float ngam; };
   __device__ static void load_row_s(const Args& a, const Scal& sc, int64_t i, Row& r) {
-    ld_scaled<D>(a.r0, i, a.scale, r.q);
+    ld_coord<D>(a, a.r0, i, r.q);
     ld<D>(a.r1, i, r.p);
     ld<D>(a.r3, i, r.b);
     const float ia = 1.0f / a.scale;
@@ -598,7 +598,7 @@ struct OpOdeSelfBwd2 {
     r.ngam = -gam;
   }
   __device__ static void load_col_s(const Args& a, const Scal& sc, int64_t j, float* rec) {
-    ld_scaled<D>(a.c0, j, a.scale, rec);
+    ld_coord<D>(a, a.c0, j, rec);
     ld<D>(a.c1, j, rec + D);
     ld_scaled<D>(a.c2, j, 1.0f / sc.aux1, rec + 2 * D);
     ld<D>(a.c3, j, rec + 3 * D);

@@ -114,13 +114,15 @@ struct SymBwd {
 
   __device__ static void load_row(const Args& a, const Scal& sc, int64_t i, bool valid, Row& r) {
     const float ia = 1.0f / a.scale, gam = sc.aux0;
+    float c[D];
+    load_shift<D>(a, c);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float q = valid ? a.r0[i * D + d] : 0.f;
       const float p = valid ? a.r1[i * D + d] : 0.f;
       const float av = valid ? a.r2[i * D + d] : 0.f;
       const float b = valid ? a.r3[i * D + d] : 0.f;
-      r.q[d] = valid ? a.scale * q : kFar;
+      r.q[d] = valid ? a.scale * (q - c[d]) : kFar;
       r.p[d] = p;
       r.b[d] = b;
       r.ia_a[d] = ia * av;
@@ -131,13 +133,15 @@ struct SymBwd {
   // column record: q' (D), p (D), a / alpha (D), b (D), gam p (D)
   __device__ static void load_col(const Args& a, const Scal& sc, int64_t j, bool valid, float* rec) {
     const float ia = 1.0f / a.scale, gam = sc.aux0;
+    float c[D];
+    load_shift<D>(a, c);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float q = valid ? a.c0[j * D + d] : 0.f;
       const float p = valid ? a.c1[j * D + d] : 0.f;
       const float av = valid ? a.c2[j * D + d] : 0.f;
       const float b = valid ? a.c3[j * D + d] : 0.f;
-      rec[d] = valid ? a.scale * q : kFar;
+      rec[d] = valid ? a.scale * (q - c[d]) : kFar;
       rec[D + d] = p;
       rec[2 * D + d] = ia * av;
       rec[3 * D + d] = b;
@@ -227,16 +231,20 @@ struct SymFwd {
     float q[D], p[D];
   };
   __device__ static void load_row(const Args& a, const Scal&, int64_t i, bool valid, Row& r) {
+    float c[D];
+    load_shift<D>(a, c);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      r.q[d] = valid ? a.scale * a.r0[i * D + d] : kFar;
+      r.q[d] = valid ? a.scale * (a.r0[i * D + d] - c[d]) : kFar;
       r.p[d] = valid ? a.r1[i * D + d] : 0.f;
     }
   }
   __device__ static void load_col(const Args& a, const Scal&, int64_t j, bool valid, float* rec) {
+    float c[D];
+    load_shift<D>(a, c);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      rec[d] = valid ? a.scale * a.c0[j * D + d] : kFar;
+      rec[d] = valid ? a.scale * (a.c0[j * D + d] - c[d]) : kFar;
       rec[D + d] = valid ? a.c1[j * D + d] : 0.f;
     }
 #pragma unroll

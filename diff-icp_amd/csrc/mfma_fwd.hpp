@@ -66,6 +66,8 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int64_t i0 = (int64_t)blockIdx.x * kMfRowsWG;
   const float al = a.scale;
+  float sh[D];
+  load_shift<D>(a, sh);
   auto rowidx = [&](int64_t i) -> int64_t { return order ? (int64_t)order[i] : i; };
 
   // ---- centre c: mean of q' over this workgroup's rows (thread t: row i0 + t) ----
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
     if (ie < M) {
       const int64_t g = rowidx(ie);
 #pragma unroll
-      for (int d = 0; d < D; ++d) qe[d] = al * a.r0[g * D + d];
+      for (int d = 0; d < D; ++d) qe[d] = al * (a.r0[g * D + d] - sh[d]);
     } else {
 #pragma unroll
       for (int d = 0; d < D; ++d) qe[d] = 0.f;
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
     if (ii >= M) ii = M - 1;  // rows past the end: computed, never stored
     const int64_t g = rowidx(ii);
 #pragma unroll
-    for (int d = 0; d < D; ++d) qr[rb][d] = al * a.r0[g * D + d];
+    for (int d = 0; d < D; ++d) qr[rb][d] = al * (a.r0[g * D + d] - sh[d]);
   }
 
   const int64_t j0 = (int64_t)blockIdx.y * chunk;
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
         float pj[D], qt[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-          qj[d] = al * a.c0[j * D + d];
+          qj[d] = al * (a.c0[j * D + d] - sh[d]);
           pj[d] = a.c1[j * D + d];
           qt[d] = qj[d] - c[d];
         }
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
       const int64_t g = rowidx(ie);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        const float t = al * a.r0[g * D + d] - c[d];
+        const float t = al * (a.r0[g * D + d] - sh[d]) - c[d];
         r2 = fmaf(t, t, r2);
       }
     }
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
       const int64_t g = rowidx(ii);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        qi[d] = al * a.r0[g * D + d];
+        qi[d] = al * (a.r0[g * D + d] - sh[d]);
         pi[d] = a.r1[g * D + d];
       }
     }
@@ -293,7 +295,7 @@ __global__ __launch_bounds__(256) void mfma_fwd_kernel(Args a, Scal sc, int64_t 
   float qt[D], p[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    qt[d] = al * a.r0[g * D + d] - c[d];
+    qt[d] = al * (a.r0[g * D + d] - sh[d]) - c[d];
     p[d] = a.r1[g * D + d];
   }
   const float* V = S;
