@@ -15,6 +15,7 @@ integrator (up to fp32 rounding); the trajectory (nt+1 states) stays resident in
 from __future__ import annotations
 
 import threading
+import weakref
 from collections import OrderedDict
 
 import torch
@@ -176,9 +177,13 @@ class ShootCache:
                 self._d.move_to_end(key)
         # p0 first: it is what differs between the closures of one L-BFGS run (each
         # torch.equal is a device round trip).  The L-BFGS parameter is updated in place, so
-        # the same storage at a newer version is a miss without comparing (at worst a false
-        # miss -- a recomputation -- never a stale hit)
-        if e is not None and p0.data_ptr() == e["p0src"][0] and p0._version != e["p0src"][1]:
+        # the same tensor at a newer version is a miss without comparing.  Same tensor OBJECT
+        # (weak reference), not just the same address: a new tensor that the allocator put at
+        # the old one's address starts a version count of its own, and taking it for an
+        # in-place update would make hits depend on allocation order (a false miss -- a
+        # recomputation -- never a stale hit, but not a reproducible one)
+        if (e is not None and e["p0src"][0]() is p0 and p0.data_ptr() == e["p0src"][1]
+                and p0._version != e["p0src"][2]):
             self.misses += 1
             return None
         if (e is None or e["params"] != params or (e["x0"] is None) != (x0 is None)
@@ -198,7 +203,7 @@ class ShootCache:
         return e
 
     def store(self, q0, p0, x0, params, outs, saved):
-        e = {"q0": q0, "q0c": outs[0][0], "p0": p0.detach().clone(), "p0src": (p0.data_ptr(), p0._version),
+        e = {"q0": q0, "q0c": outs[0][0], "p0": p0.detach().clone(), "p0src": (weakref.ref(p0), p0.data_ptr(), p0._version),
              "x0": None if x0 is None else x0.detach().clone(),
              "params": params, "outs": outs, "saved": saved}
         e["nbytes"] = _nbytes(list(outs) + list(saved) + [e["p0"], e["x0"]])

@@ -351,6 +351,28 @@ def test_shoot_cache_no_stale_hit_on_reused_address(fake, scheme):
     cache_case.shoot_cache_stale_check(LM, 30, 2, "cpu")
 
 
+def test_shoot_cache_fast_miss_is_per_tensor(fake, monkeypatch):
+    """The in-place-update fast miss (no bitwise compare) applies to the SAME p0 tensor only:
+    a different tensor whose version count happens to differ is compared, so a hit never
+    depends on the allocator's address reuse."""
+    from difficp_amd.core.LDDMM import LDDMMModel
+    LM = LDDMMModel(sigma=0.3, D=2, lambd=5.0, version="hybrid", scheme="Euler", nt=3, spec=CPU)
+    q0 = torch.rand(25, 2)
+    p = 0.05 * torch.randn(25, 2)
+    LM.Shoot(q0, p)
+    calls = []
+    real_equal = torch.equal
+    monkeypatch.setattr(torch, "equal", lambda a, b: calls.append(1) or real_equal(a, b))
+    p.add_(0.01)                                # in-place update of the same tensor
+    LM.Shoot(q0, p)
+    assert LM.shoot_cache.misses >= 1 and not calls     # fast miss: nothing compared
+    other = p.clone()                           # equal content, a different tensor ...
+    other.add_(0.0)
+    other.add_(0.0)                             # ... with a version count of its own
+    LM.Shoot(q0, other)
+    assert calls and LM.shoot_cache.hits == 1   # compared, and reused
+
+
 def test_shoot_cache_is_bounded(fake):
     """LRU eviction by entry count and by bytes; entries hold the keyed q0 alive."""
     from difficp_amd.core.LDDMM import LDDMMModel
