@@ -26,8 +26,9 @@ void set_error(const char* fmt, ...) {
 extern "C" const char* dicp_last_error(void) { return g_err; }
 
 extern "C" const char* dicp_version(void) {
-  return "difficp_hip 0.1 (gfx950; ops: gauss_red x13, ode_self fwd/bwd, ode_ext fwd/bwd, "
-         "gmm estep/mstep/targets, kernel ridge CG, reduction gradients x5)";
+  return "difficp_hip 0.1 (gfx950; ops: gauss_red x13 (centred / packed KRed), ode_self fwd/bwd, "
+         "ode_ext fwd/bwd (centred / packed), gmm estep/mstep/targets, kernel ridge CG, "
+         "reduction gradients x5)";
 }
 
 extern "C" size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D) {
