@@ -148,6 +148,24 @@ def _zs_buf(zs, rows, D, dev, name="zs_out"):
     return zs
 
 
+class coord_mode:
+    """Context manager: the packed shooting kernels in original-unit coordinates (raw=True) or
+    in scaled ones (library option coord_raw, per host thread)."""
+
+    def __init__(self, raw: bool):
+        self.raw = int(bool(raw))
+
+    def __enter__(self):
+        self.old = get_option("coord_raw")
+        if self.old != self.raw:
+            set_option("coord_raw", self.raw)
+        return self
+
+    def __exit__(self, *exc):
+        if self.old != self.raw:
+            set_option("coord_raw", self.old)
+
+
 def set_option(name: str, value: int):
     """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
     _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")

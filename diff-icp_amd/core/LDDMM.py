@@ -11,6 +11,8 @@ backward) instead of the reference's per-reduction integrator loop.
 from __future__ import annotations
 
 import math
+import threading
+import weakref
 
 import torch
 
@@ -21,6 +23,11 @@ from ..tools.spec import defspec, getspec
 from .shooting import (HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootCache, ShootFn,
                        complete_p1, row_order_for, skip_p1)
 
+
+
+# per host thread: (q0 weak reference, q0 version, sigma, extent / sigma) of the last support
+# whose extent was read (LDDMMModel._raw_for): one device read per new q0 tensor
+_EXTENT_MEMO = threading.local()
 
 class Shoot(list):
     """A "shoot" variable: list of (q, p, cost[, x]) states at the nt+1 integration times
@@ -205,7 +212,7 @@ class LDDMMModel:
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
                              float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet),
                              self.row_split, getattr(self, "row_orders", None),
-                             getattr(self, "shoot_cache", None), bool(need_p1))
+                             getattr(self, "shoot_cache", None), bool(need_p1), self._raw_for(q0))
         if x0 is None:
             Q, P, C, H0 = outs
             sh = Shoot(Q, P, C, None, H0)
@@ -252,25 +259,28 @@ class LDDMMModel:
             H0 = self.Hamiltonian(q0, p0)
         return self.lam * H0 + cost
 
-    # extent of the support, in units of sigma, beyond which the fused shooting kernels'
-    # scaled coordinates (q' = alpha (q - q_0), csrc/common.hpp ld_coord) can no longer
-    # guarantee the parity criterion (1e-5 norm-wise against float64): measured 2.8e-6 at
-    # 100 sigma, 1.3e-5 at 300 sigma (profiles/r03_extent_precision.jsonl)
-    EXTENT_WARN_SIGMA = 200.0
+    # Coordinates of the fused shooting kernels (library option coord_raw).  "scaled": q' =
+    # alpha (q - q_0), one packed multiply per two pairs fewer, float32-exact differences only
+    # while the support spans up to ~200 sigma (2.8e-6 at 100 sigma, 1.3e-5 at 300 sigma
+    # against float64, profiles/r03_extent_precision.jsonl); "raw": original units, the
+    # reference's accuracy at any extent; "auto" (default): raw when q0 spans more than
+    # RAW_EXTENT_SIGMA sigma (one small device read per new q0 tensor, per host thread).
+    coord_mode = "auto"
+    RAW_EXTENT_SIGMA = 128.0
 
-    def _check_extent(self, q0):
-        """Warn once per model when the support spans more than EXTENT_WARN_SIGMA sigma (one
-        small device read per Optimize call)."""
-        if getattr(self, "_extent_warned", False) or q0.numel() == 0 or q0.device.type != "cuda":
-            return
+    def _raw_for(self, q0):
+        mode = self.coord_mode
+        if mode == "raw":
+            return True
+        if mode != "auto" or q0.numel() == 0 or q0.device.type != "cuda":
+            return False
+        last = getattr(_EXTENT_MEMO, "last", None)
+        if (last is not None and last[0]() is q0 and last[1] == q0._version
+                and last[2] == float(self.Kernel.sigma)):
+            return last[3] > self.RAW_EXTENT_SIGMA
         ext = float((q0.amax(0) - q0.amin(0)).norm()) / float(self.Kernel.sigma)
-        if ext > self.EXTENT_WARN_SIGMA:
-            import warnings
-            self._extent_warned = True
-            warnings.warn(f"LDDMM support spans {ext:.0f} sigma: beyond ~{self.EXTENT_WARN_SIGMA:.0f} sigma "
-                          "the scaled-coordinate shooting kernels lose float32 digits against the "
-                          "reference arithmetic (relative error > 1e-5); rescale the problem or use "
-                          "a larger sigma", RuntimeWarning)
+        _EXTENT_MEMO.last = (weakref.ref(q0), q0._version, float(self.Kernel.sigma), ext)
+        return ext > self.RAW_EXTENT_SIGMA
 
     def Optimize(self, dataloss, q0, p0, x0=None, nmax=10, tol=1e-3, errthresh=1e8):
         """min_p0 trajloss + dataloss(q1 or x1) with L-BFGS (LDDMM.py:338-398).
@@ -280,7 +290,6 @@ class LDDMMModel:
         q0 = q0.detach()
         if is_x:
             x0 = x0.detach()
-        self._check_extent(q0)
 
         last_eval = {}
 

@@ -294,13 +294,23 @@ class ShootFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split=None, orders=None,
-                cache=None, need_p1=True):
+                cache=None, need_p1=True, raw=False):
         """orders: optional RowOrderCache; the forward passes then visit the support rows in
         the spatial order of q0 (kept for every step: the flow moves neighbours together).
         cache: optional ShootCache (bitwise reuse of a repeated shooting, see there).
         need_p1=False: the final momenta P[nt] are not formed when skip_p1(...) holds (the last
         fused Euler step skips its Gs' sums) and P[nt] is filled with NaN; the caller must not
-        read it (LDDMMModel.Optimize's closures do not) or complete it (complete_p1)."""
+        read it (LDDMMModel.Optimize's closures do not) or complete it (complete_p1).
+        raw: the packed shooting kernels in original-unit coordinates (library option
+        coord_raw, per host thread: set here around the forward's launches and again in the
+        backward, which autograd may run on another thread)."""
+        ctx.raw = bool(raw)
+        with _lib.coord_mode(ctx.raw):
+            return ShootFn._forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split, orders,
+                                    cache, need_p1)
+
+    @staticmethod
+    def _forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split, orders, cache, need_p1):
         ctx.set_materialize_grads(False)   # unused outputs (cost, H0, ...) get None, not zeros
         has_x = x0 is not None
         skip = skip_p1(need_p1, scheme, has_x, eta, split, nt)
@@ -310,7 +320,7 @@ class ShootFn(torch.autograd.Function):
         use_zs = bool(want_div) and scheme == "Euler" and not has_x and nt >= 2 and _lib.zs_ok(eta)
         ctx.has_zs = use_zs
         params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
-                  None if split is None else (split.rank, split.world), skip, use_zs)
+                  None if split is None else (split.rank, split.world), skip, use_zs, ctx.raw)
         hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
         if hit is not None:
             ctx.split = split if (split is not None and not has_x and scheme == "Euler"
@@ -506,6 +516,11 @@ class ShootFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gQ, gP, gC, *rest):
+        with _lib.coord_mode(ctx.raw):
+            return ShootFn._backward(ctx, gQ, gP, gC, *rest)
+
+    @staticmethod
+    def _backward(ctx, gQ, gP, gC, *rest):
         gX, gH = rest if len(rest) == 2 else (None, rest[0])
         sigma, eta, nt, scheme, want_div, has_x = \
             ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x
@@ -625,7 +640,7 @@ class ShootFn(torch.autograd.Function):
             lp = lp + gH * v0
         if not ctx.needs_input_grad[0]:
             lq = None
-        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None, None
+        return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None, None, None
 
 
 class HamiltonianFn(torch.autograd.Function):

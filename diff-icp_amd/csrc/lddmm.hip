@@ -46,6 +46,11 @@ int g_bwd_eta_alg = DICP_BWD_ETA_ALG;
 // original units (OpOdeExtFwd / OpOdeExtBwdX / OpOdeExtBwdQ / OpKRed), 1 = packed-FP32 rows in
 // scaled coordinates (ext_pk.hpp; the external-point VJP only for eta = 0)
 int g_ext_alg = 1;
+// coordinates of the default packed shooting kernels (OpOdeSelfFwdPk, SymBwdPk): 0 = scaled,
+// q' = alpha (q - q_0), one packed multiply per two pairs fewer; 1 = original units, exact
+// differences whatever the cloud's extent.  Per HOST THREAD (the shooting
+// sets it around its own launches; concurrent frames run on their own threads).
+thread_local int tl_coord_raw = 0;
 // eta = 0 forward: 0 = OpOdeSelfFwd (ordered rows, R = 2), 1 = symmetric pair-once kernel
 // (lddmm_sym.hpp SymFwd: 17 VALU + 0.5 exp per ordered pair instead of 20 + 1, but 3-5%
 // slower: issue-stalled on its rotating column sums), 2 = packed-FP32 rows (packed.hpp: the
@@ -117,6 +122,28 @@ void scale_coords(Args& a, Scal& sc, double sigma) {
   sc.aux1 = (float)(1.0 / (sigma * sigma) / alpha);
 }
 
+// original-unit coordinates for the RAW packed kernels: alpha = 1, no shift, aux1 = s / 1
+void raw_coords(Args& a, Scal& sc) {
+  a.scale = 1.f;
+  a.shift = nullptr;
+  sc.aux1 = sc.s;
+}
+
+template <class OpS, class OpR>
+int launch_fwd_pk(bool raw, const char* name, Args a, Scal sc, int64_t nrows, int64_t M, const Outs& o,
+                  void* ws, size_t wsb, hipStream_t st) {
+  if (raw) {
+    raw_coords(a, sc);
+    return launch_rowred_pk<OpR>(name, a, sc, nrows, M, o, ws, wsb, st);
+  }
+  return launch_rowred_pk<OpS>(name, a, sc, nrows, M, o, ws, wsb, st);
+}
+template <class OpS, class OpR>
+size_t fwd_pk_ws(int64_t nrows, int64_t M) {
+  const size_t a = rowred_pk_ws_bytes<OpS>(nrows, M), b = rowred_pk_ws_bytes<OpR>(nrows, M);
+  return a > b ? a : b;
+}
+
 }  // namespace
 
 extern "C" int dicp_supports_dim(int D) { return supported_dim(D) ? 1 : 0; }
@@ -163,6 +190,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     red_alg() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "coord_raw")) {
+    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    tl_coord_raw = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "ext_alg")) {
     if (value < 0 || value > 1) return DICP_ERR_INVALID;
     g_ext_alg = value;
@@ -195,6 +227,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "red_alg")) { *value = red_alg(); return DICP_OK; }
   if (!strcmp(name, "cx_rho_x100")) { *value = cx_rho_x100(); return DICP_OK; }
   if (!strcmp(name, "ext_alg")) { *value = g_ext_alg; return DICP_OK; }
+  if (!strcmp(name, "coord_raw")) { *value = tl_coord_raw; return DICP_OK; }
   if (!strcmp(name, "r_fwd")) { *value = r_fwd(); return DICP_OK; }
   if (!strcmp(name, "r_bwd")) { *value = r_bwd(); return DICP_OK; }
   set_error("dicp_get_option: unknown option %s", name);
@@ -286,6 +319,7 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
   scale_coords(a, sc, sigma);
+  const bool raw = tl_coord_raw != 0;   // the packed kernels below; the others stay scaled
   if (zs != nullptr) {
     // divergence rows out through the (unused) h slot: the packed ordered pass only
     if (eta != 0.0 || o.ptr[3] != nullptr || (o.ptr[1] != nullptr && g_fwd_alg != 2)) {
@@ -298,23 +332,23 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     oz.accumulate[3] = 0;
     oz.alpha[3] = 1.f;
     if (o.ptr[1] == nullptr)
-      return launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, false, true>>("ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
+      return launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
                                                                            M, oz, ws, wsb, st);
-    return launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, true, true>>("ode_self_fwd(pk, zs)", a, sc, nrows, M, oz,
+    return launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, true, true>, OpOdeSelfFwdPk<D, true, false, true, true, true>>(raw, "ode_self_fwd(pk, zs)", a, sc, nrows, M, oz,
                                                                         ws, wsb, st);
   }
   if (eta != 0.0) {
     if (g_fwd_alg >= 2 && o.ptr[1] == nullptr)  // mG not wanted: without the Gs', Hs, GL' sums
-      return launch_rowred_pk<OpOdeSelfFwdPk<D, true, true, false>>("ode_self_fwd_eta(pk, no mG)", a, sc, nrows, M, o,
+      return launch_fwd_pk<OpOdeSelfFwdPk<D, true, true, false>, OpOdeSelfFwdPk<D, true, true, false, false, true>>(raw, "ode_self_fwd_eta(pk, no mG)", a, sc, nrows, M, o,
                                                                      ws, wsb, st);
     return g_fwd_alg >= 2
-               ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, true>>("ode_self_fwd_eta(pk)", a, sc, nrows, M, o, ws, wsb, st)
+               ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, true>, OpOdeSelfFwdPk<D, true, true, true, false, true>>(raw, "ode_self_fwd_eta(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
   }
   if (o.ptr[1] == nullptr)  // mG not wanted (eta = 0): the packed forward without the Gs' sums
     return o.ptr[2] != nullptr
-               ? launch_rowred_pk<OpOdeSelfFwdPk<D, true, false, false>>("ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st)
-               : launch_rowred_pk<OpOdeSelfFwdPk<D, false, false, false>>("ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st);
+               ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false>, OpOdeSelfFwdPk<D, true, false, false, false, true>>(raw, "ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st)
+               : launch_fwd_pk<OpOdeSelfFwdPk<D, false, false, false>, OpOdeSelfFwdPk<D, false, false, false, false, true>>(raw, "ode_self_fwd(pk, no mG)", a, sc, nrows, M, o, ws, wsb, st);
   if ((g_fwd_alg == 1 || g_fwd_alg == 4) && all)
     return o.ptr[2] != nullptr ? launch_sym_fwd<D, true>(a, sc, M, o, ws, wsb, st, g_fwd_alg == 4)
                                : launch_sym_fwd<D, false>(a, sc, M, o, ws, wsb, st, g_fwd_alg == 4);
@@ -324,8 +358,8 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
                : launch_mfma_fwd<D, false>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order);
   if (g_fwd_alg == 2 || g_fwd_alg == 4)
     return o.ptr[2] != nullptr
-               ? launch_rowred_pk<OpOdeSelfFwdPk<D, true>>("ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
-               : launch_rowred_pk<OpOdeSelfFwdPk<D, false>>("ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st);
+               ? launch_fwd_pk<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
+               : launch_fwd_pk<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st);
   if (o.ptr[2] != nullptr)
     return launch_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), "ode_self_fwd", a, sc, nrows, M, o, ws, wsb, st);
@@ -337,14 +371,14 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
   for (size_t v : {ws_r<OpOdeSelfFwd<D, true, true>>(r_fwd(), nrows, M),
                    ws_r<OpOdeSelfFwd<D, false, true>>(r_fwd(), nrows, M),
                    ws_r<OpOdeSelfFwd<D, false, false>>(r_fwd(), nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, true>>(nrows, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, true>, OpOdeSelfFwdPk<D, true, true, true, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, false>, OpOdeSelfFwdPk<D, true, false, false, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, true, false>, OpOdeSelfFwdPk<D, true, true, false, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, false, false, false>, OpOdeSelfFwdPk<D, false, false, false, false, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, true, true>, OpOdeSelfFwdPk<D, true, false, true, true, true>>(nrows, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(nrows, M),
                    mfma_fwd_ws_bytes<D, true>(nrows, M), mfma_fwd_ws_bytes<D, false>(nrows, M)})
     m = v > m ? v : m;
   return m;
@@ -360,14 +394,14 @@ size_t ode_self_fwd_ws(int64_t M) {
   a = a > c ? a : c;
   const size_t d = sym_ws_bytes(M, 3 * D);
   a = a > d ? a : d;
-  for (size_t e : {rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, true>>(M, M),
-                   rowred_pk_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, true>>(M, M),
+  for (size_t e : {fwd_pk_ws<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, true>, OpOdeSelfFwdPk<D, true, true, true, false, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, false>, OpOdeSelfFwdPk<D, true, false, false, false, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, true, false>, OpOdeSelfFwdPk<D, true, true, false, false, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, false, false, false>, OpOdeSelfFwdPk<D, false, false, false, false, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, true, true>, OpOdeSelfFwdPk<D, true, false, true, true, true>>(M, M),
+                   fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(M, M),
                    mfma_fwd_ws_bytes<D, true>(M, M), mfma_fwd_ws_bytes<D, false>(M, M)})
     a = a > e ? a : e;
   return a;
@@ -401,9 +435,11 @@ int ode_self_bwd_d(const float* q, const float* p, const float* gv, const float*
   Scal sc = make_scal(sigma, 0.0);
   scale_coords(a, sc, sigma);
   sc.dev0 = gdiv;  // nullptr -> aux0 = 0
-  if (b0) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, true, true, zs, zr0, zn);
+  const bool raw = tl_coord_raw != 0 && (b0 || g_bwd_alg == 3);   // packed kernels only
+  if (raw) raw_coords(a, sc);
+  if (b0) return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, true, true, zs, zr0, zn, raw);
   if (g_bwd_alg >= 2)
-    return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, g_bwd_alg == 3, false, zs, zr0, zn);
+    return launch_sym_bwd<D>(a, sc, M, o, ws, wsb, st, 0, 1, g_bwd_alg == 3, false, zs, zr0, zn, raw);
   if (g_bwd_alg == 1)
     return launch_r<OpOdeSelfBwd2<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
   return launch_r<OpOdeSelfBwd<D>>(r_bwd(), "ode_self_bwd", a, sc, M, M, o, ws, wsb, st);
@@ -431,8 +467,11 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
     Scal sc = make_scal(sigma, 0.0);
     scale_coords(a, sc, sigma);
     sc.dev0 = gdiv;
-    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts,
-                             b0 || g_bwd_alg == 3, b0, zs, zr0, zn);
+    const bool pk = b0 || g_bwd_alg == 3;
+    const bool raw = tl_coord_raw != 0 && pk;
+    if (raw) raw_coords(a, sc);
+    return launch_sym_bwd<D>(a, sc, M, make_outs(gq, gp), ws, wsb, st, part, nparts, pk, b0, zs, zr0,
+                             zn, raw);
   }
   if (eta != 0.0 && g_bwd_eta_alg == 2) {  // symmetric packed eta VJP: quads Q = part (mod nparts)
     const float* gb = b0 ? gv : gmG;

@@ -894,18 +894,22 @@ int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, 
 }
 
 // packed-FP32 variant of sym_bwd_kernel (lddmm_sym_pk.hpp); GQ = false: gp half only; GT =
-// false: without the divergence cotangent's pair terms
-template <int D, bool GQ, bool B0, bool GT>
+// false: without the divergence cotangent's pair terms; RAW: coordinates in original units
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
 __global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                   int64_t slot_stride, int qoff, int qstride);
 
 template <int D, bool GQ, bool B0>
-inline void sym_bwd_pk_launch(bool gt, dim3 grid, hipStream_t st, const Args& a, const Scal& sc, int64_t M,
-                              const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
-  if (gt)
-    sym_bwd_pk_kernel<D, GQ, B0, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+inline void sym_bwd_pk_launch(bool gt, bool raw, dim3 grid, hipStream_t st, const Args& a, const Scal& sc,
+                              int64_t M, const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
+  if (gt && raw)
+    sym_bwd_pk_kernel<D, GQ, B0, true, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+  else if (gt)
+    sym_bwd_pk_kernel<D, GQ, B0, true, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+  else if (raw)
+    sym_bwd_pk_kernel<D, GQ, B0, false, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
   else
-    sym_bwd_pk_kernel<D, GQ, B0, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+    sym_bwd_pk_kernel<D, GQ, B0, false, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
 }
 
 // b0: the cotangent on mG (Args r3 / c3) is identically zero -- those pointers are then not
@@ -913,10 +917,12 @@ inline void sym_bwd_pk_launch(bool gt, dim3 grid, hipStream_t st, const Args& a,
 // zs (rows [zr0, zr0 + zn)): the forward's divergence rows (OpOdeSelfFwdZs); with them, or
 // without a divergence cotangent (sc.dev0 == NULL: gam = 0), the packed kernels run without
 // the divergence cotangent's pair terms and the merge adds their row totals.
+// raw: the packed kernels in original coordinates (the caller passes Args::scale = 1, no shift,
+// Scal::aux1 = s); ignored by the scalar kernel (pk = false), which is scaled only
 template <int D>
 int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
                    hipStream_t st, int part = 0, int nparts = 1, bool pk = false, bool b0 = false,
-                   const float* zs = nullptr, int64_t zr0 = 0, int64_t zn = 0) {
+                   const float* zs = nullptr, int64_t zr0 = 0, int64_t zn = 0, bool raw = false) {
   if (M <= 0) return DICP_OK;
   if (zs != nullptr && !pk) {
     set_error("ode_self_bwd(sym): divergence rows need the packed kernel (bwd_alg 3)");
@@ -942,9 +948,9 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     if (nq1 > 0) {
       const dim3 grid((unsigned)g.Kmax, (unsigned)nq1);
       if (b0)
-        sym_bwd_pk_launch<D, false, true>(gt, grid, st, a, sc, M, g, slab, stride1, part, nparts);
+        sym_bwd_pk_launch<D, false, true>(gt, raw, grid, st, a, sc, M, g, slab, stride1, part, nparts);
       else
-        sym_bwd_pk_launch<D, false, false>(gt, grid, st, a, sc, M, g, slab, stride1, part, nparts);
+        sym_bwd_pk_launch<D, false, false>(gt, raw, grid, st, a, sc, M, g, slab, stride1, part, nparts);
       int rc = check_launch("ode_self_bwd(sym gp)");
       if (rc) return rc;
     }
@@ -962,9 +968,9 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   if (nq_own > 0) {
     const dim3 grid((unsigned)g.Kmax, (unsigned)nq_own);
     if (pk && b0)
-      sym_bwd_pk_launch<D, true, true>(gt, grid, st, a, sc, M, g, slab, stride, part, nparts);
+      sym_bwd_pk_launch<D, true, true>(gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else if (pk)
-      sym_bwd_pk_launch<D, true, false>(gt, grid, st, a, sc, M, g, slab, stride, part, nparts);
+      sym_bwd_pk_launch<D, true, false>(gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else
       sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
           a, sc, M, g.nG, g.L, slab, stride, part, nparts);

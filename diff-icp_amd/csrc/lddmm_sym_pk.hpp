@@ -25,7 +25,10 @@ namespace dicp {
 #ifndef DICP_SYMBWD_SCALAR_CT
 #define DICP_SYMBWD_SCALAR_CT 1
 #endif
-template <int D, bool GQ = true, bool B0 = false, bool GT = true>
+// RAW = true: coordinates in original units (Args::scale = 1, no shift, Scal::aux1 = s): z is
+// exact for nearby points whatever the cloud's extent; K = exp2(nc r2) costs one packed
+// multiply more per step (coord_raw).
+template <int D, bool GQ = true, bool B0 = false, bool GT = true, bool RAW = false>
 struct SymBwdPk {
   using S = SymBwd<D>;
   static constexpr int W = GQ ? 2 * D : D;
@@ -52,10 +55,11 @@ struct SymBwdPk {
   }
   struct Prm {
     float gt, c;  // gam s1 / alpha, s1 / alpha (SymBwd::Prm)
+    float nc, s2; // exponent multiplier (RAW), s / alpha^2 (kS2 scaled, s raw)
   };
   __device__ static Prm params(const Args& a, const Scal& sc) {
     const float cs = sc.aux1 / a.scale;
-    return Prm{sc.aux0 * cs, cs};
+    return Prm{sc.aux0 * cs, cs, sc.nc, RAW ? sc.s : kS2};
   }
   struct Row2 {
     f2 q[D], p[D], b[D], ia_a[D], gp[D];
@@ -74,7 +78,8 @@ struct SymBwdPk {
     f2 z[D], u[D];
     f2 K, w, cKzb;
   };
-  __device__ static void shared_terms(float c, const Row2& r, const f2* cv, Shared& t) {
+  __device__ static void shared_terms(const Prm& prm, const Row2& r, const f2* cv, Shared& t) {
+    const float c = prm.c;
     const f2* qj = cv;
     const f2* pj = cv + D;
     const f2* aj = cv + 2 * D;
@@ -86,7 +91,12 @@ struct SymBwdPk {
       t.z[d] = r.q[d] - qj[d];
       r2 = pk_fma(t.z[d], t.z[d], r2);
     }
-    t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    if constexpr (RAW) {
+      const f2 e = splat(prm.nc) * r2;
+      t.K = f2{fast_exp2(e.x), fast_exp2(e.y)};
+    } else {
+      t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    }
     if constexpr (B0) {
       // b = 0: u = gam (p_i - p_j), zb = 0
       if constexpr (GQ) {
@@ -99,7 +109,7 @@ struct SymBwdPk {
           zu = pk_fma(t.z[d], t.u[d], zu);
           iap = pk_fma(r.ia_a[d], pj[d], pk_fma(r.p[d], aj[d], iap));
         }
-        t.w = pk_fma(splat(kS2), zu, -iap);
+        t.w = pk_fma(splat(prm.s2), zu, -iap);
       }
       (void)bj;
       (void)c;
@@ -121,7 +131,7 @@ struct SymBwdPk {
         zb = pk_fma(t.z[d], db[d], zb);
         iap = pk_fma(r.ia_a[d], pj[d], pk_fma(r.p[d], aj[d], iap));
       }
-      t.w = pk_fma(splat(kS2), zu, -iap);
+      t.w = pk_fma(splat(prm.s2), zu, -iap);
       t.cKzb = (splat(c) * zb) * t.K;
     } else {
       f2 zb = t.z[0] * (r.b[0] - bj[0]);
@@ -136,7 +146,7 @@ struct SymBwdPk {
     f2 cv[5 * D];
     colvec(rec, cv);
     Shared t;
-    shared_terms(prm.c, r, cv, t);
+    shared_terms(prm, r, cv, t);
     const f2* pj = cv + D;
     const f2* aj = cv + 2 * D;
 #pragma unroll
@@ -156,7 +166,7 @@ struct SymBwdPk {
     f2 cv[5 * D];
     colvec(rec, cv);
     Shared t;
-    shared_terms(prm.c, r, cv, t);
+    shared_terms(prm, r, cv, t);
     const f2* pj = cv + D;
     const f2* aj = cv + 2 * D;
     if constexpr (!GT) {
@@ -412,11 +422,11 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
   }
 }
 
-template <int D, bool GQ, bool B0, bool GT>
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, DICP_SYMBWD_PK_WMAX))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
-  sym_pk_body<SymBwdPk<D, GQ, B0, GT>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdPk<D, GQ, B0, GT, RAW>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 // Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /

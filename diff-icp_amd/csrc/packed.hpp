@@ -24,21 +24,26 @@ __device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
 // ZS = true (eta = 0, DIV): the row's Z' sum also goes out, in original units, through the
 // h slot (which an Euler step does not use): zs_i = sum_j K (q_i - q_j) = Z'_i / alpha -- the
 // divergence rows the matching VJP reuses (OpOdeSelfFwdZs, sym_merge_kernel).
-template <int D, bool DIV, bool ETA = false, bool G = true, bool ZS = false>
+// RAW = true: coordinates in original units (the launcher sets Args::scale = 1, no shift,
+// Scal::aux1 = s): z = q_i - q_j is exact for nearby points whatever the cloud's extent, and
+// the exponent costs one packed multiply more per two pairs (K = exp2(nc r2)); every sum and
+// epilogue is otherwise the same (coord_raw).
+template <int D, bool DIV, bool ETA = false, bool G = true, bool ZS = false, bool RAW = false>
 struct OpOdeSelfFwdPk {
   static_assert(!ZS || (DIV && !ETA), "zs rows: eta = 0 with the divergence sums only");
   using Base = std::conditional_t<ZS, OpOdeSelfFwdZs<D>, OpOdeSelfFwd<D, ETA, DIV || ETA>>;
   // column splits as the full pass: the same chunk boundaries, hence bitwise the same v / g
-  using SplitAs = OpOdeSelfFwdPk<D, DIV, ETA, true>;
+  using SplitAs = OpOdeSelfFwdPk<D, DIV, ETA, true, false, RAW>;
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = Base::NACC;
   static constexpr int kNOut = Base::kNOut;
   static constexpr bool kMin = false;
   struct Row2 {
     f2 q[D], p[D];
+    f2 nc, s2;   // exponent multiplier (RAW) and s / alpha^2 (kS2 scaled, s raw)
   };
-  __device__ static void load_rows(const Args& a, int64_t i0, int64_t i1, Row2& r,
-                                   typename Base::Row& b0, typename Base::Row& b1) {
+  __device__ static void load_rows_s(const Args& a, const Scal& sc, int64_t i0, int64_t i1, Row2& r,
+                                     typename Base::Row& b0, typename Base::Row& b1) {
     Base::load_row(a, i0, b0);
     Base::load_row(a, i1, b1);
 #pragma unroll
@@ -46,6 +51,8 @@ struct OpOdeSelfFwdPk {
       r.q[d] = f2{b0.q[d], b1.q[d]};
       r.p[d] = f2{b0.p[d], b1.p[d]};
     }
+    r.nc = splat(sc.nc);
+    r.s2 = splat(RAW ? sc.s : kS2);
   }
   __device__ static void pair2(const Row2& r, const float* rec, f2* acc) {
     f2 z[D];
@@ -55,7 +62,13 @@ struct OpOdeSelfFwdPk {
       z[d] = r.q[d] - splat(rec[d]);
       r2 = pk_fma(z[d], z[d], r2);
     }
-    const f2 K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    f2 K;
+    if constexpr (RAW) {
+      const f2 e = r.nc * r2;
+      K = f2{fast_exp2(e.x), fast_exp2(e.y)};
+    } else {
+      K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    }
     const float* pj = rec + D;
     if constexpr (G) {
       f2 pp = r.p[0] * splat(pj[0]);
@@ -71,7 +84,7 @@ struct OpOdeSelfFwdPk {
       if (DIV || ETA) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
     }
     if (ETA) {  // OpOdeSelfFwd::pair, eta != 0 terms
-      const f2 sr2 = splat(kS2) * r2;
+      const f2 sr2 = r.s2 * r2;
       if constexpr (G) {  // Hs, GL' feed mG only
         f2 u[D];
 #pragma unroll
@@ -79,7 +92,7 @@ struct OpOdeSelfFwdPk {
         f2 zu = z[0] * u[0];
 #pragma unroll
         for (int d = 1; d < D; ++d) zu = pk_fma(z[d], u[d], zu);
-        const f2 szu = splat(kS2) * zu;
+        const f2 szu = r.s2 * zu;
         const f2 KGL = K * (sr2 - splat((float)(D + 2)));
 #pragma unroll
         for (int d = 0; d < D; ++d) {
