@@ -169,6 +169,8 @@ class coord_mode:
 def set_option(name: str, value: int):
     """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
     _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")
+    if name != "coord_raw":     # every other knob may change a workspace size
+        _WS_BYTES.clear()
 
 
 def _zero_b_ok(eta) -> bool:
@@ -208,11 +210,19 @@ def _dev(t: torch.Tensor, name: str) -> torch.Tensor:
 
 
 def _ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    # a plain int: ctypes converts it for the c_void_p parameters without an object per call
+    return None if t is None else t.data_ptr()
 
 
-def _stream(device) -> ctypes.c_void_p:
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _stream(device):
+    """Handle of the current HIP stream of `device` (torch's current stream: concurrent frames
+    set their own with torch.cuda.stream)."""
+    if _raw_stream is not None:
+        return _raw_stream(device.index if device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def _order(order, n: int, device):
@@ -302,8 +312,14 @@ def _launch(name, pairs, nbytes, fn):
     return r
 
 
+_WS_BYTES = {}   # (kind, M, N, D) -> dicp_workspace_bytes; cleared by set_option
+
+
 def _workspace(kind: int, M: int, N: int, D: int, device):
-    nbytes = int(lib().dicp_workspace_bytes(kind, int(M), int(N), int(D)))
+    key = (kind, int(M), int(N), int(D))
+    nbytes = _WS_BYTES.get(key)
+    if nbytes is None:
+        nbytes = _WS_BYTES[key] = int(lib().dicp_workspace_bytes(kind, int(M), int(N), int(D)))
     if nbytes == 0:
         return None, 0
     return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes

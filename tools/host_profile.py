@@ -1,7 +1,7 @@
-"""cProfile of the host side of one timed PSR iteration of the C2 bench workload (where the
-idle gaps of the device timeline come from).
+"""cProfile of one diff-ICP iteration at a small point count (device work negligible, so the
+profile is the host path: L-BFGS, autograd, wrappers, launches), on one GPU.
 
-    python tools/host_profile.py [--N 50000] > out.txt
+    python tools/host_profile.py [--N 2000] [--workload two_set|atlas] [--top 45]
 """
 import argparse
 import cProfile
@@ -18,7 +18,8 @@ from difficp_amd import workloads  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--N", type=int, default=50000)
+    ap.add_argument("--N", type=int, default=2000)
+    ap.add_argument("--top", type=int, default=45)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     psr = workloads.build_two_set(a.N, dev, seed=0)
@@ -29,11 +30,10 @@ def main():
     workloads.psr_iteration(psr)
     torch.cuda.synchronize()
     pr.disable()
-    s = io.StringIO()
-    st = pstats.Stats(pr, stream=s)
-    st.sort_stats("tottime").print_stats(35)
-    st.sort_stats("cumulative").print_stats(35)
-    print(s.getvalue())
+    for key in ("tottime", "cumulative"):
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(a.top)
+        print(s.getvalue())
 
 
 if __name__ == "__main__":
