@@ -340,7 +340,8 @@ const char* dicp_last_error(void);
 const char* dicp_version(void);
 /* 1 if D is compiled in. */
 int dicp_supports_dim(int D);
-/* Tuning / A-B knobs (process-wide; results of every setting agree to fp32 summation order):
+/* Tuning / A-B knobs (process-wide unless stated; results of every setting agree to fp32
+ * summation order):
  *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
  *                  rows (default), 3 channel contraction on the matrix cores (opt-in; fp32
  *                  error bounded by the rows' spread: pass a spatial row_order), 4 symmetric
@@ -351,6 +352,15 @@ int dicp_supports_dim(int D);
  *   "bwd_eta_alg"  eta != 0 VJP: 0 ordered, 1 symmetric, 2 symmetric packed-FP32 (default)
  *   "r_fwd" / "r_bwd"  rows per thread {1,2,4} of the ordered passes (env DICP_R_FWD / DICP_R_BWD)
  *   "split_rounds", "force_splits", "sym_L"  column-split / symmetric-chunk geometry (0 = auto)
+ *   "red_alg"      KBase / KRedScal / KRed / GradKRed and the external-point forward: 0 never
+ *                  the centred expansion, 1 automatic by size (default), 2 always
+ *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
+ *   "ext_alg"      KRed and the external-point passes below the centred sizes: 0 generic
+ *                  scalar rows, 1 packed-FP32 rows (default)
+ *   "coord_raw"    PER HOST THREAD: 1 runs the default packed shooting kernels (fwd_alg 2,
+ *                  bwd_alg 3) in original-unit coordinates -- exact pair differences at any
+ *                  cloud extent, one packed multiply more per two pairs; 0 (default) scaled
+ *                  coordinates alpha (q - q_0), float32-exact up to ~200 sigma of extent
  * Returns DICP_ERR_INVALID for an unknown name or an out-of-range value. */
 int dicp_set_option(const char* name, int value);
 /* Current value of a knob of dicp_set_option (same names; the compile-time defaults until
