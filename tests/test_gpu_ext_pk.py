@@ -119,3 +119,27 @@ def test_kred_paths(dev, path, N, M, D):
         out = _lib.gauss_red(_lib.KRED, xf, yf, SIG, b=bf)
     ref, _ = F.ext_terms(xf.double(), yf.double(), bf.double(), SIG, 0.0)
     assert rel_err(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("path", ["packed", "generic"])
+def test_empty_support_and_points(dev, path):
+    """No support points: v(x) = 0, divergence rows 0, gx = 0; no external points: empty gx and
+    the accumulators untouched (LDDMM.py:111-112, 131-132)."""
+    from difficp_amd import _lib
+    x = torch.rand(37, 3, device=dev)
+    a = torch.randn(37, 3, device=dev)
+    q0 = torch.empty(0, 3, device=dev)
+    gd = torch.full((1,), 0.3, device=dev)
+    with options(**PATHS[path]):
+        vx, gx = _lib.ode_ext_fwd(x, q0, q0, SIG, 0.0, True)
+        assert vx.shape == (37, 3) and not vx.abs().any() and not gx.abs().any()
+        gxb = _lib.ode_ext_bwd(x, q0, q0, a, gd, SIG, 0.0, torch.empty(0, 3, device=dev),
+                               torch.empty(0, 3, device=dev))
+        assert gxb.shape == (37, 3) and not gxb.abs().any()
+        kr = _lib.gauss_red(_lib.KRED, x, q0, SIG, b=q0)
+        assert kr.shape == (37, 3) and not kr.abs().any()
+        q = torch.rand(11, 3, device=dev)
+        gq, gp = torch.ones(11, 3, device=dev), torch.ones(11, 3, device=dev)
+        e = torch.empty(0, 3, device=dev)
+        gxe = _lib.ode_ext_bwd(e, q, q, e, gd, SIG, 0.0, gq, gp)
+        assert gxe.shape == (0, 3) and bool((gq == 1).all()) and bool((gp == 1).all())
