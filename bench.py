@@ -213,9 +213,10 @@ def kernel_sum_probe(dev, M, reps=5):
     fl = _lib.FLOPS_PER_PAIR.get("gauss_red", 15)
     # the compute bound of the sum is max(flops / P_fp32, exps / P_exp)
     bound_s = max(pairs * fl / (FP32_PEAK_TFLOPS * 1e12), pairs * 1.0 / (EXP_PEAK_TPS * 1e12))
-    path = ("centred expansion (csrc/centred.hpp: Morton-sorted 64-column sub-tiles, 7 VALU + 1 exp "
-            "per pair, prep pass included in the time)" if _lib.get_option("red_alg") and M >= 16384
-            else "generic skeleton (common.hpp)")
+    path = ("centred expansion (csrc/centred.hpp: Morton-sorted 64-column sub-tiles, 6 FMA + 1 exp "
+            "per pair, 4 rows per thread packed in pairs, prep pass included in the time)"
+            if _lib.get_option("red_alg") and M >= 32768 and float(M) * M >= 2.5e9
+            else "packed scaled-coordinate kernel (ext_pk.hpp)")
     return {"op": "KRed (kernel.py:138) x = y, D = 3, sigma 0.1", "M": M, "ms": round(best, 4),
             "path": path, "Tpair_per_s": round(pairs / s / 1e12, 3),
             "tflops": round(pairs * fl / s / 1e12, 2), "frac_fp32_peak": round(pairs * fl / s / 1e12 / FP32_PEAK_TFLOPS, 4),

@@ -88,12 +88,14 @@ bool cx_eligible(int64_t M, int64_t N, bool ext) {
   if (red_alg() == 2) return M > 0 && N > 0;
   // the prep pass (bounding box, Morton codes, radix sort, records) costs ~40-60 us: measured
   // break-even against the generic reductions between 20k x 20k (0.8x) and 50k x 50k (1.09x),
-  // at 100k rows x 20k columns (1.04x) (tools/cx_ab.py, profiles/r03_ab_centred_shapes.json).
+  // at 100k rows x 20k columns (1.04x) (tools/cx_ab.py, profiles/r03_ab_centred_shapes.json);
+  // with the packed scaled-coordinate KRed below it, the centred form wins from 50k x 50k
+  // (1.04x) and loses at 100k x 20k (0.91x) and 30k x 30k (0.80x) (profiles/r03_ab_cx_r4.json).
   // The external-point forward has a packed scaled-coordinate kernel below these sizes
   // (ext_pk.hpp, 1.2x the generic one), which the centred form only beats from ~50k x 50k on
   // (tools/ext_ab.py, profiles/r03_ab_ext_packed.json).
   if (ext) return N >= 32768 && (double)M * (double)N >= 2.5e9;
-  return N >= 16384 && (double)M * (double)N >= 2.0e9;
+  return N >= 32768 && (double)M * (double)N >= 2.5e9;
 }
 
 // Launch the centred reduction Op over rows x (M, D) and columns (y, fields in a.c1..) (N).
@@ -174,7 +176,7 @@ int launch_cx(const char* name, const float* x, int64_t M, Args a, int64_t N, do
 }
 
 #ifndef DICP_CX_R
-#define DICP_CX_R 2
+#define DICP_CX_R 4
 #endif
 constexpr int kCxR = DICP_CX_R;  // rows per thread
 

@@ -30,15 +30,36 @@
 #pragma once
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
+#include "packed.hpp"
 
 namespace dicp {
+
+// The compact pair terms are written once for a scalar row (T = float) and for two rows
+// packed in one VGPR pair (T = f2: every fma is one v_pk_fma_f32, the column field broadcast
+// into both halves), so the packed loop is bitwise the scalar one.
+template <class T> __device__ __forceinline__ T bc(float x);
+template <> __device__ __forceinline__ float bc<float>(float x) { return x; }
+template <> __device__ __forceinline__ f2 bc<f2>(float x) { return splat(x); }
+__device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return pk_fma(a, b, c); }
 
 constexpr int kSub = 64;  // columns per centred sub-tile (one wave64 in the prep pass)
 constexpr float kCxShift = 16.f;     // m: exponent shift between the row factor and the pair term
 constexpr float kCxClamp = 14.f;     // |X| clamp (see above); needs rho <= kCxRhoCap
 constexpr float kCxRhoCap = 4.f;     // largest sub-tile radius the expanded form accepts
+#ifndef DICP_CX_PK
+#define DICP_CX_PK 1
+#endif
+constexpr bool kCxPk = DICP_CX_PK != 0;  // packed compact loop (two rows per v_pk_fma_f32)
 
-// ---- ops: record = [2Y (D) | -|Y|^2 | fields... | y (D, raw)] ------------------------------
+// ---- ops: record = [2Y_0, 2Y_1 | c, c | 2Y_2 (D = 3) | fields... | y (D, raw)] -------------
+// c = -|Y|^2 - m, stored twice: the packed loop takes the aligned pair (rec[2], rec[3]) as the
+// exponent's initial value for both rows without a register copy, and a D = 3 KRed record's
+// compact part is two whole float4s (ds_read_b128: 4 LDS cycles per wave; a 3-float tail
+// would be a ds_read_b96, 8 cycles, MI355X_MICROARCH.md LDS table).
+constexpr int kCxC = 2;                                            // c, c at rec[2], rec[3]
+template <int D> constexpr int cx_f = D + 2;                       // first field
+__host__ __device__ constexpr int cx_y(int d) { return d < 2 ? d : d + 2; }   // 2Y_d
 // pair(K, e, rec, acc): compact sub-tiles (K without the row factor F, e its exponent);
 // pair_z(K, e, z, rec, acc): wide sub-tiles, z = alpha (x - y) from raw coordinates, the
 // z-linear sums accumulated directly in the slots the compact form uses for its Y sums;
@@ -52,11 +73,12 @@ struct CxBase {
 // KBase: sum_j K                                                     kernel.py:131 / :178
 template <int D>
 struct CxKBase : CxBase<D> {
-  static constexpr int kRaw = D + 1;
-  static constexpr int RW4 = cw4(2 * D + 1), NACC = 1, NTOT = 1, kNOut = 1;
+  static constexpr int kRaw = cx_f<D>;
+  static constexpr int RW4 = cw4(kRaw + D), NACC = 1, NTOT = 1, kNOut = 1;
   static constexpr int kOutW[4] = {1, 0, 0, 0};
   __device__ static void build(const Args&, int64_t, const float*, float*) {}
-  __device__ static void pair(float K, float, const float*, float* acc) { acc[0] += K; }
+  template <class T>
+  __device__ static void pair(T K, T, const float*, T* acc) { acc[0] += K; }
   __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
   __device__ static void fold(const float*, const float* acc, float* tot, bool c, float F, float) {
     tot[0] = fmaf(c ? F : 1.f, acc[0], tot[0]);
@@ -67,11 +89,12 @@ struct CxKBase : CxBase<D> {
 // KRedScal: sum_j K d_j                                              kernel.py:135 / :182
 template <int D>
 struct CxKRedScal : CxBase<D> {
-  static constexpr int kRaw = D + 2;
-  static constexpr int RW4 = cw4(2 * D + 2), NACC = 1, NTOT = 1, kNOut = 1;
+  static constexpr int kRaw = cx_f<D> + 1;
+  static constexpr int RW4 = cw4(kRaw + D), NACC = 1, NTOT = 1, kNOut = 1;
   static constexpr int kOutW[4] = {1, 0, 0, 0};
-  __device__ static void build(const Args& a, int64_t o, const float*, float* rec) { rec[D + 1] = a.c1[o]; }
-  __device__ static void pair(float K, float, const float* rec, float* acc) { acc[0] = fmaf(K, rec[D + 1], acc[0]); }
+  __device__ static void build(const Args& a, int64_t o, const float*, float* rec) { rec[cx_f<D>] = a.c1[o]; }
+  template <class T>
+  __device__ static void pair(T K, T, const float* rec, T* acc) { acc[0] = vfma(K, bc<T>(rec[cx_f<D>]), acc[0]); }
   __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
   __device__ static void fold(const float*, const float* acc, float* tot, bool c, float F, float) {
     tot[0] = fmaf(c ? F : 1.f, acc[0], tot[0]);
@@ -82,16 +105,17 @@ struct CxKRedScal : CxBase<D> {
 // KRed: sum_j K b_j  (the velocity field, LDDMM.py:114)             kernel.py:138 / :186
 template <int D>
 struct CxKRed : CxBase<D> {
-  static constexpr int kRaw = 2 * D + 1;
-  static constexpr int RW4 = cw4(3 * D + 1), NACC = D, NTOT = D, kNOut = 1;
+  static constexpr int kRaw = cx_f<D> + D;
+  static constexpr int RW4 = cw4(kRaw + D), NACC = D, NTOT = D, kNOut = 1;
   static constexpr int kOutW[4] = {D, 0, 0, 0};
   __device__ static void build(const Args& a, int64_t o, const float*, float* rec) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) rec[D + 1 + d] = a.c1[o * D + d];
+    for (int d = 0; d < D; ++d) rec[cx_f<D> + d] = a.c1[o * D + d];
   }
-  __device__ static void pair(float K, float, const float* rec, float* acc) {
+  template <class T>
+  __device__ static void pair(T K, T, const float* rec, T* acc) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + 1 + d], acc[d]);
+    for (int d = 0; d < D; ++d) acc[d] = vfma(K, bc<T>(rec[cx_f<D> + d]), acc[d]);
   }
   __device__ static void pair_z(float K, float e, const float*, const float* rec, float* acc) { pair(K, e, rec, acc); }
   __device__ static void fold(const float*, const float* acc, float* tot, bool c, float F, float) {
@@ -109,14 +133,15 @@ struct CxKRed : CxBase<D> {
 // (wide sub-tiles: -(s/alpha) sum K z' accumulated directly)
 template <int D>
 struct CxGradK : CxBase<D> {
-  static constexpr int kRaw = D + 1;
-  static constexpr int RW4 = cw4(2 * D + 1), NACC = D + 1, NTOT = D, kNOut = 1;
+  static constexpr int kRaw = cx_f<D>;
+  static constexpr int RW4 = cw4(kRaw + D), NACC = D + 1, NTOT = D, kNOut = 1;
   static constexpr int kOutW[4] = {D, 0, 0, 0};
   __device__ static void build(const Args&, int64_t, const float*, float*) {}
-  __device__ static void pair(float K, float, const float* rec, float* acc) {
+  template <class T>
+  __device__ static void pair(T K, T, const float* rec, T* acc) {
     acc[0] += K;
 #pragma unroll
-    for (int d = 0; d < D; ++d) acc[1 + d] = fmaf(K, rec[d], acc[1 + d]);  // sum K 2Y
+    for (int d = 0; d < D; ++d) acc[1 + d] = vfma(K, bc<T>(rec[cx_y(d)]), acc[1 + d]);  // sum K 2Y
   }
   __device__ static void pair_z(float K, float, const float* z, const float*, float* acc) {
 #pragma unroll
@@ -139,8 +164,9 @@ struct CxGradK : CxBase<D> {
 //   sum K (z.p_j) = (X.sum K p - sum K (Y.p_j)) / alpha  (w_j = Y.p_j in the record).
 template <int D, bool ETA, bool DIV>
 struct CxExtFwd : CxBase<D> {
-  static constexpr int kW = 2 * D + 1;                       // w_j slot
-  static constexpr int kRaw = 2 * D + 1 + (DIV ? 1 : 0);
+  static constexpr int kP = cx_f<D>;                         // p_j slots
+  static constexpr int kW = kP + D;                          // w_j slot
+  static constexpr int kRaw = kP + D + (DIV ? 1 : 0);
   static constexpr int RW4 = cw4(kRaw + D);
   // acc: V (D) | W | K, K2Y (D), Ke  (wide sub-tiles: W <- sum K (z.p), K2Y <- sum K z)
   static constexpr int oW = D, oK = D + (DIV ? 1 : 0);
@@ -155,26 +181,27 @@ struct CxExtFwd : CxBase<D> {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const float pd = a.c1[o * D + d];
-      rec[D + 1 + d] = pd;
+      rec[kP + d] = pd;
       w = fmaf(Yc[d], pd, w);
     }
     if (DIV) rec[kW] = w;
   }
-  __device__ static void pair(float K, float e, const float* rec, float* acc) {
+  template <class T>
+  __device__ static void pair(T K, T e, const float* rec, T* acc) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + 1 + d], acc[d]);
-    if (DIV) acc[oW] = fmaf(K, rec[kW], acc[oW]);
+    for (int d = 0; d < D; ++d) acc[d] = vfma(K, bc<T>(rec[kP + d]), acc[d]);
+    if (DIV) acc[oW] = vfma(K, bc<T>(rec[kW]), acc[oW]);
     if (ETA) {
       acc[oK] += K;
 #pragma unroll
-      for (int d = 0; d < D; ++d) acc[oK + 1 + d] = fmaf(K, rec[d], acc[oK + 1 + d]);
-      acc[oK + 1 + D] = fmaf(K, e, acc[oK + 1 + D]);
+      for (int d = 0; d < D; ++d) acc[oK + 1 + d] = vfma(K, bc<T>(rec[cx_y(d)]), acc[oK + 1 + d]);
+      acc[oK + 1 + D] = vfma(K, e, acc[oK + 1 + D]);
     }
   }
   __device__ static void pair_z(float K, float e, const float* z, const float* rec, float* acc) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[D + 1 + d], acc[d]);
-    if (DIV) acc[oW] = fmaf(K, dot<D>(z, rec + D + 1), acc[oW]);
+    for (int d = 0; d < D; ++d) acc[d] = fmaf(K, rec[kP + d], acc[d]);
+    if (DIV) acc[oW] = fmaf(K, dot<D>(z, rec + kP), acc[oW]);
     if (ETA) {
       acc[oK] += K;
 #pragma unroll
@@ -327,7 +354,7 @@ __global__ __launch_bounds__(256) void cx_codes_kernel(const float* __restrict__
 }
 
 // One wave per sub-tile of 64 sorted columns: the sub-tile centre (mid-range of its scaled
-// coordinates), its radius, and the column records [2Y | -|Y|^2 | fields] relative to it.
+// coordinates), its radius, and the column records (layout above) relative to it.
 // meta[t] = (raw centre (D), 1 if the sub-tile is compact (scaled radius^2 <= rho2max) else 0).
 template <int D, class Op>
 __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float alpha, float rho2max,
@@ -368,10 +395,10 @@ __global__ __launch_bounds__(256) void cx_build_kernel(Args a, int64_t N, float 
     for (int k = 0; k < Op::RW4 * 4; ++k) rec[k] = 0.f;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      rec[d] = 2.f * Yc[d];
+      rec[cx_y(d)] = 2.f * Yc[d];
       rec[Op::kRaw + d] = y[d];
     }
-    rec[D] = -r2 - kCxShift;
+    rec[kCxC] = rec[kCxC + 1] = -r2 - kCxShift;
     Op::build(a, o, Yc, rec);
 #pragma unroll
     for (int k = 0; k < Op::RW4; ++k)
@@ -461,7 +488,41 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
         for (int k = 0; k < Op::NACC; ++k) acc[r][k] = 0.f;
       }
       const float4* tile = lds[buf] + b0 * RW4;
-      if (compact) {  // compact sub-tile: expanded exponent, D fma
+      if (compact && kCxPk && R % 2 == 0) {  // compact, rows packed in pairs (v_pk_fma_f32)
+        constexpr int H = R / 2;
+        f2 Xp[H][D], ap[H][Op::NACC];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+#pragma unroll
+          for (int d = 0; d < D; ++d) Xp[h][d] = f2{X[2 * h][d], X[2 * h + 1][d]};
+#pragma unroll
+          for (int k = 0; k < Op::NACC; ++k) ap[h][k] = splat(0.f);
+        }
+        constexpr int CW = (Op::kRaw + 3) / 4;  // float4s of the record the compact terms read
+#pragma unroll 2
+        for (int t = 0; t < n; ++t) {
+          float rec[RW4 * 4];
+#pragma unroll
+          for (int k = 0; k < CW; ++k) {
+            const float4 q = tile[t * RW4 + k];
+            rec[4 * k] = q.x; rec[4 * k + 1] = q.y; rec[4 * k + 2] = q.z; rec[4 * k + 3] = q.w;
+          }
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            f2 e = f2{rec[kCxC], rec[kCxC + 1]};
+#pragma unroll
+            for (int d = 0; d < D; ++d) e = pk_fma(Xp[h][d], splat(rec[cx_y(d)]), e);
+            Op::pair(f2{fast_exp2(e.x), fast_exp2(e.y)}, e, rec, ap[h]);
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < H; ++h)
+#pragma unroll
+          for (int k = 0; k < Op::NACC; ++k) {
+            acc[2 * h][k] = ap[h][k].x;
+            acc[2 * h + 1][k] = ap[h][k].y;
+          }
+      } else if (compact) {  // compact sub-tile: expanded exponent, D fma
 #pragma unroll 2
         for (int t = 0; t < n; ++t) {
           float rec[RW4 * 4];
@@ -472,9 +533,9 @@ __global__ __launch_bounds__(kBlock) void cx_kernel(const float* __restrict__ x,
           }
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            float e = rec[D];
+            float e = rec[kCxC];
 #pragma unroll
-            for (int d = 0; d < D; ++d) e = fmaf(X[r][d], rec[d], e);
+            for (int d = 0; d < D; ++d) e = fmaf(X[r][d], rec[cx_y(d)], e);
             Op::pair(fast_exp2(e), e, rec, acc[r]);
           }
         }

@@ -27,6 +27,11 @@ def main():
     mu2 = (q * q).sum(-1)
     w2 = torch.zeros(M, device=dev)
     zs = torch.empty_like(q)
+    if os.environ.get("PMC_OPS") == "kred":   # the north_star's kernel sum alone (centred path)
+        for _ in range(5):
+            _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)
+        torch.cuda.synchronize()
+        return
     # the variants the bench's timed Euler steps run (shooting.ShootFn, t = 1..nt-2): the fused
     # forward step writing the divergence rows zs, and the full adjoint step reusing them
     for _ in range(3):
