@@ -188,6 +188,38 @@ __global__ __launch_bounds__(256) void bf16_mix_probe(float* out, int iters, flo
   if (s == 12345.f) out[threadIdx.x] = s;
 }
 
+// FMA / transcendental co-issue probe: per iteration 16 independent FMA chains and NE v_exp_f32
+// whose inputs are chain values and whose results are the next iteration's multipliers of NE
+// chains (no extra instructions); compare the time per iteration across NE = 0, 2, 4, 8:
+// + ~10 SIMD cycles per exp = the exps serialise with the FMAs, + ~2 = they overlap.
+template <int NE, bool ILV = false>
+__global__ __launch_bounds__(256) void coissue_probe(float* out, int iters, float seed) {
+  float a[16], m[16];
+  const float c = seed * 0.999f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    a[k] = seed * (threadIdx.x + k) * 1e-3f;
+    m[k] = seed * (0.5f + k * 1e-3f);
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = fmaf(a[k], m[k], c);
+#pragma unroll
+    for (int r = 0; r < NE; ++r) m[r] = __builtin_amdgcn_exp2f(a[(r + 8) & 15]);
+    if constexpr (ILV) {  // one transcendental, then 16 / NE FMAs, repeated (LLVM sched groups)
+#pragma unroll
+      for (int r = 0; r < NE; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x0400, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0002, 16 / NE, 0);
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += a[k] + m[k];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
 template <int CTRL>
 __global__ __launch_bounds__(64) void dpp_probe(int* out) {
   const int l = threadIdx.x;
@@ -206,7 +238,9 @@ extern "C" int dicp_mb_dpp(int which, int* out, void* stream) {
 }
 
 // kind: 0 = exp2, 1 = fma, 2 = pk_fma, 3 = dpp(wave_rol:1)+add, 4 = dpp(row_ror:1)+add,
-// 5 = kChains fma + 1 exp2 per iteration, 10..13 = mfma_mix_probe<kind - 10>.  Returns 0 on
+// 5 = kChains fma + 1 exp2 per iteration, 10..13 = mfma_mix_probe<kind - 10>,
+// 30..33 = coissue_probe<0, 2, 4, 8> (16 fma + NE exp2 per iteration), 34 / 35 = NE 4 / 2
+// interleaved one exp per 16 / NE fma.  Returns 0 on
 // success.  ops per launch: blocks*256*iters*kChains (x2 lanes for pk_fma).
 extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -221,6 +255,12 @@ extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void*
   else if (kind == 11) mfma_mix_probe<1><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 12) mfma_mix_probe<2><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 13) mfma_mix_probe<3><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 30) coissue_probe<0><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 31) coissue_probe<2><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 32) coissue_probe<4><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 33) coissue_probe<8><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 34) coissue_probe<4, true><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 35) coissue_probe<2, true><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 20) bf16_mix_probe<0><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 21) bf16_mix_probe<1><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 22) bf16_mix_probe<2><<<g, b, 0, st>>>(out, iters, 1.0f);
