@@ -42,6 +42,37 @@ struct OpOdeSelfFwdPk {
     f2 q[D], p[D];
     f2 nc, s2;   // exponent multiplier (RAW) and s / alpha^2 (kS2 scaled, s raw)
   };
+  // LDS column record of the packed pair: D = 3 as [q (3) | q_z | p (3) | p_z], so that the
+  // z components are the aligned register pairs (.z, .w) of one ds_read_b128 each instead of
+  // broadcasts, which the register allocator materialises with a v_mov per column (the x / y
+  // broadcasts go through op_sel); D = 2 keeps the base record [q | p]
+#ifndef DICP_FWD_PK_REC4
+#define DICP_FWD_PK_REC4 1
+#endif
+  static constexpr int kP = (DICP_FWD_PK_REC4 && D == 3) ? 4 : D;
+  static_assert(kP + D <= 4 * CW4, "record fits the base op's float4s");
+  __device__ static void load_col_pk(const Args& a, const Scal& sc, int64_t j, float* rec) {
+    float t[4 * CW4];
+    op_load_col<Base>(a, sc, j, t);
+#pragma unroll
+    for (int k = 0; k < 4 * CW4; ++k) rec[k] = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      rec[d] = t[d];
+      rec[kP + d] = t[D + d];
+    }
+    if (kP > D) {
+      rec[D] = t[D - 1];
+      rec[kP + D] = t[2 * D - 1];
+    }
+  }
+  // column field d of the record as a broadcast pair (the duplicated z components: the pair)
+  __device__ static f2 colq(const float* rec, int d) {
+    return (kP > D && d == D - 1) ? f2{rec[d], rec[D]} : splat(rec[d]);
+  }
+  __device__ static f2 colp(const float* rec, int d) {
+    return (kP > D && d == D - 1) ? f2{rec[kP + d], rec[kP + D]} : splat(rec[kP + d]);
+  }
   __device__ static void load_rows_s(const Args& a, const Scal& sc, int64_t i0, int64_t i1, Row2& r,
                                      typename Base::Row& b0, typename Base::Row& b1) {
     Base::load_row(a, i0, b0);
@@ -59,7 +90,7 @@ struct OpOdeSelfFwdPk {
     f2 r2 = splat(0.f);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      z[d] = r.q[d] - splat(rec[d]);
+      z[d] = r.q[d] - colq(rec, d);
       r2 = pk_fma(z[d], z[d], r2);
     }
     f2 K;
@@ -69,18 +100,20 @@ struct OpOdeSelfFwdPk {
     } else {
       K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
     }
-    const float* pj = rec + D;
-    if constexpr (G) {
-      f2 pp = r.p[0] * splat(pj[0]);
+    f2 pj[D];
 #pragma unroll
-      for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], splat(pj[d]), pp);
+    for (int d = 0; d < D; ++d) pj[d] = colp(rec, d);
+    if constexpr (G) {
+      f2 pp = r.p[0] * pj[0];
+#pragma unroll
+      for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], pj[d], pp);
       const f2 Kpp = K * pp;
 #pragma unroll
       for (int d = 0; d < D; ++d) acc[D + d] = pk_fma(Kpp, z[d], acc[D + d]);
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      acc[d] = pk_fma(K, splat(pj[d]), acc[d]);
+      acc[d] = pk_fma(K, pj[d], acc[d]);
       if (DIV || ETA) acc[2 * D + d] = pk_fma(K, z[d], acc[2 * D + d]);
     }
     if (ETA) {  // OpOdeSelfFwd::pair, eta != 0 terms
@@ -88,7 +121,7 @@ struct OpOdeSelfFwdPk {
       if constexpr (G) {  // Hs, GL' feed mG only
         f2 u[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) u[d] = r.p[d] - splat(pj[d]);
+        for (int d = 0; d < D; ++d) u[d] = r.p[d] - pj[d];
         f2 zu = z[0] * u[0];
 #pragma unroll
         for (int d = 1; d < D; ++d) zu = pk_fma(z[d], u[d], zu);
@@ -121,6 +154,17 @@ struct has_rows_s : std::false_type {};
 template <class T>
 struct has_rows_s<T, std::void_t<decltype(&T::load_rows_s)>> : std::true_type {};
 
+// packed ops may lay the LDS column record out for their pair2 (load_col_pk)
+template <class T, class = void>
+struct has_col_pk : std::false_type {};
+template <class T>
+struct has_col_pk<T, std::void_t<decltype(&T::load_col_pk)>> : std::true_type {};
+template <class Op>
+__device__ __forceinline__ void pk_load_col(const Args& a, const Scal& sc, int64_t j, float* rec) {
+  if constexpr (has_col_pk<Op>::value) Op::load_col_pk(a, sc, j, rec);
+  else op_load_col<typename Op::Base>(a, sc, j, rec);
+}
+
 template <class Op>
 __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
                                                            int64_t chunk, Outs outs) {
@@ -151,7 +195,7 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
   float pre[CW4 * 4];
   int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
   if (cnt > 0 && tid < cnt) {
-    op_load_col<Base>(args, sc, j0 + tid, pre);
+    pk_load_col<Op>(args, sc, j0 + tid, pre);
 #pragma unroll
     for (int k = 0; k < CW4; ++k)
       lds[0][tid * CW4 + k] = make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
@@ -162,7 +206,7 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
     const int64_t jn = jt + kTile;
     const int cntn = jn < j1 ? (int)((j1 - jn) < kTile ? (j1 - jn) : kTile) : 0;
     if (tid < cntn) {
-      op_load_col<Base>(args, sc, jn + tid, pre);
+      pk_load_col<Op>(args, sc, jn + tid, pre);
 #pragma unroll
       for (int k = 0; k < CW4; ++k)
         lds[buf ^ 1][tid * CW4 + k] =

@@ -4,7 +4,9 @@ external-point forward (eta = 0 and eta != 0, with the divergence row), each bui
 subprocess (DICP_LIB_PATH), builds alternated `--passes` times, minimum per op reported;
 outputs of every build are compared bitwise with the first build's.
 
-    python tools/cx_pk_ab.py [--M 100000] [--passes 2] [--out f.json] base cxpk0 cxr4 ...
+    python tools/cx_pk_ab.py [--M 100000] [--passes 2] [--set cx|fwd] [--out f.json] base cxpk0 ...
+(--set fwd: the fused self forward -- Euler step with divergence rows, without mG, eta != 0,
+with the Hamiltonian rows -- instead of the centred reductions)
 ("base" = the default in-tree library.)
 """
 import argparse
@@ -27,12 +29,19 @@ g = torch.Generator().manual_seed(M)
 x = torch.rand(M, 3, generator=g).to(dev)
 b = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
 xe = torch.rand(M, 3, generator=g).to(dev)
-L.set_option("red_alg", 2)
-fns = {"KRed": lambda: L.gauss_red(L.KRED, x, x, 0.1, b=b),
-       "GradKRed": lambda: L.gauss_red(L.GRADK, x, x, 0.1),
-       "KBase": lambda: L.gauss_red(L.KBASE, x, x, 0.1),
-       "ext_fwd_eta0": lambda: L.ode_ext_fwd(xe, x, b, 0.1, 0.0, True),
-       "ext_fwd_eta": lambda: L.ode_ext_fwd(xe, x, b, 0.1, 1e-3, True)}
+zs = torch.empty_like(x)
+if %r == "fwd":   # the fused self forward (packed.hpp) in the variants the shooting runs
+    fns = {"step_zs": lambda: L.euler_step(x, b, 0.1, 0.0, 0.1, True, zs_out=zs),
+           "step_nog": lambda: L.euler_step(x, b, 0.1, 0.0, 0.1, True, want_p=False),
+           "fwd_eta": lambda: L.ode_self_fwd(x, b, 0.1, 1e-3, True),
+           "fwd_h": lambda: L.ode_self_fwd(x, b, 0.1, 0.0, True, want_h=True)}
+else:
+    L.set_option("red_alg", 2)
+    fns = {"KRed": lambda: L.gauss_red(L.KRED, x, x, 0.1, b=b),
+           "GradKRed": lambda: L.gauss_red(L.GRADK, x, x, 0.1),
+           "KBase": lambda: L.gauss_red(L.KBASE, x, x, 0.1),
+           "ext_fwd_eta0": lambda: L.ode_ext_fwd(xe, x, b, 0.1, 0.0, True),
+           "ext_fwd_eta": lambda: L.ode_ext_fwd(xe, x, b, 0.1, 1e-3, True)}
 out, digest = {}, {}
 for k, fn in fns.items():
     r = fn()
@@ -57,6 +66,7 @@ def main():
     ap.add_argument("--M", type=int, default=100000)
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--set", default="cx", choices=["cx", "fwd"])
     ap.add_argument("names", nargs="+")
     a = ap.parse_args()
     res, dig = {}, {}
@@ -65,7 +75,7 @@ def main():
             env = dict(os.environ)
             if name != "base":
                 env["DICP_LIB_PATH"] = os.path.join(VAR, f"libdifficp_hip_{name}.so")
-            r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, a.M)], env=env,
+            r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, a.M, a.set)], env=env,
                                capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 res.setdefault(name, {})["error"] = r.stderr[-800:]

@@ -13,11 +13,12 @@ _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs)
 fn = lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs)
 st = torch.cuda.current_stream()
 res = {}
-for L in (4, 6, 8, 3):
+Ls = tuple(int(v) for v in os.environ.get("SYM_LS", "4,6,8,3").split(","))
+for L in Ls:
     _lib.set_option("sym_L", L); fn()
 torch.cuda.synchronize()
 for _ in range(4):
-    for L in (4, 6, 8, 3):
+    for L in Ls:
         _lib.set_option("sym_L", L)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
