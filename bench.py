@@ -40,6 +40,9 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (vector v_pk_fma_f32 = f32 MFMA),
 # ISSUE cost") -> 64 / 8 lanes per cycle x 1024 SIMDs x 2.4 GHz
 EXP_PEAK_TPS = 64 / 8 * 1024 * 2.4e9 / 1e12
 HBM_PEAK_GBPS = 8000.0
+# measured issue costs on MI355X (tools/probes/coissue.py, profiles/r03_probe_coissue.json): SIMD
+# cycles per wave64 instruction at the nominal 2.4 GHz; a v_exp_f32 does not overlap the FMAs
+FMA_ISSUE_CYC, EXP_ISSUE_CYC = 2.36, 10.2
 
 # BASELINE.json "metric": value is the PSR iterations/sec half; the kernel-sum HBM GB/s half
 # (algorithmic bytes of all hot-path launches / their summed device time) is kernel_sum_hbm_GBps
@@ -224,6 +227,11 @@ def kernel_sum_probe(dev, M, reps=5):
             "frac_of_compute_bound": round(bound_s / s, 4),
             "compute_bound": (f"max(15 flop x M^2 / {FP32_PEAK_TFLOPS} TFLOP/s, 1 exp x M^2 / "
                               f"{EXP_PEAK_TPS:.2f} Texp/s) (SURVEY 8(d))"),
+            # the pair loop's instruction-stream floor: 6 FMA + 1 exp per pair (centred path) at
+            # the probed issue costs, 1024 SIMDs x 64 lanes at 2.4 GHz -- what the kernel could
+            # reach if nothing but its pair arithmetic issued (no prep, sub-tile or loop work)
+            "issue_floor_ms": round(pairs / 64 / 1024 * (6 * FMA_ISSUE_CYC + EXP_ISSUE_CYC) / 2.4e9 * 1e3, 4),
+            "frac_of_issue_floor": round(pairs / 64 / 1024 * (6 * FMA_ISSUE_CYC + EXP_ISSUE_CYC) / 2.4e9 / s, 4),
             "alg_hbm_GBps": round(4 * 12 * M / s / 1e9, 3),
             "effective_pair_stream_GBps": round(pairs * 2 * 3 * 4 / s / 1e9, 1),
             "note": "compute-bound (15 flop + 1 exp per pair, O(M) bytes): the HBM roofline does not "
