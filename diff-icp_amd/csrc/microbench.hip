@@ -220,6 +220,49 @@ __global__ __launch_bounds__(256) void coissue_probe(float* out, int iters, floa
   if (s == 12345.f) out[threadIdx.x] = s;
 }
 
+// Packed / scalar issue mix: per iteration NPK independent v_pk_fma_f32 chains and NSC scalar
+// FMA chains (FMAC: accumulator form a = fma(m, c, a) -> v_fmac_f32 (VOP2); else a = fma(a, m, c)
+// -> v_fma_f32 (VOP3)); DPP > 0: NSC of the scalar ops are v_add_f32 with a wave_rol:1 DPP
+// source instead.  Answers whether scalar f32 ops keep their ~2.4-cycle issue cost among packed
+// ones.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int NPK, int NSC, bool FMAC, bool DPP = false>
+__global__ __launch_bounds__(256) void pkmix_probe(float* out, int iters, float seed) {
+  f2v ap[NPK > 0 ? NPK : 1], mp[NPK > 0 ? NPK : 1];
+  float a[NSC > 0 ? NSC : 1], m[NSC > 0 ? NSC : 1];
+  const float c = seed * 0.999f;
+  const f2v cp = {c, c};
+#pragma unroll
+  for (int k = 0; k < NPK; ++k) {
+    ap[k] = f2v{seed * (threadIdx.x + k), seed * (threadIdx.x - k)} * 1e-3f;
+    mp[k] = f2v{seed * (0.5f + k * 1e-3f), seed * (0.5f - k * 1e-3f)};
+  }
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) {
+    a[k] = seed * (threadIdx.x + 3 * k) * 1e-3f;
+    m[k] = seed * (0.5f + 2e-3f * k);
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < NPK; ++k) ap[k] = __builtin_elementwise_fma(ap[k], mp[k], cp);
+#pragma unroll
+    for (int k = 0; k < NSC; ++k) {
+      if constexpr (DPP)
+        a[k] = a[k] + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m[k]), 0x134, 0xF, 0xF, false));
+      else if constexpr (FMAC)
+        a[k] = fmaf(m[k], c, a[k]);
+      else
+        a[k] = fmaf(a[k], m[k], c);
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPK; ++k) s += ap[k].x + ap[k].y;
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) s += a[k];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
 template <int CTRL>
 __global__ __launch_bounds__(64) void dpp_probe(int* out) {
   const int l = threadIdx.x;
@@ -239,6 +282,7 @@ extern "C" int dicp_mb_dpp(int which, int* out, void* stream) {
 
 // kind: 0 = exp2, 1 = fma, 2 = pk_fma, 3 = dpp(wave_rol:1)+add, 4 = dpp(row_ror:1)+add,
 // 5 = kChains fma + 1 exp2 per iteration, 10..13 = mfma_mix_probe<kind - 10>,
+// 40..47 = pkmix_probe (packed / scalar / DPP issue mixes, see there),
 // 30..33 = coissue_probe<0, 2, 4, 8> (16 fma + NE exp2 per iteration), 34 / 35 = NE 4 / 2
 // interleaved one exp per 16 / NE fma.  Returns 0 on
 // success.  ops per launch: blocks*256*iters*kChains (x2 lanes for pk_fma).
@@ -261,6 +305,14 @@ extern "C" int dicp_mb_launch(int kind, int blocks, int iters, float* out, void*
   else if (kind == 33) coissue_probe<8><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 34) coissue_probe<4, true><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 35) coissue_probe<2, true><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 40) pkmix_probe<0, 16, false><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 41) pkmix_probe<0, 16, true><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 42) pkmix_probe<8, 0, false><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 43) pkmix_probe<8, 8, false><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 44) pkmix_probe<8, 8, true><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 45) pkmix_probe<0, 16, false, true><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 46) pkmix_probe<8, 8, false, true><<<g, b, 0, st>>>(out, iters, 1.0f);
+  else if (kind == 47) pkmix_probe<12, 4, true><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 20) bf16_mix_probe<0><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 21) bf16_mix_probe<1><<<g, b, 0, st>>>(out, iters, 1.0f);
   else if (kind == 22) bf16_mix_probe<2><<<g, b, 0, st>>>(out, iters, 1.0f);

@@ -27,6 +27,13 @@ def main():
     mu2 = (q * q).sum(-1)
     w2 = torch.zeros(M, device=dev)
     zs = torch.empty_like(q)
+    if os.environ.get("PMC_OPS") == "symfwd":  # ordered vs symmetric packed forward (fwd_alg 2 / 4)
+        for alg in (2, 4, 2, 4):
+            _lib.set_option("fwd_alg", alg)
+            _lib.ode_self_fwd(q, p, 0.1, 0.0, True)
+        _lib.set_option("fwd_alg", 2)
+        torch.cuda.synchronize()
+        return
     if os.environ.get("PMC_OPS") == "kred":   # the north_star's kernel sum alone (centred path)
         for _ in range(5):
             _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)
