@@ -355,6 +355,8 @@ int dicp_supports_dim(int D);
  *   "red_alg"      KBase / KRedScal / KRed / GradKRed and the external-point forward: 0 never
  *                  the centred expansion, 1 automatic by size (default), 2 always
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
+ *   "mfma_rmax_x100"  matrix-core forward (fwd_alg 3): largest workgroup row spread (scaled
+ *                  units x 100) that takes the MFMA branch; >= 100000 always, 0 never (default 300)
  *   "ext_alg"      KRed and the external-point passes below the centred sizes: 0 generic
  *                  scalar rows, 1 packed-FP32 rows (default)
  *   "coord_raw"    PER HOST THREAD: 1 runs the default packed shooting kernels (fwd_alg 2,
