@@ -165,6 +165,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     force_splits() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "pk_rp")) {   // packed row passes: row pairs per thread, 0 = automatic
+    if (value < 0 || value > 2) return DICP_ERR_INVALID;
+    pk_rp_force() = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "fwd_alg")) {
     if (value < 0 || value > 4) return DICP_ERR_INVALID;
     g_fwd_alg = value;
@@ -220,6 +225,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "split_rounds")) { *value = split_rounds(); return DICP_OK; }
   if (!strcmp(name, "sym_L")) { *value = sym_L(); return DICP_OK; }
   if (!strcmp(name, "force_splits")) { *value = force_splits(); return DICP_OK; }
+  if (!strcmp(name, "pk_rp")) { *value = pk_rp_force(); return DICP_OK; }
   if (!strcmp(name, "fwd_alg")) { *value = g_fwd_alg; return DICP_OK; }
   if (!strcmp(name, "mfma_rmax_x100")) { *value = mfma_rmax_x100(); return DICP_OK; }
   if (!strcmp(name, "bwd_eta_alg")) { *value = g_bwd_eta_alg; return DICP_OK; }

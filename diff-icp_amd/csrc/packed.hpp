@@ -34,6 +34,7 @@ struct OpOdeSelfFwdPk {
   using Base = std::conditional_t<ZS, OpOdeSelfFwdZs<D>, OpOdeSelfFwd<D, ETA, DIV || ETA>>;
   // column splits as the full pass: the same chunk boundaries, hence bitwise the same v / g
   using SplitAs = OpOdeSelfFwdPk<D, DIV, ETA, true, false, RAW>;
+  static constexpr int kRP = ETA ? 1 : 2;   // 4 rows per thread at eta = 0 (rowred_pk_kernel)
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = Base::NACC;
   static constexpr int kNOut = Base::kNOut;
@@ -165,7 +166,31 @@ __device__ __forceinline__ void pk_load_col(const Args& a, const Scal& sc, int64
   else op_load_col<typename Op::Base>(a, sc, j, rec);
 }
 
+// Row pairs per thread RP (each pair = one f2 lane pair of rows i, i + 256): RP = 2 shares every
+// column record (LDS reads, LDS address, broadcast moves) among 4 rows.  Ops opt in with
+// kRP = 2 (the eta = 0 fused forward; tools/probes/pk_rp_sweep.py, profiles/
+// r03_ab_pk_rp_sweep.jsonl: Euler step 1.01x at 30k, 1.02-1.05x at 40k-70k, 1.045x at 100k,
+// 1.05x at 200k, 0.96x at 20k where the halved workgroup count leaves a tail); the launcher
+// uses it from DICP_PK_RP2_ROWS rows on.
+// dicp_set_option "pk_rp" (0 auto, 1, 2) forces it for every packed op (A/B).
+inline int& pk_rp_force() {
+  static int v = 0;
+  return v;
+}
+#ifndef DICP_PK_RP2_ROWS
+#define DICP_PK_RP2_ROWS 32768
+#endif
+template <class T, class = void>
+struct pk_rp_pref { static constexpr int value = 1; };
+template <class T>
+struct pk_rp_pref<T, std::void_t<decltype(T::kRP)>> { static constexpr int value = T::kRP; };
 template <class Op>
+int pk_rp(int64_t M) {
+  if (pk_rp_force() > 0) return pk_rp_force() >= 2 ? 2 : 1;
+  return (pk_rp_pref<Op>::value >= 2 && M >= DICP_PK_RP2_ROWS) ? 2 : 1;
+}
+
+template <class Op, int RP>
 __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
                                                            int64_t chunk, Outs outs) {
   using Base = typename Op::Base;
@@ -175,18 +200,23 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
 
   const int tid = threadIdx.x;
-  const int64_t ibase = (int64_t)blockIdx.x * (kBlock * 2) + tid;
-  int64_t i0 = ibase, i1 = ibase + kBlock;
-  typename Base::Row brow[2];
-  typename Op::Row2 row;
-  if constexpr (has_rows_s<Op>::value)
-    Op::load_rows_s(args, sc, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row, brow[0], brow[1]);
-  else
-    Op::load_rows(args, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row, brow[0], brow[1]);
-
-  f2 tot[NACC];
+  const int64_t ibase = (int64_t)blockIdx.x * (kBlock * 2 * RP) + tid;
+  typename Base::Row brow[RP][2];
+  typename Op::Row2 row[RP];
 #pragma unroll
-  for (int k = 0; k < NACC; ++k) tot[k] = splat(0.f);
+  for (int h = 0; h < RP; ++h) {
+    const int64_t i0 = ibase + (int64_t)(2 * h) * kBlock, i1 = i0 + kBlock;
+    if constexpr (has_rows_s<Op>::value)
+      Op::load_rows_s(args, sc, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row[h], brow[h][0], brow[h][1]);
+    else
+      Op::load_rows(args, i0 < M ? i0 : M - 1, i1 < M ? i1 : M - 1, row[h], brow[h][0], brow[h][1]);
+  }
+
+  f2 tot[RP][NACC];
+#pragma unroll
+  for (int h = 0; h < RP; ++h)
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) tot[h][k] = splat(0.f);
 
   const int64_t j0 = (int64_t)blockIdx.y * chunk;
   int64_t j1 = j0 + chunk;
@@ -212,9 +242,11 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
         lds[buf ^ 1][tid * CW4 + k] =
             make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
     }
-    f2 acc[NACC];
+    f2 acc[RP][NACC];
 #pragma unroll
-    for (int k = 0; k < NACC; ++k) acc[k] = splat(0.f);
+    for (int h = 0; h < RP; ++h)
+#pragma unroll
+      for (int k = 0; k < NACC; ++k) acc[h][k] = splat(0.f);
     const float4* tile = lds[buf];
 #pragma unroll DICP_PK_PAIR_UNROLL
     for (int t = 0; t < cnt; ++t) {
@@ -227,10 +259,13 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
         rec[4 * k + 2] = q.z;
         rec[4 * k + 3] = q.w;
       }
-      Op::pair2(row, rec, acc);
+#pragma unroll
+      for (int h = 0; h < RP; ++h) Op::pair2(row[h], rec, acc[h]);
     }
 #pragma unroll
-    for (int k = 0; k < NACC; ++k) tot[k] = tot[k] + acc[k];
+    for (int h = 0; h < RP; ++h)
+#pragma unroll
+      for (int k = 0; k < NACC; ++k) tot[h][k] = tot[h][k] + acc[h][k];
     __syncthreads();
     buf ^= 1;
     cnt = cntn;
@@ -238,38 +273,41 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
 
   const bool split = gridDim.y > 1;
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int64_t i = r == 0 ? i0 : i1;
-    if (i >= M) continue;
-    float t[NACC];
+  for (int h = 0; h < RP; ++h) {
 #pragma unroll
-    for (int k = 0; k < NACC; ++k) t[k] = r == 0 ? tot[k].x : tot[k].y;
-    float vals[Base::kOutW[0] + Base::kOutW[1] + Base::kOutW[2] + Base::kOutW[3]];
-    Base::store(sc, brow[r], t, vals);
-    int off = 0;
+    for (int r = 0; r < 2; ++r) {
+      const int64_t i = ibase + (int64_t)(2 * h + r) * kBlock;
+      if (i >= M) continue;
+      float t[NACC];
 #pragma unroll
-    for (int k = 0; k < Base::kNOut; ++k) {
-      const int w = Base::kOutW[k];
-      float* base = outs.ptr[k];
-      if (base != nullptr) {
-        if (split) {
-          float* dst = base + (int64_t)blockIdx.y * M * w + i * w;
+      for (int k = 0; k < NACC; ++k) t[k] = r == 0 ? tot[h][k].x : tot[h][k].y;
+      float vals[Base::kOutW[0] + Base::kOutW[1] + Base::kOutW[2] + Base::kOutW[3]];
+      Base::store(sc, brow[h][r], t, vals);
+      int off = 0;
 #pragma unroll
-          for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
-        } else {
+      for (int k = 0; k < Base::kNOut; ++k) {
+        const int w = Base::kOutW[k];
+        float* base = outs.ptr[k];
+        if (base != nullptr) {
+          if (split) {
+            float* dst = base + (int64_t)blockIdx.y * M * w + i * w;
 #pragma unroll
-          for (int e = 0; e < w; ++e) base[i * w + e] = epilogue(outs, k, i * w + e, vals[off + e]);
+            for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < w; ++e) base[i * w + e] = epilogue(outs, k, i * w + e, vals[off + e]);
+          }
         }
+        off += w;
       }
-      off += w;
     }
   }
 }
 
-template <class Op>
+template <class Op, int RP>
 int64_t rowred_pk_capacity() {
   static int64_t cap = -1;
-  if (cap < 0) cap = (int64_t)device_cus() * blocks_per_cu(rowred_pk_kernel<Op>);
+  if (cap < 0) cap = (int64_t)device_cus() * blocks_per_cu(rowred_pk_kernel<Op, RP>);
   return cap;
 }
 
@@ -282,8 +320,9 @@ template <class Op>
 int rowred_pk_splits(int64_t M, int64_t N) {
   using Base = typename Op::Base;
   using SOp = typename split_as<Op>::type;   // ops may borrow another variant's geometry
-  return num_splits_cap(M, N, 2, rowred_pk_capacity<SOp>(), round_rows_of<Base>::rows,
-                        round_rows_of<Base>::max);
+  const int RP = pk_rp<Op>(M);                // SplitAs variants share kRP, hence RP
+  return num_splits_cap(M, N, 2 * RP, RP == 2 ? rowred_pk_capacity<SOp, 2>() : rowred_pk_capacity<SOp, 1>(),
+                        round_rows_of<Base>::rows, round_rows_of<Base>::max);
 }
 
 template <class Op>
@@ -294,17 +333,16 @@ size_t rowred_pk_ws_bytes(int64_t M, int64_t N) {
 }
 
 // Same contract as launch_rowred<Base, 2> (launch.hpp).
-template <class Op>
-int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
-                     const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
+template <class Op, int RP>
+int launch_rowred_pk_rp(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
+                        const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
   using Base = typename Op::Base;
-  if (M <= 0) return DICP_OK;
   const int S = rowred_pk_splits<Op>(M, N);
   const int64_t chunk = N > 0 ? chunk_of(N, S) : 0;
-  const int64_t bx = (M + (int64_t)kBlock * 2 - 1) / ((int64_t)kBlock * 2);
+  const int64_t bx = (M + (int64_t)kBlock * 2 * RP - 1) / ((int64_t)kBlock * 2 * RP);
   dim3 grid((unsigned)bx, (unsigned)S, 1), block(kBlock, 1, 1);
   if (S == 1) {
-    rowred_pk_kernel<Op><<<grid, block, 0, st>>>(a, sc, M, N, chunk, fin);
+    rowred_pk_kernel<Op, RP><<<grid, block, 0, st>>>(a, sc, M, N, chunk, fin);
     return check_launch(name);
   }
   const size_t need = rowred_pk_ws_bytes<Op>(M, N);
@@ -318,7 +356,7 @@ int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M,
     part.ptr[k] = fin.ptr[k] ? cur : nullptr;
     cur += (int64_t)S * M * Base::kOutW[k];
   }
-  rowred_pk_kernel<Op><<<grid, block, 0, st>>>(a, sc, M, N, chunk, part);
+  rowred_pk_kernel<Op, RP><<<grid, block, 0, st>>>(a, sc, M, N, chunk, part);
   int rc = check_launch(name);
   if (rc) return rc;
   MergeSet ms;
@@ -339,6 +377,14 @@ int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M,
     if (rc) return rc;
   }
   return DICP_OK;
+}
+
+template <class Op>
+int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
+                     const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (M <= 0) return DICP_OK;
+  return pk_rp<Op>(M) == 2 ? launch_rowred_pk_rp<Op, 2>(name, a, sc, M, N, fin, ws, ws_bytes, st)
+                           : launch_rowred_pk_rp<Op, 1>(name, a, sc, M, N, fin, ws, ws_bytes, st);
 }
 
 }  // namespace dicp
