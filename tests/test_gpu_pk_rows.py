@@ -1,0 +1,99 @@
+"""Row pairs per thread of the packed fused forward (packed.hpp rowred_pk_kernel<Op, RP>,
+dicp_set_option "pk_rp"): the 4-row form (RP = 2, automatic for the eta = 0 forward from 32k
+rows) forced at ragged sizes, row slices (the row split) and every output variant (v / mG / g,
+the divergence rows zs, the mG-less last step, the Hamiltonian rows), against the 2-row form
+(1e-6: fp32 summation order of the column splits only, bitwise when both pick the same splits)
+and against the fp64 oracle's ODE (2e-5, the tolerance of tests/test_gpu_kernels.py)."""
+import pytest
+import torch
+
+from conftest import rel_err
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+
+SIG = 0.15
+
+
+def _lib():
+    from difficp_amd import _lib
+    return _lib
+
+
+class _rp:
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        L = _lib()
+        self.old = L.get_option("pk_rp")
+        L.set_option("pk_rp", self.v)
+
+    def __exit__(self, *a):
+        _lib().set_option("pk_rp", self.old)
+
+
+def _case(M, D, seed):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.rand(M, D, generator=g, dtype=torch.float64)
+    p = 0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)
+    return q, p
+
+
+@pytest.mark.parametrize("M,D", [(1, 3), (257, 3), (1023, 2), (1025, 3), (5000, 3), (33001, 3)])
+def test_forward_four_rows_vs_two_rows(dev, M, D):
+    L = _lib()
+    q, p = _case(M, D, 7 * M + D)
+    qf, pf = q.float().to(dev), p.float().to(dev)
+    outs = {}
+    for rp in (1, 2):
+        with _rp(rp):
+            zs = torch.empty(M, D, device=dev)
+            o = {"fwd": L.ode_self_fwd(qf, pf, SIG, 0.0, True),
+                 "fwd_h": L.ode_self_fwd(qf, pf, SIG, 0.0, True, want_h=True),
+                 "step_zs": L.euler_step(qf, pf, SIG, 0.0, 0.1, True, zs_out=zs) + (zs,),
+                 "step_nog": L.euler_step(qf, pf, SIG, 0.0, 0.1, True, want_p=False)}
+            torch.cuda.synchronize()
+            outs[rp] = o
+    for k in outs[1]:
+        for a, b in zip(outs[2][k], outs[1][k]):
+            if a is None or b is None:
+                assert a is None and b is None, k
+                continue
+            assert rel_err(a.cpu(), b.cpu()) < 1e-6, (k, rel_err(a.cpu(), b.cpu()))
+    if M > 5000:   # the dense oracle holds M x M x D float64 pairs
+        return
+    # the 4-row form against the fp64 oracle's ODE (v, -G, divergence), tolerance as
+    # tests/test_gpu_kernels.py: max(2e-5, 2 x the float32 oracle's own deviation)
+    m = R.LDDMM(SIG, D, 50.0, False, True)
+    v64, mG64, c64 = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
+    m32 = R.LDDMM(SIG, D, 50.0, False, True)
+    v32, mG32, c32 = m32.ODE(q.float(), p.float(), torch.zeros(1))
+    tol = lambda r64, r32: max(2e-5, 2 * rel_err(r32, r64))
+    v, mG, g, _ = outs[2]["fwd"]
+    assert rel_err(v.cpu(), v64) <= tol(v64, v32)
+    assert rel_err(mG.cpu(), mG64) <= tol(mG64, mG32)
+    assert rel_err(g.sum().cpu(), c64) <= tol(c64, c32)
+
+
+@pytest.mark.parametrize("M,W", [(33001, 2), (40000, 3), (70001, 2)])
+def test_forward_four_rows_row_slices(dev, M, W):
+    """Row slices of the forward under the automatic choice (the full pass >= 32k rows runs 4
+    rows per thread; slices below 32k rows 2, the 35k-row slices of 70001 / 2 also 4)
+    concatenate to the full pass within fp32 summation order."""
+    L = _lib()
+    q, p = _case(M, 3, M + W)
+    qf, pf = q.float().to(dev), p.float().to(dev)
+    qn, pn, g = L.euler_step(qf, pf, SIG, 0.0, 0.1, True)
+    per = -(-M // W)
+    parts = []
+    for r in range(W):
+        r0 = min(per * r, M)
+        n = min(per, M - r0)
+        parts.append(L.euler_step_rows(qf, pf, r0, n, SIG, 0.0, 0.1, True))
+    qs = torch.cat([t[0] for t in parts])
+    ps = torch.cat([t[1] for t in parts])
+    gs = torch.cat([t[2] for t in parts])
+    assert rel_err(qs.cpu(), qn.cpu()) < 1e-6
+    assert rel_err(ps.cpu(), pn.cpu()) < 1e-6
+    assert rel_err(gs.cpu(), g.cpu()) < 1e-5
