@@ -166,7 +166,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "pk_rp")) {   // packed row passes: row pairs per thread, 0 = automatic
-    if (value < 0 || value > 2) return DICP_ERR_INVALID;
+    if (value < 0 || value > kPkRPMax) return DICP_ERR_INVALID;
     pk_rp_force() = value;
     return DICP_OK;
   }

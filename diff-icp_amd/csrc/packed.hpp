@@ -184,9 +184,14 @@ template <class T, class = void>
 struct pk_rp_pref { static constexpr int value = 1; };
 template <class T>
 struct pk_rp_pref<T, std::void_t<decltype(T::kRP)>> { static constexpr int value = T::kRP; };
+// experiment builds (-DDICP_PK_RP_EXTRA=1) also instantiate 3 and 4 row pairs per thread
+#ifndef DICP_PK_RP_EXTRA
+#define DICP_PK_RP_EXTRA 0
+#endif
+constexpr int kPkRPMax = DICP_PK_RP_EXTRA ? 4 : 2;
 template <class Op>
 int pk_rp(int64_t M) {
-  if (pk_rp_force() > 0) return pk_rp_force() >= 2 ? 2 : 1;
+  if (pk_rp_force() > 0) return pk_rp_force() > kPkRPMax ? kPkRPMax : pk_rp_force();
   return (pk_rp_pref<Op>::value >= 2 && M >= DICP_PK_RP2_ROWS) ? 2 : 1;
 }
 
@@ -321,8 +326,16 @@ int rowred_pk_splits(int64_t M, int64_t N) {
   using Base = typename Op::Base;
   using SOp = typename split_as<Op>::type;   // ops may borrow another variant's geometry
   const int RP = pk_rp<Op>(M);                // SplitAs variants share kRP, hence RP
-  return num_splits_cap(M, N, 2 * RP, RP == 2 ? rowred_pk_capacity<SOp, 2>() : rowred_pk_capacity<SOp, 1>(),
-                        round_rows_of<Base>::rows, round_rows_of<Base>::max);
+  int64_t cap;
+  switch (RP) {
+#if DICP_PK_RP_EXTRA
+    case 4: cap = rowred_pk_capacity<SOp, 4>(); break;
+    case 3: cap = rowred_pk_capacity<SOp, 3>(); break;
+#endif
+    case 2: cap = rowred_pk_capacity<SOp, 2>(); break;
+    default: cap = rowred_pk_capacity<SOp, 1>(); break;
+  }
+  return num_splits_cap(M, N, 2 * RP, cap, round_rows_of<Base>::rows, round_rows_of<Base>::max);
 }
 
 template <class Op>
@@ -383,8 +396,14 @@ template <class Op>
 int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                      const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
   if (M <= 0) return DICP_OK;
-  return pk_rp<Op>(M) == 2 ? launch_rowred_pk_rp<Op, 2>(name, a, sc, M, N, fin, ws, ws_bytes, st)
-                           : launch_rowred_pk_rp<Op, 1>(name, a, sc, M, N, fin, ws, ws_bytes, st);
+  switch (pk_rp<Op>(M)) {
+#if DICP_PK_RP_EXTRA
+    case 4: return launch_rowred_pk_rp<Op, 4>(name, a, sc, M, N, fin, ws, ws_bytes, st);
+    case 3: return launch_rowred_pk_rp<Op, 3>(name, a, sc, M, N, fin, ws, ws_bytes, st);
+#endif
+    case 2: return launch_rowred_pk_rp<Op, 2>(name, a, sc, M, N, fin, ws, ws_bytes, st);
+    default: return launch_rowred_pk_rp<Op, 1>(name, a, sc, M, N, fin, ws, ws_bytes, st);
+  }
 }
 
 }  // namespace dicp

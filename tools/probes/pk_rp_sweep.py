@@ -14,6 +14,7 @@ from difficp_amd import _lib  # noqa: E402
 dev = torch.device("cuda:0")
 st = torch.cuda.current_stream()
 out = []
+RPS = tuple(int(v) for v in os.environ.get("RPS", "1,2").split(","))
 for M in [int(v) for v in os.environ.get("SIZES", "20000,30000,40000,50000,70000,100000,200000").split(",")]:
     g = torch.Generator().manual_seed(M)
     q = torch.rand(M, 3, generator=g).to(dev)
@@ -26,7 +27,7 @@ for M in [int(v) for v in os.environ.get("SIZES", "20000,30000,40000,50000,70000
     for name, fn in fns.items():
         best = {}
         for _ in range(3):
-            for rp in (1, 2):
+            for rp in RPS:
                 _lib.set_option("pk_rp", rp)
                 fn()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -36,8 +37,8 @@ for M in [int(v) for v in os.environ.get("SIZES", "20000,30000,40000,50000,70000
                 e1.record(st)
                 e1.synchronize()
                 best[rp] = min(best.get(rp, 1e9), e0.elapsed_time(e1) / reps)
-        row[name] = {"rp1_ms": round(best[1], 4), "rp2_ms": round(best[2], 4),
-                     "rp2_speedup": round(best[1] / best[2], 4)}
+        row[name] = {f"rp{rp}_ms": round(best[rp], 4) for rp in RPS}
+        row[name].update({f"rp{rp}_speedup": round(best[1] / best[rp], 4) for rp in RPS if rp > 1})
     _lib.set_option("pk_rp", 0)
     print(json.dumps(row), flush=True)
     out.append(row)
