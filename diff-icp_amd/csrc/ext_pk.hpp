@@ -52,6 +52,7 @@ struct OpExtFwdS {
 template <int D, bool ETA, bool DIV>
 struct OpExtFwdPk {
   using Base = OpExtFwdS<D, ETA, DIV>;
+  static constexpr int kRP = 2;            // 4 rows per thread on large passes (packed.hpp pk_rp)
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = Base::NACC;
   static constexpr int kNOut = Base::kNOut;
@@ -124,6 +125,7 @@ struct OpExtBwdXS {
 template <int D>
 struct OpExtBwdXPk {
   using Base = OpExtBwdXS<D>;
+  static constexpr int kRP = 2;            // 4 rows per thread on large passes (packed.hpp pk_rp)
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = D;
   static constexpr int kNOut = 1;
@@ -198,6 +200,7 @@ struct OpExtBwdQS {
 template <int D>
 struct OpExtBwdQPk {
   using Base = OpExtBwdQS<D>;
+  static constexpr int kRP = 2;            // 4 rows per thread on large passes (packed.hpp pk_rp)
   static constexpr int CW4 = Base::CW4;
   static constexpr int NACC = Base::NACC;
   static constexpr int kNOut = 2;

@@ -170,8 +170,10 @@ __device__ __forceinline__ void pk_load_col(const Args& a, const Scal& sc, int64
 // column record (LDS reads, LDS address, broadcast moves) among 4 rows.  Ops opt in with
 // kRP = 2 (the eta = 0 fused forward; tools/probes/pk_rp_sweep.py, profiles/
 // r03_ab_pk_rp_sweep.jsonl: Euler step 1.01x at 30k, 1.02-1.05x at 40k-70k, 1.045x at 100k,
-// 1.05x at 200k, 0.96x at 20k where the halved workgroup count leaves a tail); the launcher
-// uses it from DICP_PK_RP2_ROWS rows on.
+// 1.05x at 200k, 0.96x at 20k where the halved workgroup count leaves a tail; the external-
+// point passes, tools/probes/pk_rp_ext.py, profiles/r03_ab_pk_rp_ext.jsonl: 1.02-1.05x from 10k
+// columns on, 0.93-0.94x at 2k columns); the launcher uses it from DICP_PK_RP2_ROWS rows and
+// DICP_PK_RP2_COLS columns on.
 // dicp_set_option "pk_rp" (0 auto, 1, 2) forces it for every packed op (A/B).
 inline int& pk_rp_force() {
   static int v = 0;
@@ -189,10 +191,13 @@ struct pk_rp_pref<T, std::void_t<decltype(T::kRP)>> { static constexpr int value
 #define DICP_PK_RP_EXTRA 0
 #endif
 constexpr int kPkRPMax = DICP_PK_RP_EXTRA ? 4 : 2;
+#ifndef DICP_PK_RP2_COLS
+#define DICP_PK_RP2_COLS 8192
+#endif
 template <class Op>
-int pk_rp(int64_t M) {
+int pk_rp(int64_t M, int64_t N) {
   if (pk_rp_force() > 0) return pk_rp_force() > kPkRPMax ? kPkRPMax : pk_rp_force();
-  return (pk_rp_pref<Op>::value >= 2 && M >= DICP_PK_RP2_ROWS) ? 2 : 1;
+  return (pk_rp_pref<Op>::value >= 2 && M >= DICP_PK_RP2_ROWS && N >= DICP_PK_RP2_COLS) ? 2 : 1;
 }
 
 template <class Op, int RP>
@@ -325,7 +330,7 @@ template <class Op>
 int rowred_pk_splits(int64_t M, int64_t N) {
   using Base = typename Op::Base;
   using SOp = typename split_as<Op>::type;   // ops may borrow another variant's geometry
-  const int RP = pk_rp<Op>(M);                // SplitAs variants share kRP, hence RP
+  const int RP = pk_rp<Op>(M, N);             // SplitAs variants share kRP, hence RP
   int64_t cap;
   switch (RP) {
 #if DICP_PK_RP_EXTRA
@@ -396,7 +401,7 @@ template <class Op>
 int launch_rowred_pk(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                      const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
   if (M <= 0) return DICP_OK;
-  switch (pk_rp<Op>(M)) {
+  switch (pk_rp<Op>(M, N)) {
 #if DICP_PK_RP_EXTRA
     case 4: return launch_rowred_pk_rp<Op, 4>(name, a, sc, M, N, fin, ws, ws_bytes, st);
     case 3: return launch_rowred_pk_rp<Op, 3>(name, a, sc, M, N, fin, ws, ws_bytes, st);

@@ -353,7 +353,8 @@ int dicp_supports_dim(int D);
  *   "r_fwd" / "r_bwd"  rows per thread {1,2,4} of the ordered passes (env DICP_R_FWD / DICP_R_BWD)
  *   "split_rounds", "force_splits", "sym_L"  column-split / symmetric-chunk geometry (0 = auto)
  *   "pk_rp"        packed row passes: row pairs per thread, 0 automatic (2 for the eta = 0 fused
- *                  forward from 32k rows, else 1), 1 or 2 forced
+ *                  forward and the packed external-point / KRed passes from 32k rows and 8k
+ *                  columns, else 1), 1 or 2 forced
  *   "red_alg"      KBase / KRedScal / KRed / GradKRed and the external-point forward: 0 never
  *                  the centred expansion, 1 automatic by size (default), 2 always
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)

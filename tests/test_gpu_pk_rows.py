@@ -97,3 +97,34 @@ def test_forward_four_rows_row_slices(dev, M, W):
     assert rel_err(qs.cpu(), qn.cpu()) < 1e-6
     assert rel_err(ps.cpu(), pn.cpu()) < 1e-6
     assert rel_err(gs.cpu(), g.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("N,M,D", [(1, 5, 3), (1025, 700, 3), (3001, 2049, 2), (20000, 9000, 3)])
+@pytest.mark.parametrize("eta", [0.0, 0.02])
+def test_external_point_passes_four_rows_vs_two_rows(dev, N, M, D, eta):
+    """The packed external-point forward / VJP and the packed KRed (ext_pk.hpp) with 4 rows per
+    thread forced, against 2 rows: fp32 summation order of the column splits only."""
+    L = _lib()
+    g = torch.Generator().manual_seed(N + M + D)
+    x = torch.rand(N, D, generator=g).to(dev)
+    q = torch.rand(M, D, generator=g).to(dev)
+    p = (0.1 * torch.randn(M, D, generator=g)).to(dev)
+    gvx = torch.randn(N, D, generator=g).to(dev)
+    gdiv = torch.ones(1, device=dev)
+    old = L.get_option("red_alg")
+    L.set_option("red_alg", 0)   # the packed kernels at every size
+    try:
+        res = {}
+        for rp in (1, 2):
+            with _rp(rp):
+                gq = torch.zeros(M, D, device=dev)
+                gp = torch.zeros(M, D, device=dev)
+                vx, gx = L.ode_ext_fwd(x, q, p, SIG, eta, True)
+                gxb = L.ode_ext_bwd(x, q, p, gvx, gdiv, SIG, eta, gq, gp)
+                kr = L.gauss_red(L.KRED, x, q, SIG, b=p)
+                torch.cuda.synchronize()
+                res[rp] = (vx, gx, gxb, gq, gp, kr)
+    finally:
+        L.set_option("red_alg", old)
+    for a, b in zip(res[2], res[1]):
+        assert rel_err(a.cpu(), b.cpu()) < 1e-6, rel_err(a.cpu(), b.cpu())
