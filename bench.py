@@ -2,7 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
                     [--workload two_set_100k|two_set_50k|two_set_200k|two_set_50k_exact|atlas_c4|atlas_c4_fixed|c5|c5_alt]
-    (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+    (N > 1: one rank per GPU over RCCL.  Under torch.distributed.run WORLD_SIZE must equal N;
+     started without it, bench.py starts `python -m torch.distributed.run --nproc-per-node N`
+     on itself as a child process -- before anything touches the GPU -- and exits with the
+     child's status; rank 0's JSON line reaches stdout through the child.)
 
 A "step" is one diff-ICP iteration on the workload -- GMM_opt(max_repeat_GMM=10, tol=1e-3)
 + Reg_opt(nmax=1, tol=1e-3), the loop body of ICP_two_set.py:254-282 / ICP_atlas.py:269-298 --
@@ -53,6 +56,9 @@ WORKLOADS = {
     "two_set_200k": dict(kind="two_set", N=200000),
     # the point count BASELINE.json's metric string names ("100k-pt 3D")
     "two_set_100k": dict(kind="two_set", N=100000),
+    # the north_star's "synthetic 2D/3D point sets": the same match in the plane (the
+    # reference's own examples are 2D: diffICP_basic.py, the Chui sets)
+    "two_set_100k_2d": dict(kind="two_set", N=100000, D=2),
     # SURVEY C2': the exact ICP_two_set model (gradcomponent=True, eta = 1/lambda), a0 from
     # the device ridge CG (v2p version "ridge_keops", alpha 1e-3, PSR.py:402)
     "two_set_50k_exact": dict(kind="two_set", N=50000, version="logdet",
@@ -100,7 +106,7 @@ def _round_robin(calls, budget_s):
     return times, time.perf_counter() - t_start
 
 
-def cpu_baseline_c(pair_counts, M_work, budget_s=15.0):
+def cpu_baseline_c(pair_counts, M_work, budget_s=15.0, D=3):
     """The oracle's C restatement (OpenMP) of the dominant pair kernels, timed on this host on
     a bounded sample -- repeated ODE-forward / VJP / E-step evaluations at M x M pairs (the
     workload's size, capped at 50k so one evaluation stays ~1 s) -- then extrapolated to one
@@ -109,10 +115,10 @@ def cpu_baseline_c(pair_counts, M_work, budget_s=15.0):
     threads = _cpu_threads()
     torch.manual_seed(0)
     M = int(M_work)
-    q = torch.rand(M, 3)
-    p = 0.01 * torch.randn(M, 3)
-    a = torch.randn(M, 3)
-    X = torch.rand(M, 3)
+    q = torch.rand(M, D)
+    p = 0.01 * torch.randn(M, D)
+    a = torch.randn(M, D)
+    X = torch.rand(M, D)
     w0 = torch.zeros(M)
     calls = {"fwd": lambda: c_ref.ode_self_fwd(q, p, 0.1),
              "bwd": lambda: c_ref.ode_self_bwd(q, p, a, a, 1.0, 0.1),
@@ -122,12 +128,12 @@ def cpu_baseline_c(pair_counts, M_work, budget_s=15.0):
     secs = sum(v / rates[_pair_kind(k)] for k, v in pair_counts.items())
     return {"value": 1.0 / secs, "unit": "PSR iterations/sec", "cores": threads, "kind": "port",
             "sample": (f"oracle/difficp_ref.c (OpenMP C, {threads} threads): {len(times['fwd'])} x (ODE fwd + VJP + "
-                       f"E-step) at {M}x{M} pairs ({took:.1f} s), rates fwd {rates['fwd'] / 1e9:.3f} / bwd "
+                       f"E-step) at {M}x{M} pairs, D = {D} ({took:.1f} s), rates fwd {rates['fwd'] / 1e9:.3f} / bwd "
                        f"{rates['bwd'] / 1e9:.3f} / EM {rates['em'] / 1e9:.3f} Gpair/s, extrapolated to the live "
                        "pair counts of one iteration")}
 
 
-def cpu_baseline_torch(pair_counts, budget_s=15.0, M=4000):
+def cpu_baseline_torch(pair_counts, budget_s=15.0, M=4000, D=3):
     """The reference's CPU path as SURVEY 8(d) defines the baseline: the chunked torch
     restatement of the reference's operators (oracle/torch_ref.py: the torch arithmetic of
     kernel.py / LDDMM.py / GMM.py, float32, torch.set_num_threads = the host threads), timed on
@@ -142,15 +148,15 @@ def cpu_baseline_torch(pair_counts, budget_s=15.0, M=4000):
     torch.set_num_threads(threads)
     try:
         g = torch.Generator().manual_seed(0)
-        q = torch.rand(M, 3, generator=g)
-        p = 0.01 * torch.randn(M, 3, generator=g)
-        a = torch.randn(M, 3, generator=g)
-        b = torch.randn(M, 3, generator=g)
+        q = torch.rand(M, D, generator=g)
+        p = 0.01 * torch.randn(M, D, generator=g)
+        a = torch.randn(M, D, generator=g)
+        b = torch.randn(M, D, generator=g)
         C = M // 4
-        X = torch.rand(M, 3, generator=g)
-        mu = torch.rand(C, 3, generator=g)
+        X = torch.rand(M, D, generator=g)
+        mu = torch.rand(C, D, generator=g)
         w0 = torch.zeros(C)
-        m = R.LDDMM(0.1, 3, 1e3, False, True)
+        m = R.LDDMM(0.1, D, 1e3, False, True)
         c0 = torch.zeros(1)
         opt = {"mu": True, "w": True, "sigma": True, "eta0": False}
 
@@ -172,18 +178,18 @@ def cpu_baseline_torch(pair_counts, budget_s=15.0, M=4000):
     return {"value": 1.0 / secs, "unit": "PSR iterations/sec", "cores": threads, "kind": "port",
             "sample": (f"oracle/torch_ref.py (the reference's torch arithmetic, float32, {threads} threads): "
                        f"{len(times['fwd'])} x (hybrid ODE eval, ODE eval + autograd backward, EM step) at "
-                       f"{M} points ({took:.1f} s); rates fwd {rates['fwd'] / 1e9:.4f} / bwd {rates['bwd'] / 1e9:.4f} / "
+                       f"{M} points, D = {D} ({took:.1f} s); rates fwd {rates['fwd'] / 1e9:.4f} / bwd {rates['bwd'] / 1e9:.4f} / "
                        f"EM {rates['em'] / 1e9:.4f} Gpair/s, extrapolated to the live pair counts of one "
                        "iteration; cross-timed vs the imported reference within 1.2x at N <= 4000 "
                        "(profiles/r03_cpu_crosstime.json)")}
 
 
-def cpu_baseline(pair_counts, M_work):
+def cpu_baseline(pair_counts, M_work, D=3):
     """cpu_baseline object of the bench line: the reference-path torch restatement (SURVEY
     8(d)) as the value, the faster OpenMP C restatement beside it."""
-    base = cpu_baseline_torch(pair_counts)
+    base = cpu_baseline_torch(pair_counts, D=D)
     try:
-        base["c_openmp"] = cpu_baseline_c(pair_counts, M_work, budget_s=10.0)
+        base["c_openmp"] = cpu_baseline_c(pair_counts, M_work, budget_s=10.0, D=D)
     except Exception as e:  # informative only
         base["c_openmp"] = {"error": repr(e)}
     return base
@@ -262,7 +268,49 @@ def load_issue(kernel_name):
         return None, None
 
 
+def launch_plan(argv, env):
+    """How `bench.py argv` runs, decided before any GPU call: ("run", world) in this process
+    (world 1, or a rank started by torch.distributed.run with WORLD_SIZE = --gpus), or
+    ("spawn", cmd) -- the torch.distributed.run command a plain `bench.py --gpus N` (N > 1)
+    starts as its child, one rank per GPU, with every argument passed through.  A WORLD_SIZE
+    that disagrees with --gpus raises SystemExit (the line would claim the wrong GPU count)."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args(argv)
+    if a.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} must be >= 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}: launch {a.gpus} ranks "
+                             "or pass --gpus WORLD_SIZE")
+        return ("run", int(ws))
+    if a.gpus == 1:
+        return ("run", 1)
+    port = env.get("MASTER_PORT") or str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return ("spawn", cmd)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def main():
+    plan = launch_plan(sys.argv[1:], os.environ)
+    if plan[0] == "spawn":
+        # a child process, never an exec: nothing here has touched the GPU, and the ranks'
+        # stdout (rank 0's JSON line) is this process's stdout
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        log(f"bench: --gpus > 1 without WORLD_SIZE, starting the ranks: {' '.join(plan[1])}")
+        rc = subprocess.run(plan[1], env=env).returncode
+        sys.exit(rc)
     # the driver parses ONE JSON line from stdout: everything else (e.g. the reference's
     # "GMM optimization - reached maximum number of iterations" message) goes to stderr
     real_stdout = sys.stdout
@@ -284,12 +332,14 @@ def _main(out):
     ap.add_argument("--concurrent-frames", type=int, default=None,
                     help="atlas workloads: frames optimised concurrently (host threads / HIP "
                          "streams); default automatic (4), 1 = the reference's sequential loop")
+    ap.add_argument("--lib-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="dicp_set_option before the run (A/B experiments; repeatable)")
     ap.add_argument("--replicas", action="store_true",
                     help="two-set workloads at N > 1: N independent replicas (weak scaling) "
                          "instead of row-splitting the one match over the N GPUs")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = launch_plan(sys.argv[1:], os.environ)[1]
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal on a 1-GPU box (never the driver's runs): DICP_BENCH_REHEARSE=1 puts every rank
@@ -309,6 +359,9 @@ def _main(out):
     torch.cuda.set_device(dev)
 
     from difficp_amd import _lib, workloads
+    for kv in args.lib_opt:
+        k, v = kv.split("=")
+        _lib.set_option(k, int(v))
 
     wl = WORKLOADS[args.workload]
     t_setup = time.perf_counter()
@@ -317,14 +370,17 @@ def _main(out):
         # RCCL all-gather of the new row slices, per adjoint step an all-reduce of the VJP
         # parts) -- strong scaling; --replicas: N independent copies (weak scaling)
         version = wl.get("version", "hybrid")
+        D = wl.get("D", 3)
         psr = workloads.build_two_set(wl["N"], dev, seed=0, version=version,
-                                      v2p_args=wl.get("v2p_args"))
+                                      v2p_args=wl.get("v2p_args"), D=D)
         split = world > 1 and not args.replicas
         if split:
             psr.LMi.set_row_split()
         src = {50000: "BASELINE configs[1]", 200000: "BASELINE configs[2]",
                100000: "BASELINE metric's 100k-pt 3D"}.get(wl["N"], "two-set")
-        cfg = {"workload": f"two-set 3D {wl['N']} vs {wl['N']} ({src})" +
+        if D != 3:
+            src = f"the north_star's 2D/3D point sets, {D}D"
+        cfg = {"workload": f"two-set {D}D {wl['N']} vs {wl['N']} ({src})" +
                (" exact ICP_two_set model" if version == "logdet" else ""),
                "points_per_set": wl["N"], "lddmm": f"{version} sigma=0.1 lambda=1e3 Euler nt=10 dense",
                "gmm": "mu=xB fixed, sigma optimised", "max_repeat_GMM": 10, "tol": 1e-3,
@@ -420,11 +476,13 @@ def _main(out):
             achieved = flops_per_launch / avg_s / 1e12
             # committed PMC summary: whole-size single-device launches of the default workload
             # (tools/pmc_probe.py); not the pair-subset launches of a row split
-            traffic = load_traffic(dom) if world == 1 and wl.get("N") == 100000 else None
-            # compute-bound: priced against the dense FP32 peak, 157.3 TF/s on MI355X, which is
-            # both the f32 MFMA rate and the packed-VALU rate (MI355X_MICROARCH.md); the pair
-            # kernels run on the VALU (3-wide dot products + exp: no contraction for MFMA)
-            roof = {"bound": "mfma", "compute_unit": "VALU (fp32; dense fp32 peak = f32 MFMA peak)",
+            traffic = (load_traffic(dom) if world == 1 and wl.get("N") == 100000 and wl.get("D", 3) == 3
+                       else None)
+            # compute-bound on the VALU (the north_star: "MFMA not used"): priced against the
+            # dense FP32 peak, 157.3 TF/s on MI355X, which is the packed-VALU rate (and also the
+            # f32 MFMA rate, MI355X_MICROARCH.md); 3-wide dot products + exp, no contraction
+            roof = {"bound": "valu", "compute_unit": "VALU (fp32 packed v_pk_* + v_exp_f32; dense fp32 "
+                                                     "peak = packed-VALU peak = f32 MFMA peak)",
                     "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                     "traffic": traffic, "kernel": dom, "launches": d["launches"],
@@ -458,11 +516,11 @@ def _main(out):
         base = None
         if not args.no_cpu_baseline and world == 1 and pair_counts:
             try:
-                base = cpu_baseline(pair_counts, min(wl["N"], 50000))
+                base = cpu_baseline(pair_counts, min(wl["N"], 50000), D=wl.get("D", 3))
             except Exception as e:  # baseline is informative; never fail the bench on it
                 base = {"error": repr(e)}
         ksum = None
-        if world == 1 and wl.get("N") == 100000:
+        if world == 1 and wl.get("N") == 100000 and wl.get("D", 3) == 3:
             try:
                 ksum = kernel_sum_probe(dev, wl["N"])
             except Exception as e:  # informative; never fail the bench on it

@@ -166,11 +166,22 @@ class coord_mode:
             set_option("coord_raw", self.old)
 
 
+# bumped by every set_option of a process-wide knob: a kernel-variant change (fwd_alg,
+# bwd_alg, pk_rp, split rounds, ...) makes results computed before it not bitwise what a
+# recomputation gives, so caches of results (shooting.ShootCache) key on it
+_OPTION_EPOCH = [0]
+
+
+def option_epoch() -> int:
+    return _OPTION_EPOCH[0]
+
+
 def set_option(name: str, value: int):
     """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
     _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")
     if name != "coord_raw":     # every other knob may change a workspace size
         _WS_BYTES.clear()
+        _OPTION_EPOCH[0] += 1
 
 
 def _zero_b_ok(eta) -> bool:

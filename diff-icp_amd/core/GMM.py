@@ -71,6 +71,32 @@ def _sum_ranks(x, comm):
     return _gather_rows(t, comm).sum(0)[0]
 
 
+def _sum_ranks_many(xs, comm):
+    """Deterministic cross-rank sums of several scalars in ONE collective: each is taken to
+    float64 (as _sum_ranks does), gathered, and summed in rank order."""
+    dev = next((x.device for x in xs if isinstance(x, torch.Tensor)), None) or _comm_device()
+    t = torch.stack([torch.as_tensor(x, dtype=torch.float64, device=dev).reshape(())
+                     for x in xs]).reshape(-1, 1)
+    g = _gather_rows(t, comm)                       # (W, n, 1)
+    return [g[:, i].sum(0)[0] for i in range(len(xs))]
+
+
+def _exchange(parts, comm):
+    """ONE all_gather of several tensors: each is taken to float64 and flattened into one
+    buffer (exact for the float32 statistics), gathered, and handed back per name as a
+    (W, *shape) tensor of its own dtype, in rank order."""
+    names = list(parts)
+    dev = parts[names[0]].device
+    flat = [parts[k].detach().to(device=dev, dtype=torch.float64).reshape(-1) for k in names]
+    g = _gather_rows(torch.cat(flat), comm)         # (W, L)
+    out, off = {}, 0
+    for k, f in zip(names, flat):
+        n = f.numel()
+        out[k] = g[:, off:off + n].reshape((g.shape[0],) + tuple(parts[k].shape)).to(parts[k].dtype)
+        off += n
+    return out
+
+
 class GaussianMixtureUnif(torch.nn.Module):
 
     def __init__(self, mu, sigma=None, use_outliers=False, spec=defspec, computversion="hip"):
@@ -198,27 +224,50 @@ class GaussianMixtureUnif(torch.nn.Module):
 
         # ---- M step ----
         need_col = (not skip_M) and (self.to_optimize["mu"] or self.to_optimize["w"])
+        need_eta0 = not skip_M and self.outliers is not None and self.to_optimize["eta0"]
+        need_sigma = not skip_M and self.to_optimize["sigma"]
         if need_col:
             colstats = _lib.gmm_mstep(X, T2, mu_old, w2_old, sigma_old)   # (C, D+1)
-            if dist_on:
-                g = _gather_rows(colstats, comm)                          # (W, C, D+1)
+        if need_eta0:
+            a = lgamma0_n.logsumexp(dim=0)
+            b = lgammaT_n.logsumexp(dim=0)
+        if need_sigma and not keops_sem:
+            nds = stats[:, D + 3].sum()
+        if dist_on and (need_col or need_eta0 or need_sigma):
+            # ONE collective for everything the M step needs from the other ranks (SURVEY
+            # 8(e)): the column statistics, the outlier LSE terms, the sigma numerator (torch
+            # semantics: from the E-step rows) and the point count, packed into one buffer
+            parts = {}
+            if need_col:
+                parts["col"] = colstats
+            if need_eta0:
+                parts["a"], parts["b"] = a, b
+            if need_sigma:
+                if not keops_sem:
+                    parts["nds"] = nds.double()       # summed over ranks in float64
+                parts["N"] = torch.tensor(float(N), dtype=torch.float64, device=X.device)
+            ex = _exchange(parts, comm)
+            if need_col:
+                g = ex["col"]                                             # (W, C, D+1)
                 lw = g[:, :, 0]
                 Wg = lw.logsumexp(0)
                 wt = torch.exp(lw - Wg[None, :])
                 wt = torch.where(torch.isfinite(wt), wt, torch.zeros_like(wt))
                 mu_new = (wt[:, :, None] * g[:, :, 1:]).sum(0) / wt.sum(0)[:, None]
                 w_new = Wg
-            else:
-                w_new = colstats[:, 0].contiguous()
-                mu_new = colstats[:, 1:].contiguous()
-            if self.to_optimize["mu"]:
-                self.mu = mu_new.contiguous()
-        if not skip_M and self.outliers is not None and self.to_optimize["eta0"]:
-            a = lgamma0_n.logsumexp(dim=0)
-            b = lgammaT_n.logsumexp(dim=0)
-            if dist_on:
-                a = _gather_rows(a.reshape(1), comm).logsumexp(0)[0]
-                b = _gather_rows(b.reshape(1), comm).logsumexp(0)[0]
+            if need_eta0:
+                a = ex["a"].reshape(-1, 1).logsumexp(0)[0]
+                b = ex["b"].reshape(-1, 1).logsumexp(0)[0]
+            if need_sigma:
+                if not keops_sem:
+                    nds = ex["nds"].reshape(-1, 1).sum(0)[0]
+                Ntot = int(ex["N"].reshape(-1, 1).sum(0)[0].item())
+        elif need_col:
+            w_new = colstats[:, 0].contiguous()
+            mu_new = colstats[:, 1:].contiguous()
+        if need_col and self.to_optimize["mu"]:
+            self.mu = mu_new.contiguous()
+        if need_eta0:
             self.outliers["eta0"] = (a - b).item()
         if need_col and self.to_optimize["w"]:
             self.w = w_new.contiguous()
@@ -238,12 +287,14 @@ class GaussianMixtureUnif(torch.nn.Module):
             P_row = stats[:, D + 2]
             D2new_row = None
 
-        if not skip_M and self.to_optimize["sigma"]:
-            nds = (D2new_row if keops_sem else stats[:, D + 3]).sum()
-            Ntot = N
-            if dist_on:
-                nds = _sum_ranks(nds, comm)
-                Ntot = int(_sum_ranks(float(N), comm).item())
+        if need_sigma:
+            if keops_sem:
+                # KeOps semantics: sigma from the NEW centroids' rows -- a second exchange
+                nds = D2new_row.sum()
+                if dist_on:
+                    nds = _sum_ranks(nds, comm)
+            if not dist_on:
+                Ntot = N
             self.sigma = torch.sqrt(nds / (self.D * Ntot)).item()
             if self.ensure_continuum:      # (experimental) GMM.py:298-299 / :457-458
                 self.sigma = max(self.sigma, intrinsic_scale(self.mu))
@@ -261,9 +312,9 @@ class GaussianMixtureUnif(torch.nn.Module):
         if self.outliers is None:
             Cfe = Cfe_n_comp.sum()
             q = quad_n.sum()
-            if dist_on:
-                Cfe = _sum_ranks(Cfe, comm).to(X.dtype)
-                q = _sum_ranks(q, comm)
+            if dist_on:       # one scalar exchange for the free energy's two sums
+                Cfe, q = _sum_ranks_many((Cfe, q), comm)
+                Cfe = Cfe.to(X.dtype)
             FE = Cfe + q.item() / sig2x2
         else:
             gamma0_n = lgamma0_n.exp()
@@ -273,8 +324,7 @@ class GaussianMixtureUnif(torch.nn.Module):
                    + gamma0_n * (-logJ0 + lgamma0_n - lpi0)).sum()
             q = (gammaT_n * quad_n).sum()
             if dist_on:
-                Cfe = _sum_ranks(Cfe, comm)
-                q = _sum_ranks(q, comm)
+                Cfe, q = _sum_ranks_many((Cfe, q), comm)
             Cfe = Cfe.item()
             FE = Cfe + q.item() / sig2x2
         return Y, Cfe, FE

@@ -16,6 +16,7 @@ import weakref
 
 import torch
 
+from .. import _lib
 from ..tools.integrators import EulerIntegrator, RalstonIntegrator
 from ..tools.kernel import GaussKernel, SVDpow
 from ..tools.optim import LBFGS_optimization
@@ -45,7 +46,11 @@ class Shoot(list):
 
     def detach(self):
         d = lambda t: None if t is None else t.detach()
-        return Shoot(d(self.Q), d(self.P), d(self.C), d(self.X), d(self.H0))
+        sh = Shoot(d(self.Q), d(self.P), d(self.C), d(self.X), d(self.H0))
+        for k in ("p1_missing", "raw", "q0_key"):     # LDDMMModel.complete_shoot's inputs
+            if hasattr(self, k):
+                setattr(sh, k, getattr(self, k))
+        return sh
 
 
 class LDDMMModel:
@@ -208,11 +213,13 @@ class LDDMMModel:
             # rarely used reference variant: generic integrator over the per-step ODE
             cost0 = torch.zeros(1, dtype=q0.dtype, device=q0.device)
             return self.Integrator(self.ODE, (q0, p0, cost0), self.nt)
-        outs = ShootFn.apply(q0.contiguous(), p0.contiguous(),
+        q0c = q0.contiguous()
+        raw = self._raw_for(q0)
+        outs = ShootFn.apply(q0c, p0.contiguous(),
                              None if x0 is None else x0.contiguous(), self.Kernel.sigma,
                              float(self.eta), int(self.nt), self.scheme, bool(self.withlogdet),
                              self.row_split, getattr(self, "row_orders", None),
-                             getattr(self, "shoot_cache", None), bool(need_p1), self._raw_for(q0))
+                             getattr(self, "shoot_cache", None), bool(need_p1), raw)
         if x0 is None:
             Q, P, C, H0 = outs
             sh = Shoot(Q, P, C, None, H0)
@@ -220,6 +227,10 @@ class LDDMMModel:
             sh = Shoot(*outs)
         sh.p1_missing = skip_p1(need_p1, self.scheme, x0 is not None, float(self.eta),
                                 self._split(), int(self.nt))
+        if sh.p1_missing:
+            # what complete_shoot needs to form P[nt] exactly as this shooting would have: the
+            # coordinate mode its kernels ran in and the support tensor its row order is keyed on
+            sh.raw, sh.q0_key = raw, q0c
         return sh
 
     def _split(self):
@@ -228,15 +239,25 @@ class LDDMMModel:
     def complete_shoot(self, shoot):
         """Form the final momenta of a shoot made with need_p1=False (no-op otherwise)."""
         if getattr(shoot, "p1_missing", False):
-            # the row visit order the shooting itself used (fwd_alg 3 with row_orders), so the
-            # completed P[nt] is the one a full shooting would have produced
+            # the row visit order (fwd_alg 3 with row_orders, keyed on the shooting's own q0
+            # tensor, not a view of the trajectory) and the coordinate mode (raw beyond
+            # RAW_EXTENT_SIGMA) the shooting itself used, so the completed P[nt] is bitwise the
+            # one a full shooting would have produced
             split = self._split()
-            order, order_l = row_order_for(getattr(self, "row_orders", None), shoot.Q[0],
+            key = getattr(shoot, "q0_key", None)
+            raw = getattr(shoot, "raw", None)
+            if key is None:
+                key = shoot.Q[0]
+            if raw is None:
+                raw = self._raw_for(key)
+            order, order_l = row_order_for(getattr(self, "row_orders", None), key,
                                            float(self.eta), split, shoot.Q.shape[1])
-            complete_p1(shoot.Q, shoot.P, self.Kernel.sigma, float(self.eta),
-                        bool(self.withlogdet), int(self.nt),
-                        order=order_l if split is not None else order, split=split)
+            with _lib.coord_mode(raw):
+                complete_p1(shoot.Q, shoot.P, self.Kernel.sigma, float(self.eta),
+                            bool(self.withlogdet), int(self.nt),
+                            order=order_l if split is not None else order, split=split)
             shoot.p1_missing = False
+            shoot.q0_key = None
         return shoot
 
     def BasicQuadLossFunctor(self, y, cmul=1):

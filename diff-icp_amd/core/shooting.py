@@ -319,8 +319,11 @@ class ShootFn(torch.autograd.Function):
         # cotangent's dL/dp term instead of re-summing it pair by pair (saved, nt x M x D floats)
         use_zs = bool(want_div) and scheme == "Euler" and not has_x and nt >= 2 and _lib.zs_ok(eta)
         ctx.has_zs = use_zs
+        # option_epoch: a set_option of a kernel variant between two shootings is a miss (the
+        # cached trajectory would not be bitwise what the new variant computes)
         params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
-                  None if split is None else (split.rank, split.world), skip, use_zs, ctx.raw)
+                  None if split is None else (split.rank, split.world), skip, use_zs, ctx.raw,
+                  _lib.option_epoch())
         hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
         if hit is not None:
             ctx.split = split if (split is not None and not has_x and scheme == "Euler"

@@ -62,10 +62,10 @@ struct SymGeom {
 // pair-subset launch (nparts > 1, row-split over ranks) has 1/nparts of the blocks, so L
 // shrinks until a part still has >= 2048 workgroups (2 x 256 CUs x 4 resident) to fill the
 // chip; smaller L = more (shorter) blocks and more partial slots.
-inline SymGeom sym_geom(int64_t M, int nparts = 1) {
+inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG) {
   SymGeom g;
   g.M = M;
-  g.nG = (int)((M + kSymG - 1) / kSymG);
+  g.nG = (int)((M + G - 1) / G);
   g.nQ = (g.nG + kSymQ - 1) / kSymQ;
   int L = sym_L();
   if (L <= 0) {
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxW
 // ran without the divergence cotangent's pair terms (SymBwdPk<., ., ., false>) and their row
 // total, -gam s zs_i (gam = *gdiv), is added here, once per row (row split: by the rank that
 // owns the row's forward slice).
-template <int D, bool kPart, int W = 2 * D>
+template <int D, bool kPart, int W = 2 * D, int G = kSymG>
 __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
                                                         int64_t slot_stride, int64_t M, int nG,
                                                         int L, float s, float alpha, Outs o,
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
   if (e >= M * W) return;
   const int64_t row = e / W;
   const int c = (int)(e - row * W);
-  const int T = (int)(row / kSymG);
+  const int T = (int)(row / G);
   const int ns = sym_nslots(T, nG, L);
   float acc;
   if constexpr (!kPart) {
@@ -756,8 +756,9 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
 // W = accumulators per point (SymBwd: 2D, SymFwd: 3D with the divergence, else 2D)
 inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
   if (M <= 0) return 0;
-  const SymGeom g = sym_geom(M, nparts);
-  return (size_t)g.nslot * (size_t)M * (size_t)W * sizeof(float);
+  const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256);  // 128 / 256-point groups
+  const int ns = g.nslot > g4.nslot ? g.nslot : g4.nslot;
+  return (size_t)ns * (size_t)M * (size_t)W * sizeof(float);
 }
 
 // Forward merge: one thread per row sums its slots (slot order) and applies the epilogue to
@@ -899,9 +900,54 @@ template <int D, bool GQ, bool B0, bool GT, bool RAW>
 __global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                   int64_t slot_stride, int qoff, int qstride);
 
+// 4 rows per lane (two float2 row pairs, 256-point groups: lddmm_sym_pk.hpp sym_pk4_body) for
+// the packed eta = 0 VJP.  dicp_set_option "sym_rp" (row pairs per lane): 1 = 2 rows, 2 = 4
+// rows, 0 = automatic -- 4 rows from DICP_SYM_ROWS4_MIN_M points when a launch (a row-split
+// part: 1/nparts of the pairs) still has >= DICP_SYM_ROWS4_MIN_PAIRS pairs; below that the
+// quarter as many workgroups leave a tail.  Measured on MI355X (tools/probes/sym_rp_ab.py,
+// profiles/r04_ab_sym_rp.jsonl): adjoint step with divergence rows 0.91x at 50k, 1.05x at
+// 70k, 1.07x at 90k-200k (gp-only step 1.10-1.14x); row-split parts 0.91x at 70k / 8 parts,
+// 1.03-1.15x from ~2e9 pairs per part.
+constexpr int kSymG4 = 256;
+inline int& sym_rp() {
+  static int v = 0;
+  return v;
+}
+#ifndef DICP_SYM_ROWS4_MIN_M
+#define DICP_SYM_ROWS4_MIN_M 64000
+#endif
+#ifndef DICP_SYM_ROWS4_MIN_PAIRS
+#define DICP_SYM_ROWS4_MIN_PAIRS 2.0e9
+#endif
+inline bool sym_use_rows4(int64_t M, int nparts) {
+  if (sym_rp() == 1) return false;
+  if (sym_rp() == 2) return true;
+  return M >= DICP_SYM_ROWS4_MIN_M && (double)M * (double)M / (double)nparts >= DICP_SYM_ROWS4_MIN_PAIRS;
+}
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+__global__ void sym_bwd_pk4_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
+                                   int64_t slot_stride, int qoff, int qstride);
+
 template <int D, bool GQ, bool B0>
-inline void sym_bwd_pk_launch(bool gt, bool raw, dim3 grid, hipStream_t st, const Args& a, const Scal& sc,
+inline void sym_bwd_pk4_launch(bool gt, bool raw, dim3 grid, hipStream_t st, const Args& a, const Scal& sc,
+                               int64_t M, const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
+  if (gt && raw)
+    sym_bwd_pk4_kernel<D, GQ, B0, true, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+  else if (gt)
+    sym_bwd_pk4_kernel<D, GQ, B0, true, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+  else if (raw)
+    sym_bwd_pk4_kernel<D, GQ, B0, false, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+  else
+    sym_bwd_pk4_kernel<D, GQ, B0, false, false><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
+}
+
+template <int D, bool GQ, bool B0>
+inline void sym_bwd_pk_launch(bool g4, bool gt, bool raw, dim3 grid, hipStream_t st, const Args& a, const Scal& sc,
                               int64_t M, const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
+  if (g4) {
+    sym_bwd_pk4_launch<D, GQ, B0>(gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
+    return;
+  }
   if (gt && raw)
     sym_bwd_pk_kernel<D, GQ, B0, true, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
   else if (gt)
@@ -930,7 +976,8 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   }
   const bool gt = !(zs != nullptr || sc.dev0 == nullptr);  // pair loop with the gam terms
   const float* gd = zs != nullptr ? sc.dev0 : nullptr;
-  const SymGeom g = sym_geom(M, nparts);
+  const bool g4 = pk && sym_use_rows4(M, nparts);   // 256-point groups (fewer slots: the 128 workspace fits)
+  const SymGeom g = sym_geom(M, nparts, g4 ? kSymG4 : kSymG);
   const size_t need = sym_ws_bytes(M, 2 * D, nparts);
   if (ws == nullptr || wsb < need) {
     set_error("ode_self_bwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
@@ -948,14 +995,20 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     if (nq1 > 0) {
       const dim3 grid((unsigned)g.Kmax, (unsigned)nq1);
       if (b0)
-        sym_bwd_pk_launch<D, false, true>(gt, raw, grid, st, a, sc, M, g, slab, stride1, part, nparts);
+        sym_bwd_pk_launch<D, false, true>(g4, gt, raw, grid, st, a, sc, M, g, slab, stride1, part, nparts);
       else
-        sym_bwd_pk_launch<D, false, false>(gt, raw, grid, st, a, sc, M, g, slab, stride1, part, nparts);
+        sym_bwd_pk_launch<D, false, false>(g4, gt, raw, grid, st, a, sc, M, g, slab, stride1, part, nparts);
       int rc = check_launch("ode_self_bwd(sym gp)");
       if (rc) return rc;
     }
     const dim3 mg((unsigned)((M * D + 255) / 256));
-    if (nparts > 1)
+    if (g4 && nparts > 1)
+      sym_merge_kernel<D, true, D, kSymG4><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
+                                                                     part, nparts, zs, zr0, zn, gd);
+    else if (g4)
+      sym_merge_kernel<D, false, D, kSymG4><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
+                                                                      0, 1, zs, zr0, zn, gd);
+    else if (nparts > 1)
       sym_merge_kernel<D, true, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
                                                              part, nparts, zs, zr0, zn, gd);
     else
@@ -968,9 +1021,9 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   if (nq_own > 0) {
     const dim3 grid((unsigned)g.Kmax, (unsigned)nq_own);
     if (pk && b0)
-      sym_bwd_pk_launch<D, true, true>(gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
+      sym_bwd_pk_launch<D, true, true>(g4, gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else if (pk)
-      sym_bwd_pk_launch<D, true, false>(gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
+      sym_bwd_pk_launch<D, true, false>(g4, gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else
       sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
           a, sc, M, g.nG, g.L, slab, stride, part, nparts);
@@ -978,11 +1031,18 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     if (rc) return rc;
   }
   const int64_t n = M * 2 * D;
-  if (nparts > 1)
-    sym_merge_kernel<D, true><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+  const dim3 mgn((unsigned)((n + 255) / 256));
+  if (g4 && nparts > 1)
+    sym_merge_kernel<D, true, 2 * D, kSymG4><<<mgn, dim3(256), 0, st>>>(
+        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn, gd);
+  else if (g4)
+    sym_merge_kernel<D, false, 2 * D, kSymG4><<<mgn, dim3(256), 0, st>>>(
+        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
+  else if (nparts > 1)
+    sym_merge_kernel<D, true><<<mgn, dim3(256), 0, st>>>(
         slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn, gd);
   else
-    sym_merge_kernel<D, false><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
+    sym_merge_kernel<D, false><<<mgn, dim3(256), 0, st>>>(
         slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
   return check_launch("ode_self_bwd(sym merge)");
 }

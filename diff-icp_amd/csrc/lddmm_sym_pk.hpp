@@ -218,6 +218,49 @@ struct SymBwdPk {
       }
     }
   }
+  // 4 rows per lane (sym_pk4_body): unordered pairs {i, j} of both row pairs r0, r1 against one
+  // column record.  The column's total over the 4 rows is formed with packed products -- the
+  // two row pairs' terms are chained into one float2 and only its two halves are added as
+  // scalars -- instead of two scalar FMAs per row and accumulator (4 rows: per D-component
+  // 4-5 v_pk + 1 scalar add instead of 8-10 scalar FMAs + 2 adds).
+  __device__ static void pair_sym4(const Prm& prm, const Row2& r0, const Row2& r1, const float* rec,
+                                   f2* acc0, f2* acc1, float* ct) {
+    const float gt = prm.gt;
+    f2 cv[5 * D];
+    colvec(rec, cv);
+    Shared t0, t1;
+    shared_terms(prm, r0, cv, t0);
+    shared_terms(prm, r1, cv, t1);
+    const f2* pj = cv + D;
+    const f2* aj = cv + 2 * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const f2 ka0 = GT ? pk_fma(splat(-gt), t0.z[d], aj[d]) : aj[d];
+      const f2 ka1 = GT ? pk_fma(splat(-gt), t1.z[d], aj[d]) : aj[d];
+      const f2 tt0 = GT ? pk_fma(splat(gt), t0.z[d], r0.ia_a[d]) : r0.ia_a[d];
+      const f2 tt1 = GT ? pk_fma(splat(gt), t1.z[d], r1.ia_a[d]) : r1.ia_a[d];
+      f2 cg;
+      if constexpr (B0) {
+        acc0[d] = pk_fma(t0.K, ka0, acc0[d]);
+        acc1[d] = pk_fma(t1.K, ka1, acc1[d]);
+        cg = pk_fma(t1.K, tt1, t0.K * tt0);
+      } else {
+        acc0[d] = pk_fma(t0.cKzb, pj[d], pk_fma(t0.K, ka0, acc0[d]));
+        acc1[d] = pk_fma(t1.cKzb, pj[d], pk_fma(t1.K, ka1, acc1[d]));
+        cg = pk_fma(t1.cKzb, r1.p[d], pk_fma(t1.K, tt1, pk_fma(t0.cKzb, r0.p[d], t0.K * tt0)));
+      }
+      ct[d] = cg.x + cg.y;
+      if constexpr (GQ) {
+        const f2 e0 = pk_fma(t0.w, t0.z[d], -t0.u[d]);
+        const f2 e1 = pk_fma(t1.w, t1.z[d], -t1.u[d]);
+        const f2 Ke0 = t0.K * e0;
+        acc0[D + d] = acc0[D + d] + Ke0;
+        acc1[D + d] = pk_fma(t1.K, e1, acc1[D + d]);
+        const f2 cs = pk_fma(t1.K, e1, Ke0);
+        ct[D + d] = -(cs.x + cs.y);
+      }
+    }
+  }
 };
 
 // LDS layout of the column records in sym_pk_body: record float i lives in plane
@@ -420,6 +463,177 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 #pragma unroll
     for (int k = 0; k < W; ++k) dst[k] = r == 0 ? racc[k].x : racc[k].y;
   }
+}
+
+// 4 rows per lane (dicp_set_option "sym_rp", automatic from ~90k points): sym_pk_body with 256-point
+// groups -- a wave's lane holds rows r*64 + l (r = 0..3) of its group as two float2 row pairs,
+// the column record and the DPP rotation of the column sums are shared by the 4 rows, and a
+// column group is staged as 256 records (four 64-column quarters).  Slots and merge are those
+// of the 128 form with G = 256 (sym_merge_kernel<..., kSymG4>).
+#ifndef DICP_SYMBWD4_PK_CT
+#define DICP_SYMBWD4_PK_CT 1   // column sums over the 4 rows in packed form (SymBwdPk::pair_sym4)
+#endif
+#ifndef DICP_SYMBWD4_UNROLL
+#define DICP_SYMBWD4_UNROLL 2
+#endif
+#ifndef DICP_SYMBWD4_WMIN
+#define DICP_SYMBWD4_WMIN 1
+#endif
+template <class P>
+__device__ __forceinline__ void sym_pk4_body(Args a, Scal sc, int64_t M, int nG, int L,
+                                             float* __restrict__ slab, int64_t slot_stride, int qoff,
+                                             int qstride) {
+  using S = typename P::S;
+  using LY = rec_layout<P>;
+  constexpr int G = kSymG4;
+  constexpr int CW = S::CW, NP = LY::kPlanes, W = P::W;
+  __shared__ float4 planes[2][NP][G];
+  __shared__ float colacc[kSymQ][G][W];
+  if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
+  const typename P::Prm prm = P::params(a, sc);
+
+  const int Q = qoff + qstride * (int)blockIdx.y, kc = blockIdx.x;
+  const int B0 = kSymQ * Q + kc * L;
+  if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
+  const int B1 = min(B0 + L, nG);
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int A = kSymQ * Q + wv;
+
+  typename P::Row2 row[2];
+  int64_t ri[4];
+  bool rv[4];
+  {
+    typename S::Row r4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ri[r] = (int64_t)A * G + r * 64 + l;
+      rv[r] = A < nG && ri[r] < M;
+      S::load_row(a, sc, rv[r] ? ri[r] : 0, rv[r], r4[r]);
+    }
+    P::pack(r4[0], r4[1], row[0]);
+    P::pack(r4[2], r4[3], row[1]);
+  }
+  f2 racc[2][W];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < W; ++k) racc[h][k] = splat(0.f);
+
+  auto stage = [&](int B, int buf) {
+    const int64_t j = (int64_t)B * G + tid;   // 256 threads: one record each
+    float rec[4 * CW], ph[4 * NP];
+    S::load_col(a, sc, j < M ? j : 0, j < M, rec);
+#pragma unroll
+    for (int k = 0; k < 4 * NP; ++k) ph[k] = 0.f;
+#pragma unroll
+    for (int i = 0; i < S::kUsed; ++i) ph[LY::slot(i)] = rec[i];
+    if constexpr (LY::kDupW) {
+#pragma unroll
+      for (int m = 0; m < NP; ++m) ph[4 * m + 3] = ph[4 * m + 2];
+    }
+#pragma unroll
+    for (int m = 0; m < NP; ++m)
+      planes[buf][m][tid] = make_float4(ph[4 * m], ph[4 * m + 1], ph[4 * m + 2], ph[4 * m + 3]);
+  };
+
+  int buf = 0;
+  auto ldrec = [&](int col, float* rec) {
+    float ph[4 * NP];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      const int w = plane_width<P>(m);
+      const float* src = reinterpret_cast<const float*>(&planes[buf][m][col]);
+      if (w == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = v.z, ph[4 * m + 3] = v.w;
+      } else if (w == 3) {
+        const float3 v = *reinterpret_cast<const float3*>(src);
+        ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = v.z, ph[4 * m + 3] = 0.f;
+      } else if (w == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = ph[4 * m + 3] = 0.f;
+      } else {
+        ph[4 * m] = src[0], ph[4 * m + 1] = ph[4 * m + 2] = ph[4 * m + 3] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * CW; ++i) rec[i] = i < S::kUsed ? ph[LY::slot(i)] : 0.f;
+#pragma unroll
+    for (int m = 0; m < NP; ++m) rec[4 * CW + m] = LY::kDupW ? ph[4 * m + 3] : 0.f;
+  };
+  stage(B0, 0);
+  __syncthreads();
+  for (int B = B0; B < B1; ++B) {
+    if (B + 1 < B1) stage(B + 1, buf ^ 1);
+    const bool sym = A < B;          // wave-uniform
+    const bool diag = A == B;
+#pragma unroll 1
+    for (int h = 0; h < G / 64; ++h) {
+      float cacc[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+      if (sym) {
+#pragma unroll DICP_SYMBWD4_UNROLL
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW + NP];
+          ldrec(col, rec);
+#if DICP_SYMBWD4_PK_CT
+          float ct[W];
+          P::pair_sym4(prm, row[0], row[1], rec, racc[0], racc[1], ct);
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+#else
+          float ct0[W], ct1[W];   // each row pair's column sums in scalar form, then added
+          P::pair_sym(prm, row[0], rec, racc[0], ct0);
+          P::pair_sym(prm, row[1], rec, racc[1], ct1);
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + (ct0[k] + ct1[k]);
+#endif
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+      } else if (diag) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = h * 64 + ((l + k2) & 63);
+          float rec[4 * CW + NP];
+          ldrec(col, rec);
+          P::pair_row(prm, row[0], rec, racc[0]);
+          P::pair_row(prm, row[1], rec, racc[1]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) colacc[wv][h * 64 + l][k] = cacc[k];
+    }
+    __syncthreads();
+    {
+      const int64_t j = (int64_t)B * G + tid;
+      if (j < M) {
+        float* dst = slab + (int64_t)Q * slot_stride + j * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+          dst[k] = ((colacc[0][tid][k] + colacc[1][tid][k]) + colacc[2][tid][k]) + colacc[3][tid][k];
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (!rv[r]) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+    const f2* ra = racc[r >> 1];
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = (r & 1) == 0 ? ra[k].x : ra[k].y;
+  }
+}
+
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD4_WMIN, 4))) void sym_bwd_pk4_kernel(
+    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
+    int qstride) {
+  sym_pk4_body<SymBwdPk<D, GQ, B0, GT, RAW>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
 }
 
 template <int D, bool GQ, bool B0, bool GT, bool RAW>

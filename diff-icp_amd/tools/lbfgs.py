@@ -40,6 +40,12 @@ import math
 import numpy as np
 import torch
 
+# the host-scalar line search reaches torch's decisions through NEP 50 promotion (a numpy
+# float32 scalar combined with a Python float stays float32), which numpy 1.x does not do
+if int(np.__version__.split(".")[0]) < 2:
+    raise ImportError(f"difficp_amd.tools.lbfgs needs numpy >= 2 (NEP 50 scalar promotion), "
+                      f"found {np.__version__}")
+
 
 def _rowdots(A, v):
     """A @ v as a deterministic elementwise product + row reduction, accumulated in float64

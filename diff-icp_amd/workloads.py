@@ -18,22 +18,26 @@ from .core.LDDMM import LDDMMModel
 from .core.PSR import DiffPSR
 
 
-def _gmm_cloud(n, ncent, sig, g):
-    cent = torch.rand(ncent, 3, generator=g)
+def _gmm_cloud(n, ncent, sig, g, D=3):
+    cent = torch.rand(ncent, D, generator=g)
     lab = torch.randint(0, ncent, (n,), generator=g)
-    return cent[lab] + sig * torch.randn(n, 3, generator=g)
+    return cent[lab] + sig * torch.randn(n, D, generator=g)
 
 
-def _phi(x, amp, perm=(1, 2, 0)):
-    """Smooth synthetic deformation x + amp sin(2 pi x_perm)."""
+def _phi(x, amp, perm=None):
+    """Smooth synthetic deformation x + amp sin(2 pi x_perm) (perm: a cyclic shift of the axes)."""
+    if perm is None:
+        perm = [(d + 1) % x.shape[1] for d in range(x.shape[1])]
     return x + amp * torch.sin(2 * math.pi * x[:, list(perm)])
 
 
-def two_set_points(N, seed=0):
-    """C2/C3 inputs: xB from a 64-centre 3D GMM (sigma 0.02); xA = phi(xB) + N(0, 0.005^2)."""
+def two_set_points(N, seed=0, D=3):
+    """C2/C3 inputs: xB from a 64-centre GMM in D dimensions (sigma 0.02); xA = phi(xB) +
+    N(0, 0.005^2).  D = 2 is the planar form of the same generator (the reference's examples
+    are 2D: diffICP_basic.py, the Chui sets)."""
     g = torch.Generator().manual_seed(seed)
-    xB = _gmm_cloud(N, 64, 0.02, g)
-    xA = _phi(xB, 0.03) + 0.005 * torch.randn(N, 3, generator=g)
+    xB = _gmm_cloud(N, 64, 0.02, g, D)
+    xA = _phi(xB, 0.03) + 0.005 * torch.randn(N, D, generator=g)
     return xA.float().contiguous(), xB.float().contiguous()
 
 
@@ -64,16 +68,16 @@ def multi_structure_frames(K, S, N, seed=0):
 
 
 def build_two_set(N, device, seed=0, sigma_gmm=0.05, sigma_lddmm=0.1, lam=1e3, nt=10,
-                  scheme="Euler", version="hybrid", v2p_args=None):
+                  scheme="Euler", version="hybrid", v2p_args=None, D=3):
     """ICP_two_set (ICP_two_set.py:176-226): GMM with mu = xB, w frozen, sigma optimised;
     LDDMM hybrid (withlogdet, gradcomponent False), Euler nt=10, dense support.
     version="logdet" is the exact ICP_two_set model (gradcomponent=True, ICP_two_set.py:203-207;
     SURVEY C2'): its a0 is initialised by v2p, here the device ridge CG (v2p_args)."""
     spec = {"device": device, "dtype": torch.float32}
-    xA, xB = two_set_points(N, seed)
+    xA, xB = two_set_points(N, seed, D)
     G = GaussianMixtureUnif(xB.to(device), sigma=sigma_gmm, spec=spec)
     G.to_optimize = {"mu": False, "sigma": True, "w": False, "eta0": False}
-    LM = LDDMMModel(sigma=sigma_lddmm, D=3, lambd=lam, version=version, scheme=scheme, nt=nt, spec=spec)
+    LM = LDDMMModel(sigma=sigma_lddmm, D=D, lambd=lam, version=version, scheme=scheme, nt=nt, spec=spec)
     psr = DiffPSR(xA.to(device), G, LM, dataspec=spec, compspec=spec, v2p_args=v2p_args)
     psr.printstuff = False
     return psr

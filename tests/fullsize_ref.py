@@ -149,3 +149,86 @@ def gmm_columns(X, mu, lpi, sigma, chunk=16384):
         sd2 = sd2 + (lg.exp() * D2).sum()
         m = mn
     return m + acc_w.log(), acc_x / acc_w[:, None], sd2
+
+
+# ---------------------------------------------------------------------------------------
+# Whole shootings and their gradients at full size (Euler; LDDMM.py:286-299, :318-334,
+# integrators.py:20-33; the gradient of tools/optim.py:46's L.backward()), row-chunked
+# ---------------------------------------------------------------------------------------
+def ode_full(q, p, sigma, eta=0.0, withlogdet=True, rows=2048):
+    """LDDMMModel.ODE (LDDMM.py:176-227) for ALL rows: (v, mG, dcost) with dcost =
+    mdivsum(q, q, p) = sum_i g_i (hybrid / logdet) or 0 (classic)."""
+    vs, ms, gsum = [], [], torch.zeros((), dtype=q.dtype, device=q.device)
+    for r0 in range(0, q.shape[0], rows):
+        v, mG, g, _ = self_terms(q[r0:r0 + rows], p[r0:r0 + rows], q, p, sigma, eta)
+        vs.append(v)
+        ms.append(mG)
+        gsum = gsum + g.sum()
+    dc = gsum if withlogdet else torch.zeros_like(gsum)
+    return torch.cat(vs), torch.cat(ms), dc
+
+
+def hamiltonian_full(q, p, sigma, eta=0.0, rows=2048):
+    """H(q, p) (LDDMM.py:142-159) as the sum of self_terms' per-row h."""
+    H = torch.zeros((), dtype=q.dtype, device=q.device)
+    for r0 in range(0, q.shape[0], rows):
+        H = H + self_terms(q[r0:r0 + rows], p[r0:r0 + rows], q, p, sigma, eta)[3].sum()
+    return H
+
+
+def ode_vjp_full(q, p, a, b, gam, sigma, eta=0.0, withlogdet=True, rows=1024, chunk=4096):
+    """d/d(q, p) of L = sum_k a_k.v_k + b_k.mG_k + gam dcost over ALL rows (b None: zero mG
+    cotangent), by autograd of row chunks of the ODE against all columns."""
+    gq = torch.zeros_like(q)
+    gp = torch.zeros_like(p)
+    with torch.enable_grad():
+        qq = q.detach().clone().requires_grad_(True)
+        pp = p.detach().clone().requires_grad_(True)
+        for r0 in range(0, q.shape[0], rows):
+            sl = slice(r0, r0 + rows)
+            v, mG, g, _ = self_terms(qq[sl], pp[sl], qq, pp, sigma, eta, chunk)
+            L = (a[sl] * v).sum()
+            if b is not None:
+                L = L + (b[sl] * mG).sum()
+            if withlogdet:
+                L = L + gam * g.sum()
+            dq, dp = torch.autograd.grad(L, (qq, pp))
+            gq += dq
+            gp += dp
+    return gq, gp
+
+
+def shoot_full(q0, p0, sigma, nt, eta=0.0, withlogdet=True):
+    """Euler shooting (integrators.py:20-33 over LDDMM.py:176-227): lists Q, P (nt+1) and
+    the cost at each time (float64 scalars)."""
+    dt = 1.0 / nt
+    Q, P, C = [q0], [p0], [torch.zeros((), dtype=q0.dtype, device=q0.device)]
+    for _ in range(nt):
+        v, mG, dc = ode_full(Q[-1], P[-1], sigma, eta, withlogdet)
+        Q.append(Q[-1] + dt * v)
+        P.append(P[-1] + dt * mG)
+        C.append(C[-1] + dt * dc)
+    return Q, P, C
+
+
+def shoot_loss_grad_p0(q0, p0, sigma, nt, lam, y, eta=0.0, withlogdet=True, rows=1024, chunk=4096):
+    """Optimize's loss at p0 (LDDMM.py:318-334 trajloss + the quadratic data loss
+    1/2 |q1 - y|^2) and its gradient w.r.t. p0 (optim.py:46), by the discrete adjoint of
+    the Euler shooting with chunked-autograd VJPs of each step.  Returns
+    (q1, cost1, trajloss, loss, grad_p0)."""
+    dt = 1.0 / nt
+    Q, P, C = shoot_full(q0, p0, sigma, nt, eta, withlogdet)
+    H0 = hamiltonian_full(q0, p0, sigma, eta)
+    traj = lam * H0 + C[-1]
+    loss = traj + 0.5 * ((Q[-1] - y) ** 2).sum()
+    lq = Q[-1] - y              # dL/dq1
+    lp = None                   # the loss does not read p1
+    for t in range(nt - 1, -1, -1):
+        gq, gp = ode_vjp_full(Q[t], P[t], lq, lp, 1.0, sigma, eta, withlogdet, rows, chunk)
+        lq = lq + dt * gq
+        lp = (0 if lp is None else lp) + dt * gp
+    # dH0/dp0 = v(q0, p0) (eta = 0) -- by autograd of the chunked Hamiltonian in general
+    with torch.enable_grad():
+        pp = p0.detach().clone().requires_grad_(True)
+        dH, = torch.autograd.grad(hamiltonian_full(q0, pp, sigma, eta), (pp,))
+    return Q[-1], C[-1], traj, loss, lp + lam * dH

@@ -56,3 +56,17 @@ def test_no_cpu_fallback():
     x = torch.rand(4, 3)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.gauss_red(_lib.KRED, x, x, 0.5, b=x)
+
+
+def test_option_epoch_bumps_on_kernel_variant_change(lib):
+    """ShootCache keys on _lib.option_epoch(): a set_option of a kernel variant between two
+    shootings makes the cached trajectory a miss; the per-thread coordinate
+    mode does not bump it (it is keyed separately)."""
+    from difficp_amd import _lib
+    e0 = _lib.option_epoch()
+    old = _lib.get_option("bwd_alg")
+    _lib.set_option("bwd_alg", old)
+    assert _lib.option_epoch() == e0 + 1
+    with _lib.coord_mode(True):
+        pass
+    assert _lib.option_epoch() == e0 + 1

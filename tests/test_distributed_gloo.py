@@ -107,3 +107,73 @@ def test_sharded_atlas_matches_single_process(world, K, outliers):
     for r in range(1, world):
         assert np.array_equal(out[0][1]["mu"], out[r][1]["mu"])
         assert out[0][1]["sigma"] == out[r][1]["sigma"]
+
+
+def _count_worker(rank, world, port, q, outliers):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, HERE)
+        sys.path.insert(0, ROOT)
+        import fake_hip
+        fake_hip.install_plain()
+        from difficp_amd.core.GMM import GaussianMixtureUnif
+        calls = []
+        names = ("all_gather", "all_gather_into_tensor", "all_reduce", "broadcast", "reduce_scatter",
+                 "all_to_all", "gather", "scatter", "barrier")
+        orig = {n: getattr(dist, n) for n in names}
+
+        def wrap(n):
+            def f(*a, **k):
+                calls.append(n)
+                return orig[n](*a, **k)
+            return f
+        spec = {"device": "cpu", "dtype": torch.float32}
+        g = torch.Generator().manual_seed(3 + rank)
+        X = torch.rand(40 + 7 * rank, 2, generator=g)
+        mu0 = torch.rand(5, 2, generator=torch.Generator().manual_seed(1))
+        G = GaussianMixtureUnif(mu0, sigma=0.1, use_outliers=outliers, spec=spec)
+        G.to_optimize = {"mu": True, "sigma": True, "w": True, "eta0": True}
+        G.comm = True
+        if outliers:
+            G.set_vol0(X)           # (one-off, outside the counted EM steps)
+        for n in names:
+            setattr(dist, n, wrap(n))
+        per_step = []
+        try:
+            for _ in range(3):
+                del calls[:]
+                G.EM_step(X)
+                per_step.append(list(calls))
+        finally:
+            for n in names:
+                setattr(dist, n, orig[n])
+        q.put((rank, per_step, G.mu.numpy().copy(), G.sigma))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("outliers", [False, True])
+def test_em_step_one_stats_exchange(outliers):
+    """SURVEY 8(e) / VERDICT r03: an EM step of the sharded GMM exchanges its statistics in
+    ONE packed collective (column statistics, sigma numerator, outlier LSE terms, point
+    count) plus ONE scalar exchange for the free energy -- at most 2 collectives."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_count_worker, args=(r, world, port, q, outliers)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, per_step, mu, sigma in out:
+        for calls in per_step:
+            assert len(calls) <= 2, (rank, calls)
+    assert np.array_equal(out[0][2], out[1][2]) and out[0][3] == out[1][3]

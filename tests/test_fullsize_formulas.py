@@ -83,3 +83,29 @@ def test_gmm_rows_and_columns_match_oracle():
     D2 = ((X[:, None] - mu[None]) ** 2).sum(-1)
     t = lpi[None] - D2 / (2 * sig ** 2) - lgn
     assert rel_err(T, t.logsumexp(1)) < 1e-13
+
+
+@pytest.mark.parametrize("version", ["hybrid", "classic", "logdet"])
+def test_shoot_loss_grad_matches_oracle_autograd(version):
+    """The chunked whole-shooting restatement (fullsize_ref.shoot_loss_grad_p0: Euler shoot,
+    trajloss, quadratic data loss and the discrete-adjoint gradient w.r.t. p0) equals the
+    oracle's Shoot / trajloss with torch autograd (float64, small size)."""
+    g = torch.Generator().manual_seed(21)
+    M, sig, nt, lam = 150, 0.2, 5, 30.0
+    grad_comp, logdet = {"hybrid": (False, True), "classic": (False, False), "logdet": (True, True)}[version]
+    eta = 1.0 / lam if grad_comp else 0.0
+    q0 = torch.rand(M, 3, generator=g, dtype=torch.float64)
+    p0 = 0.05 * torch.randn(M, 3, generator=g, dtype=torch.float64)
+    y = q0 + 0.02 * torch.randn(M, 3, generator=g, dtype=torch.float64)
+    m = R.LDDMM(sig, 3, lam, grad_comp, logdet, scheme="Euler", nt=nt)
+    pr = p0.clone().requires_grad_(True)
+    sh = m.Shoot(q0, pr)
+    traj = m.trajloss(sh)
+    loss = traj + 0.5 * ((sh[-1][0] - y) ** 2).sum()
+    gref, = torch.autograd.grad(loss, (pr,))
+    q1, c1, tr, lo, gp0 = F.shoot_loss_grad_p0(q0, p0, sig, nt, lam, y, eta, logdet)
+    assert rel_err(q1, sh[-1][0].detach()) < 1e-12
+    assert abs(float(c1 - sh[-1][2].detach().sum())) < 1e-10 * max(1.0, abs(float(c1)))
+    assert abs(float(tr - traj.detach())) < 1e-10 * abs(float(traj))
+    assert abs(float(lo - loss.detach())) < 1e-10 * abs(float(loss))
+    assert rel_err(gp0, gref) < 1e-10

@@ -152,18 +152,21 @@ def test_fullsize_deterministic_and_split_invariant(full):
 
 
 @pytest.mark.gpu
-def test_estep_fullsize_subset_and_properties(dev):
-    """Two-set E/M passes at C2 size: 50k points x 50k components (mu = xB)."""
+@pytest.mark.parametrize("NF", [M_FULL, 100000, 200000])
+def test_estep_fullsize_subset_and_properties(dev, NF):
+    """Two-set E/M passes at C2 size (50k points x 50k components, mu = xB), the headline's
+    100k x 100k and C3's 200k x 200k (GMM.py:260-282): sampled rows against float64, and the
+    size-independent column identities."""
     from difficp_amd import _lib
     g = torch.Generator().manual_seed(5)
-    X = torch.rand(M_FULL, 3, generator=g, dtype=torch.float64)
-    mu = torch.rand(M_FULL, 3, generator=g, dtype=torch.float64)
-    w = 0.1 * torch.randn(M_FULL, generator=g, dtype=torch.float64)
+    X = torch.rand(NF, 3, generator=g, dtype=torch.float64)
+    mu = torch.rand(NF, 3, generator=g, dtype=torch.float64)
+    w = 0.1 * torch.randn(NF, generator=g, dtype=torch.float64)
     lpi = w - w.logsumexp(0)
     lgn = 3 * (math.log(SIG_G) + 0.5 * math.log(2 * math.pi))
     f = lambda t: t.float().to(dev).contiguous()
     T, T2, stats = _lib.gmm_estep(f(X), f(mu), f(lpi / math.log(2)), f((mu * mu).sum(-1)), SIG_G, lgn, True)
-    sub = torch.randperm(M_FULL, generator=g)[:NSUB]
+    sub = torch.randperm(NF, generator=g)[:NSUB]
     D2 = ((X[sub][:, None, :] - mu[None]) ** 2).sum(-1)
     t = lpi[None] - D2 / (2 * SIG_G ** 2) - lgn
     T64 = t.logsumexp(1)
@@ -175,7 +178,7 @@ def test_estep_fullsize_subset_and_properties(dev):
     # M-step column statistics: log sum_n gamma_nc and the gamma-weighted means
     col = _lib.gmm_mstep(f(X), T2, f(mu), f(lpi / math.log(2)), SIG_G).cpu().double()
     wn = col[:, 0]
-    assert abs(float(wn.logsumexp(0)) - math.log(M_FULL)) < 1e-5      # sum_nc gamma = N
+    assert abs(float(wn.logsumexp(0)) - math.log(NF)) < 1e-5      # sum_nc gamma = N
     fin = torch.isfinite(wn)
     xsum = (torch.exp(wn[fin])[:, None] * col[fin, 1:]).sum(0)
     assert rel_err(xsum, X.sum(0)) < 1e-5                             # sum_c sum_n gamma x_n = sum_n x_n

@@ -128,3 +128,94 @@ def test_external_point_passes_four_rows_vs_two_rows(dev, N, M, D, eta):
         L.set_option("red_alg", old)
     for a, b in zip(res[2], res[1]):
         assert rel_err(a.cpu(), b.cpu()) < 1e-6, rel_err(a.cpu(), b.cpu())
+
+
+# --- the symmetric VJP with 4 rows per lane (lddmm_sym_pk.hpp sym_pk4_body, "sym_rp") ---
+
+class _srp(_rp):
+    def __enter__(self):
+        L = _lib()
+        self.old = L.get_option("sym_rp")
+        L.set_option("sym_rp", self.v)
+
+    def __exit__(self, *a):
+        _lib().set_option("sym_rp", self.old)
+
+
+def _vjp_variants(L, qf, pf, a, b, gd, zs, raw):
+    """Every launch form of the packed eta = 0 VJP: plain (with / without the divergence
+    cotangent), the adjoint steps reusing the divergence rows (full, zero momentum cotangent,
+    gp only) and the pair-subset parts of a 3-way row split (summed)."""
+    with L.coord_mode(raw):
+        o = {"bwd": L.ode_self_bwd(qf, pf, a, b, gd, SIG, 0.0),
+             "bwd_nodiv": L.ode_self_bwd(qf, pf, a, b, None, SIG, 0.0),
+             "adj_zs": L.euler_adjoint_step(qf, pf, a, b, gd, SIG, 0.0, 0.1, zs=zs),
+             "adj_b0": L.euler_adjoint_step(qf, pf, a, None, gd, SIG, 0.0, 0.1, zs=zs),
+             "adj_gp": (L.euler_adjoint_step(qf, pf, a, b, gd, SIG, 0.0, 0.1, want_lq=False, zs=zs)[1],)}
+        sq, sp = torch.zeros_like(qf), torch.zeros_like(qf)
+        for r in range(3):
+            pq, pp = L.ode_self_bwd_part(qf, pf, a, b, gd, SIG, 0.0, r, 3)
+            sq += pq
+            sp += pp
+        o["parts3"] = (sq, sp)
+    torch.cuda.synchronize()
+    return o
+
+
+@pytest.mark.parametrize("M,D", [(1, 3), (129, 2), (257, 3), (1023, 2), (1025, 3), (4700, 3), (33001, 3)])
+@pytest.mark.parametrize("raw", [False, True])
+def test_vjp_four_rows_vs_two_rows(dev, M, D, raw):
+    """The packed symmetric VJP forced to 4 rows per lane (256-point groups, packed column sums
+    over the 4 rows) against 2 rows at ragged sizes, every launch variant, scaled and raw
+    coordinates: fp32 summation order only (2e-6); and against float64 autograd of the
+    oracle's ODE (2e-5, tests/test_gpu_kernels.py::test_ode_self_bwd's tolerance)."""
+    L = _lib()
+    g = torch.Generator().manual_seed(11 * M + D)
+    q = torch.rand(M, D, generator=g, dtype=torch.float64)
+    p = 0.1 * torch.randn(M, D, generator=g, dtype=torch.float64)
+    a = torch.randn(M, D, generator=g, dtype=torch.float64)
+    b = torch.randn(M, D, generator=g, dtype=torch.float64)
+    gam = torch.randn(1, generator=g, dtype=torch.float64)
+    f = lambda t: t.float().to(dev)
+    qf, pf, af, bf, gd = f(q), f(p), f(a), f(b), f(gam)
+    zs = torch.empty(M, D, device=dev)
+    L.euler_step(qf, pf, SIG, 0.0, 0.1, True, zs_out=zs)
+    outs = {}
+    for rp in (1, 2):
+        with _srp(rp):
+            outs[rp] = _vjp_variants(L, qf, pf, af, bf, gd, zs, raw)
+    for k in outs[1]:
+        for x4, x2 in zip(outs[2][k], outs[1][k]):
+            assert rel_err(x4.cpu(), x2.cpu()) < 2e-6, (k, rel_err(x4.cpu(), x2.cpu()))
+    # determinism: the 4-row kernel is bitwise reproducible run to run
+    with _srp(2):
+        again = _vjp_variants(L, qf, pf, af, bf, gd, zs, raw)
+    for k in again:
+        for x, y in zip(again[k], outs[2][k]):
+            assert torch.equal(x, y), k
+    if M > 5000:
+        return
+    qq, pp = q.clone().requires_grad_(True), p.clone().requires_grad_(True)
+    m = R.LDDMM(SIG, D, 50.0, False, True)
+    v, mG, c = m.ODE(qq, pp, torch.zeros(1, dtype=torch.float64))
+    gq64, gp64 = torch.autograd.grad((a * v).sum() + (b * mG).sum() + (gam * c).sum(), (qq, pp))
+    gq, gp = outs[2]["bwd"]
+    assert rel_err(gq.cpu(), gq64) < 2e-5 and rel_err(gp.cpu(), gp64) < 2e-5
+    gq, gp = outs[2]["parts3"]
+    assert rel_err(gq.cpu(), gq64) < 2e-5 and rel_err(gp.cpu(), gp64) < 2e-5
+
+
+def test_vjp_rows_automatic_rule(dev):
+    """sym_rp 0 (automatic) picks 4 rows from 64k points (and 2e9 pairs per part) and 2 below: the
+    automatic result equals the forced form bitwise on each side of the threshold."""
+    L = _lib()
+    for M, want in ((20000, 1), (100000, 2)):
+        g = torch.Generator().manual_seed(M)
+        qf = torch.rand(M, 3, generator=g).to(dev)
+        pf = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
+        a = torch.randn(M, 3, generator=g).to(dev)
+        res = {}
+        for rp in (0, want):
+            with _srp(rp):
+                res[rp] = L.ode_self_bwd(qf, pf, a, a, None, SIG, 0.0)
+        assert torch.equal(res[0][0], res[want][0]) and torch.equal(res[0][1], res[want][1]), M

@@ -18,6 +18,10 @@ CHILD = r"""
 import json, sys, torch
 sys.path.insert(0, %r)
 from difficp_amd import _lib
+import os
+for kv in filter(None, os.environ.get("DICP_AB_OPTS", "").split(",")):   # e.g. sym_rp=2
+    k, v = kv.split("=")
+    _lib.set_option(k, int(v))
 M = %d
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
