@@ -332,6 +332,10 @@ def _main(out):
     ap.add_argument("--concurrent-frames", type=int, default=None,
                     help="atlas workloads: frames optimised concurrently (host threads / HIP "
                          "streams); default automatic (4), 1 = the reference's sequential loop")
+    ap.add_argument("--batch-frames", choices=["auto", "on", "off"], default="auto",
+                    help="atlas workloads: the local frames' shooting launches in lockstep batches "
+                         "(core/batching.py; auto = whenever the path allows), --concurrent-frames "
+                         "groups of them on their own HIP streams")
     ap.add_argument("--lib-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="dicp_set_option before the run (A/B experiments; repeatable)")
     ap.add_argument("--replicas", action="store_true",
@@ -393,12 +397,14 @@ def _main(out):
         comm = True if world > 1 else None
         psr = workloads.build_atlas(K, wl["N"], wl["C"], dev, comm=comm, seed=0, S=wl["S"])
         psr.concurrent_frames = args.concurrent_frames
+        psr.batch_frames = {"auto": None, "on": True, "off": False}[args.batch_frames]
         cfg = {"workload": f"groupwise atlas {K} frames x {wl['S']} structures x {wl['N']} 3D points, "
                            f"C={wl['C']} per structure" + (" (BASELINE configs[3], fixed)" if fixed else ""),
                "frames_per_rank": (f"{K // world}-{-(-K // world)}" if fixed else wl["K_per_rank"]),
                "lddmm": "hybrid sigma=0.1 lambda=1e3 Euler nt=10 dense", "max_repeat_GMM": 10,
                "tol": 1e-3, "parallelism": f"frame-sharded dp{world} (RCCL suff-stat exchange)",
-               "concurrent_frames": args.concurrent_frames or "auto"}
+               "concurrent_frames": args.concurrent_frames or "auto",
+               "batch_frames": args.batch_frames}
         scaling = "strong" if fixed else "weak"
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s")
@@ -497,8 +503,11 @@ def _main(out):
                     "alg_bytes_per_launch": d["bytes"] / d["launches"],
                     "alg_hbm_GBps": round(d["bytes"] / d["launches"] / avg_s / 1e9, 3),
                     "share_of_step_time": round(d["ms"] / prof_iters * 1e-3 / (elapsed / args.steps), 3),
-                    "measured_on": ("one extra sequential-frame iteration after the timed region "
-                                    "(the timed iterations overlap frames on HIP streams)") if concurrent
+                    "measured_on": (("one extra iteration after the timed region with all local frames "
+                                     "in ONE lockstep launch batch (the timed iterations overlap several "
+                                     "batches on HIP streams)") if getattr(psr, "batch_stats", None)
+                                    else ("one extra sequential-frame iteration after the timed region "
+                                          "(the timed iterations overlap frames on HIP streams)")) if concurrent
                                    else "the timed iterations",
                     "note": "pair kernels are fp32 VALU/exp-bound (O(N) bytes, O(N^2) work): "
                             "compute roofline, HBM bytes reported as alg_hbm_GBps/traffic; traffic "
@@ -528,6 +537,8 @@ def _main(out):
         tot_ms = sum(v["ms"] for v in summ.values())
         kern_gbps = (round(sum(v["bytes"] for v in summ.values()) / (tot_ms * 1e-3) / 1e9, 3)
                      if tot_ms > 0 else None)
+        if getattr(psr, "batch_stats", None):
+            cfg["batch_stats_last_reg_opt"] = psr.batch_stats
         line = {
             "metric": METRIC, "value": round(value, 5), "unit": "PSR iterations/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

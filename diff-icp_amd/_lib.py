@@ -76,6 +76,9 @@ _SIGNATURES = {
     "dicp_num_splits": [_INT, _I64, _I64],
     "dicp_set_option": [ctypes.c_char_p, _INT],
     "dicp_get_option": [ctypes.c_char_p, ctypes.POINTER(_INT)],
+    "dicp_batch_begin": [],
+    "dicp_batch_end": [_P],
+    "dicp_batch_abort": [],
 }
 _RESTYPES = {"dicp_workspace_bytes": _SZ, "dicp_last_error": ctypes.c_char_p,
              "dicp_version": ctypes.c_char_p}
@@ -280,7 +283,9 @@ FLOPS_PER_PAIR["ode_self_fwd_eta_nog"] = round(70 * 14 / 39)
 
 
 class KernelProfile:
-    """Context manager collecting (name, pairs, flops, bytes, start, end) per launch."""
+    """Context manager collecting (name, pairs, flops, bytes, start, end[, share]) per launch;
+    a batched launch over several calls (LaunchBatcher) is one record per kernel name, whose
+    time is the batch's time x that name's share of the batch's flops."""
 
     def __init__(self):
         self.records = []
@@ -297,20 +302,33 @@ class KernelProfile:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, pairs, flops, nbytes, e0, e1 in self.records:
+        for rec in self.records:
+            name, pairs, flops, nbytes, e0, e1 = rec[:6]
+            share = rec[6] if len(rec) > 6 else 1.0
             d = out.setdefault(name, {"launches": 0, "pairs": 0, "flops": 0, "bytes": 0, "ms": 0.0})
             d["launches"] += 1
             d["pairs"] += pairs
             d["flops"] += flops
             d["bytes"] += nbytes
-            d["ms"] += e0.elapsed_time(e1)
+            d["ms"] += e0.elapsed_time(e1) * share
         return out
 
 
 _prof = None
 
 
+# per host thread: the LaunchBatcher (core/batching.py) its batchable launches go through
+_tl = threading.local()
+# the launches a LaunchBatcher may batch: the packed eta = 0 shooting passes (fwd_alg 2 /
+# bwd_alg 3, the C-ABI's batchable paths, include/difficp_hip.h dicp_batch_begin)
+BATCHABLE = frozenset({"ode_self_fwd", "ode_self_fwd_nog", "ode_self_bwd", "ode_self_bwd_b0",
+                       "ode_self_bwd_gp"})
+
+
 def _launch(name, pairs, nbytes, fn):
+    b = getattr(_tl, "batcher", None)
+    if b is not None and name in BATCHABLE:
+        return b.submit(name, pairs, nbytes, fn)
     if _prof is None:
         return fn()
     st = torch.cuda.current_stream()
@@ -333,7 +351,11 @@ def _workspace(kind: int, M: int, N: int, D: int, device):
         nbytes = _WS_BYTES[key] = int(lib().dicp_workspace_bytes(kind, int(M), int(N), int(D)))
     if nbytes == 0:
         return None, 0
-    return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    keep = getattr(_tl, "batch_keep", None)
+    if keep is not None:   # a batch open on this thread: the launch runs at its end
+        keep.append(ws)
+    return ws, nbytes
 
 
 # ---------------------------------------------------------------------------------------
@@ -806,3 +828,31 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, 
                                                                    _stream(q.device)))
     _check_rc(rc, "ode_self_bwd_part")
     return gq, gp
+
+
+class batch:
+    """Context manager around dicp_batch_begin / dicp_batch_end(stream) on this host thread:
+    the batchable library calls made inside record their launches, which are issued grouped
+    on `stream` at exit (include/difficp_hip.h).  An exception inside discards the batch."""
+
+    def __init__(self, stream_handle):
+        self.stream = stream_handle
+
+    def __enter__(self):
+        _check_rc(lib().dicp_batch_begin(), "batch_begin")
+        # workspaces allocated by the recorded calls stay referenced until the batch is issued
+        # (a freed block could be handed to the next call of the same batch)
+        self._prev_keep = getattr(_tl, "batch_keep", None)
+        _tl.batch_keep = []
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        try:
+            if exc_type is not None:
+                lib().dicp_batch_abort()
+                return False
+            _check_rc(lib().dicp_batch_end(self.stream), "batch_end")
+            return False
+        finally:
+            # issued on self.stream: blocks freed now are reused in that stream's order
+            _tl.batch_keep = self._prev_keep

@@ -239,6 +239,7 @@ class DiffPSR(MultiPSR):
         self.q0 = self.allx0
         self.a0 = [None] * self.K
         self.concurrent_frames = None   # Reg_opt host threads / HIP streams (None = automatic)
+        self.batch_frames = None        # Reg_opt lockstep launch batches (None = automatic)
         self.initialize_a0()
 
     def initialize_a0(self, **v2p_args):
@@ -315,6 +316,8 @@ class DiffPSR(MultiPSR):
         if nconc is None:
             nconc = 4 if str(self.compspec.get("device", "cpu")).startswith("cuda") else 1
         nconc = min(int(nconc), len(frames))
+        if self._batch_frames_ok(len(frames)):
+            return self._optimize_frames_batched(frames, max(1, nconc), nmax, tol)
         if nconc <= 1 or self.LMi.row_split is not None:
             return {k: self._optimize_frame(k, nmax, tol) for k in frames}
         import threading
@@ -342,6 +345,63 @@ class DiffPSR(MultiPSR):
 
         with ThreadPoolExecutor(max_workers=nconc) as ex:
             return dict(ex.map(work, frames))
+
+    def _batch_frames_ok(self, nframes):
+        """Whether Reg_opt runs the local frames in lockstep launch batches (core/batching.py):
+        `batch_frames` True / False, or None (default) = automatically when every frame's
+        shooting takes the batchable path -- dense support (no external points), Euler, the
+        eta = 0 models (classic / hybrid) on the packed kernels (fwd_alg 2, bwd_alg 3) -- on a
+        HIP device with at least 2 local frames."""
+        want = getattr(self, "batch_frames", None)
+        if want is False:
+            return False
+        ok = (nframes >= 2 and self.support_scheme is None and self.LMi.scheme == "Euler"
+              and self.LMi.eta == 0 and self.LMi.row_split is None
+              and not getattr(self.LMi, "try_trajcost_optim", False)
+              and getattr(self.LMi, "row_orders", None) is None
+              and str(self.compspec.get("device", "cpu")).startswith("cuda"))
+        if ok:
+            from .. import _lib
+            ok = _lib.get_option("fwd_alg") == 2 and _lib.get_option("bwd_alg") == 3
+        if want is True and not ok:
+            raise ValueError("batch_frames=True needs dense support, Euler, eta = 0, fwd_alg 2, "
+                             "bwd_alg 3 and >= 2 local frames on a HIP device")
+        return ok
+
+    def _optimize_frames_batched(self, frames, ngroups, nmax, tol):
+        """{k: Optimize(...)}: every local frame on its own host thread, the frames split into
+        `ngroups` groups (contiguous in frame order), each group on one HIP stream with one
+        LaunchBatcher -- within a group the frames' shooting launches are issued as one batched
+        grid per step (lockstep), while the groups overlap each other's host work.  Each
+        frame's computation is unchanged: results bitwise those of the sequential loop.
+        (`concurrent_frames` = the number of groups here; 1 = every local frame in one batch.)"""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from .batching import LaunchBatcher, frame_thread
+        main = torch.cuda.current_stream()
+        per = -(-len(frames) // ngroups)
+        groups = [frames[i:i + per] for i in range(0, len(frames), per)]
+        batchers = []
+        for g in groups:
+            st = torch.cuda.Stream()
+            st.wait_stream(main)
+            b = LaunchBatcher(st)
+            b.register(len(g))     # up front: the first batch waits for every frame
+            batchers.append(b)
+        owner = {k: batchers[i] for i, g in enumerate(groups) for k in g}
+
+        def work(k):
+            b = owner[k]
+            with frame_thread(b, k):
+                out = self._optimize_frame(k, nmax, tol)
+            b.stream.synchronize()       # results are consumed on `main` afterwards
+            return k, out
+
+        with ThreadPoolExecutor(max_workers=len(frames)) as ex:
+            res = dict(ex.map(work, frames))
+        self.batch_stats = {"groups": len(groups), "batches": sum(b.batches for b in batchers),
+                            "calls": sum(b.calls for b in batchers)}
+        return res
 
     def Reg_opt(self, nmax=10, tol=1e-3):
         """Per-frame LDDMM optimisation (PSR.py:521-569), local frames only when sharded."""

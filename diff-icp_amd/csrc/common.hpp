@@ -20,6 +20,8 @@
 
 #include <type_traits>
 
+#include "batch.hpp"
+
 namespace dicp {
 
 #ifndef DICP_STAGE_EARLY
@@ -300,10 +302,10 @@ struct MergeSet {
 };
 
 template <bool MIN>
-__global__ __launch_bounds__(kBlock) void merge_slabs_kernel(MergeSet m, Outs o, int S) {
-  const int j = blockIdx.y;
+__device__ __forceinline__ void merge_slabs_body(const MergeSet& m, const Outs& o, int S, unsigned bx, unsigned by) {
+  const int j = by;
   const int64_t n = m.n[j];
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t e = (int64_t)bx * kBlock + threadIdx.x;
   if (e >= n) return;
   const float* __restrict__ slab = m.slab[j];
   float a = slab[e];
@@ -313,6 +315,28 @@ __global__ __launch_bounds__(kBlock) void merge_slabs_kernel(MergeSet m, Outs o,
   }
   const int k = m.k[j];
   o.ptr[k][e] = epilogue(o, k, e, a);
+}
+
+template <bool MIN>
+__global__ __launch_bounds__(kBlock) void merge_slabs_kernel(MergeSet m, Outs o, int S) {
+  merge_slabs_body<MIN>(m, o, S, blockIdx.x, blockIdx.y);
+}
+
+// batched form (batch.hpp): blockIdx.z = the recorded call
+struct MergeEntry {
+  MergeSet m;
+  Outs o;
+  int S;
+  unsigned gx, gy;
+};
+template <bool MIN>
+__global__ __launch_bounds__(kBlock) void merge_slabs_batch_kernel(BatchTab<MergeEntry> t) {
+  const MergeEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
+  merge_slabs_body<MIN>(e.m, e.o, e.S, blockIdx.x, blockIdx.y);
+}
+inline int merge_slabs_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<MergeEntry>(merge_slabs_batch_kernel<false>, es, st, "merge_slabs");
 }
 
 }  // namespace dicp

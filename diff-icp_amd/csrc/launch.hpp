@@ -128,6 +128,7 @@ int rowred_splits(int64_t M, int64_t N) {
 }
 
 inline int check_launch(const char* what) {
+  if (batching()) return batch_check(what);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error("%s: HIP launch failed: %s", what, hipGetErrorString(e));
@@ -153,6 +154,7 @@ size_t rowred_ws_bytes(int64_t M, int64_t N) {
 template <class Op, int R>
 int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                   const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (int rc = no_batch("rowred (scalar rows)")) return rc;
   if (M <= 0) return DICP_OK;
   const int S = rowred_splits<Op, R>(M, N);
   const int64_t chunk = N > 0 ? chunk_of(N, S) : 0;

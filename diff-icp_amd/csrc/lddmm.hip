@@ -496,6 +496,7 @@ int ode_self_bwd_part_d(const float* q, const float* p, const float* gv, const f
     set_error("ode_self_bwd_part: a NULL mG cotangent (zero) needs a symmetric packed kernel");
     return DICP_ERR_INVALID;
   }
+  if (int rc = no_batch("ode_self_bwd_part(ordered)")) return rc;
   const int64_t per = (M + nparts - 1) / nparts;
   const int64_t r0 = per * part < M ? per * part : M;
   const int64_t r1 = r0 + per < M ? r0 + per : M;
@@ -629,6 +630,7 @@ extern "C" int dicp_lddmm_ode_self_fwd_f32(const float* q, const float* p, int64
                                            double sigma, double eta, float* v, float* mG,
                                            float* g, float* h, void* ws, size_t ws_bytes,
                                            dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || (M > 0 && (!q || !p || !v || !mG)) || !(sigma > 0)) {
     set_error("dicp_lddmm_ode_self_fwd_f32: invalid arguments");
@@ -646,6 +648,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_f32(const float* q, const float* p, const
                                            int D, double sigma, double eta, float* gq,
                                            float* gp, void* ws, size_t ws_bytes,
                                            dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || (M > 0 && (!q || !p || !gv || !gp)) || !(sigma > 0)) {  // gmG NULL = zero (eta = 0)
     set_error("dicp_lddmm_ode_self_bwd_f32: invalid arguments");
@@ -665,6 +668,7 @@ extern "C" int dicp_lddmm_euler_step_f32(const float* q, const float* p, int64_t
                                          double sigma, double eta, double dt, float* q_next,
                                          float* p_next, float* g, void* ws, size_t ws_bytes,
                                          dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || (M > 0 && (!q || !p || !q_next || !p_next)) || !(sigma > 0) ||
       (M > 0 && (q_next == q || q_next == p || p_next == q || p_next == p))) {
@@ -692,6 +696,7 @@ extern "C" int dicp_lddmm_euler_adjoint_step_zs_f32(const float* q, const float*
                                                     const float* addq, const float* addp,
                                                     const float* zs, float* lq_next, float* lp_next,
                                                     void* ws, size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const float* ins[5] = {q, p, lq, lp, zs};
   bool alias = false;
@@ -724,6 +729,7 @@ extern "C" int dicp_lddmm_euler_adjoint_step_f32(const float* q, const float* p,
                                                  const float* addq, const float* addp,
                                                  float* lq_next, float* lp_next, void* ws,
                                                  size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   return dicp_lddmm_euler_adjoint_step_zs_f32(q, p, lq, lp, gdiv, M, D, sigma, eta, dt, addq, addp, nullptr,
                                               lq_next, lp_next, ws, ws_bytes, stream);
 }
@@ -732,6 +738,7 @@ extern "C" int dicp_lddmm_ode_ext_fwd_f32(const float* x, int64_t N, const float
                                           const float* p, int64_t M, int D, double sigma,
                                           double eta, float* vx, float* gx, void* ws,
                                           size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (N < 0 || M < 0 || (N > 0 && (!x || !vx)) || (M > 0 && (!q || !p)) || !(sigma > 0)) {
     set_error("dicp_lddmm_ode_ext_fwd_f32: invalid arguments");
@@ -749,6 +756,7 @@ extern "C" int dicp_lddmm_ode_ext_bwd_f32(const float* x, int64_t N, const float
                                           double eta, const float* gvx, const float* gdiv,
                                           float* gxo, float* gq, float* gp, void* ws,
                                           size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (N < 0 || M < 0 || (N > 0 && (!x || !gvx || !gxo)) || (M > 0 && (!q || !p || !gq || !gp)) ||
       !(sigma > 0)) {
@@ -769,6 +777,7 @@ extern "C" int dicp_lddmm_ode_self_fwd_rows_f32(const float* q, const float* p, 
                                                 double sigma, double eta, float* v, float* mG,
                                                 float* g, float* h, void* ws, size_t ws_bytes,
                                                 dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
       (nrows > 0 && (!q || !p || !v || !mG)) || !(sigma > 0)) {
@@ -788,6 +797,7 @@ extern "C" int dicp_lddmm_euler_step_rows_f32(const float* q, const float* p, in
                                               double eta, double dt, float* q_next,
                                               float* p_next, float* g, void* ws,
                                               size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
       (nrows > 0 && (!q || !p || !q_next || !p_next)) || !(sigma > 0)) {
@@ -812,6 +822,7 @@ extern "C" int dicp_lddmm_ode_self_fwd_zs_f32(const float* q, const float* p, in
                                               int64_t nrows, int D, double sigma, double eta,
                                               const int32_t* row_order, float* v, float* mG, float* g,
                                               float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
       (nrows > 0 && (!q || !p || !v || !mG || !zs)) || !(sigma > 0)) {
@@ -831,6 +842,7 @@ extern "C" int dicp_lddmm_ode_self_fwd_ord_f32(const float* q, const float* p, i
                                                double eta, const int32_t* row_order, float* v,
                                                float* mG, float* g, float* h, void* ws,
                                                size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
       (nrows > 0 && (!q || !p || !v || !mG)) || !(sigma > 0)) {
@@ -850,6 +862,7 @@ extern "C" int dicp_lddmm_euler_step_zs_f32(const float* q, const float* p, int6
                                             const int32_t* row_order, float* q_next, float* p_next,
                                             float* g, float* zs, void* ws, size_t ws_bytes,
                                             dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // p_next may be NULL: the momenta update is not wanted (the packed pass skips its Gs' / Hs /
   // GL' sums); zs may be NULL (no divergence rows)
@@ -877,6 +890,7 @@ extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int
                                              double eta, double dt, const int32_t* row_order,
                                              float* q_next, float* p_next, float* g, void* ws,
                                              size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   return dicp_lddmm_euler_step_zs_f32(q, p, M, row0, nrows, D, sigma, eta, dt, row_order, q_next, p_next, g,
                                       nullptr, ws, ws_bytes, stream);
 }
@@ -887,6 +901,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_part_zs_f32(const float* q, const float* 
                                                    int nparts, const float* zs, int64_t zrow0,
                                                    int64_t znrows, float* gq, float* gp, void* ws,
                                                    size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (M < 0 || nparts < 1 || part < 0 || part >= nparts ||
       (M > 0 && (!q || !p || !gv || !gp)) || !(sigma > 0) ||  // gq may be NULL (gp only), gmG NULL = 0
@@ -907,6 +922,7 @@ extern "C" int dicp_lddmm_ode_self_bwd_part_f32(const float* q, const float* p, 
                                                 int D, double sigma, double eta, int part,
                                                 int nparts, float* gq, float* gp, void* ws,
                                                 size_t ws_bytes, dicp_stream_t stream) {
+  dicp::BatchCall batch_call_;  // a call of a launch batch (batch.hpp)
   return dicp_lddmm_ode_self_bwd_part_zs_f32(q, p, gv, gmG, gdiv, M, D, sigma, eta, part, nparts, nullptr, 0, 0,
                                              gq, gp, ws, ws_bytes, stream);
 }

@@ -698,14 +698,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, S::kMaxW
 // total, -gam s zs_i (gam = *gdiv), is added here, once per row (row split: by the rank that
 // owns the row's forward slice).
 template <int D, bool kPart, int W = 2 * D, int G = kSymG>
-__global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
-                                                        int64_t slot_stride, int64_t M, int nG,
-                                                        int L, float s, float alpha, Outs o,
-                                                        int qoff, int qstride,
-                                                        const float* __restrict__ zs = nullptr,
-                                                        int64_t zr0 = 0, int64_t zn = 0,
-                                                        const float* __restrict__ gdiv = nullptr) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void sym_merge_body(const float* __restrict__ slab, int64_t slot_stride, int64_t M,
+                                               int nG, int L, float s, float alpha, const Outs& o, int qoff,
+                                               int qstride, const float* __restrict__ zs, int64_t zr0, int64_t zn,
+                                               const float* __restrict__ gdiv, unsigned bx) {
+  const int64_t e = (int64_t)bx * 256 + threadIdx.x;
   if (e >= M * W) return;
   const int64_t row = e / W;
   const int c = (int)(e - row * W);
@@ -752,6 +749,68 @@ __global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict_
     if (o.ptr[0]) o.ptr[0][idx] = epilogue(o, 0, idx, s * acc);
   }
 }
+
+template <int D, bool kPart, int W = 2 * D, int G = kSymG>
+__global__ __launch_bounds__(256) void sym_merge_kernel(const float* __restrict__ slab,
+                                                        int64_t slot_stride, int64_t M, int nG,
+                                                        int L, float s, float alpha, Outs o,
+                                                        int qoff, int qstride,
+                                                        const float* __restrict__ zs = nullptr,
+                                                        int64_t zr0 = 0, int64_t zn = 0,
+                                                        const float* __restrict__ gdiv = nullptr) {
+  sym_merge_body<D, kPart, W, G>(slab, slot_stride, M, nG, L, s, alpha, o, qoff, qstride, zs, zr0, zn, gdiv,
+                                 blockIdx.x);
+}
+
+// batched forms (batch.hpp): blockIdx.z = the recorded call
+struct SymMergeEntry {
+  const float* slab;
+  int64_t slot_stride, M;
+  int nG, L;
+  float s, alpha;
+  Outs o;
+  int qoff, qstride;
+  const float* zs;
+  int64_t zr0, zn;
+  const float* gdiv;
+  unsigned gx, gy;
+};
+template <int D, bool kPart, int W, int G>
+__global__ __launch_bounds__(256) void sym_merge_batch_kernel(BatchTab<SymMergeEntry> t) {
+  const SymMergeEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx) return;
+  sym_merge_body<D, kPart, W, G>(e.slab, e.slot_stride, e.M, e.nG, e.L, e.s, e.alpha, e.o, e.qoff, e.qstride, e.zs,
+                                 e.zr0, e.zn, e.gdiv, blockIdx.x);
+}
+template <int D, bool kPart, int W, int G>
+int sym_merge_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<SymMergeEntry>(sym_merge_batch_kernel<D, kPart, W, G>, es, st, "sym_merge");
+}
+// launch (or record, inside a batch) one symmetric-VJP merge
+template <int D, bool kPart, int W = 2 * D, int G = kSymG>
+void sym_merge_launch(dim3 grid, hipStream_t st, const float* slab, int64_t slot_stride, int64_t M, int nG, int L,
+                      float s, float alpha, const Outs& o, int qoff, int qstride, const float* zs, int64_t zr0,
+                      int64_t zn, const float* gdiv) {
+  if (batching()) {
+    batch_record(sym_merge_batch_flush<D, kPart, W, G>,
+                 SymMergeEntry{slab, slot_stride, M, nG, L, s, alpha, o, qoff, qstride, zs, zr0, zn, gdiv, grid.x, 1u});
+    return;
+  }
+  sym_merge_kernel<D, kPart, W, G><<<grid, dim3(256), 0, st>>>(slab, slot_stride, M, nG, L, s, alpha, o, qoff,
+                                                              qstride, zs, zr0, zn, gdiv);
+}
+
+// argument entry of a batched symmetric pair kernel (lddmm_sym_pk.hpp sym_bwd_pk(4)_batch_kernel)
+struct SymEntry {
+  Args a;
+  Scal sc;
+  int64_t M;
+  int nG, L;
+  float* slab;
+  int64_t slot_stride;
+  int qoff, qstride;
+  unsigned gx, gy;
+};
 
 // W = accumulators per point (SymBwd: 2D, SymFwd: 3D with the divergence, else 2D)
 inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
@@ -802,6 +861,7 @@ __global__ void sym_fwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, flo
 template <int D, bool DIV>
 int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
                    hipStream_t st, bool pk = false) {
+  if (int rc = no_batch("ode_self_fwd(sym)")) return rc;
   using S = SymFwd<D, DIV>;
   if (M <= 0) return DICP_OK;
   const SymGeom g = sym_geom(M);
@@ -841,6 +901,7 @@ template <int D>
 int launch_sym_bwd_eta(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws,
                        size_t wsb, hipStream_t st, bool pk = false, int part = 0, int nparts = 1,
                        bool b0 = false) {
+  if (int rc = no_batch("ode_self_bwd(sym eta)")) return rc;
   using S = SymBwdEta<D>;
   if (M <= 0) return DICP_OK;
   if ((nparts > 1 || b0) && !pk) {
@@ -928,9 +989,22 @@ template <int D, bool GQ, bool B0, bool GT, bool RAW>
 __global__ void sym_bwd_pk4_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
                                    int64_t slot_stride, int qoff, int qstride);
 
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+int sym_bwd_pk_batch_flush(const std::vector<const void*>& es, hipStream_t st);
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+int sym_bwd_pk4_batch_flush(const std::vector<const void*>& es, hipStream_t st);
+
 template <int D, bool GQ, bool B0>
 inline void sym_bwd_pk4_launch(bool gt, bool raw, dim3 grid, hipStream_t st, const Args& a, const Scal& sc,
                                int64_t M, const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
+  if (batching()) {
+    const SymEntry e{a, sc, M, g.nG, g.L, slab, stride, part, nparts, grid.x, grid.y};
+    if (gt && raw) batch_record(sym_bwd_pk4_batch_flush<D, GQ, B0, true, true>, e);
+    else if (gt) batch_record(sym_bwd_pk4_batch_flush<D, GQ, B0, true, false>, e);
+    else if (raw) batch_record(sym_bwd_pk4_batch_flush<D, GQ, B0, false, true>, e);
+    else batch_record(sym_bwd_pk4_batch_flush<D, GQ, B0, false, false>, e);
+    return;
+  }
   if (gt && raw)
     sym_bwd_pk4_kernel<D, GQ, B0, true, true><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride, part, nparts);
   else if (gt)
@@ -946,6 +1020,14 @@ inline void sym_bwd_pk_launch(bool g4, bool gt, bool raw, dim3 grid, hipStream_t
                               int64_t M, const SymGeom& g, float* slab, int64_t stride, int part, int nparts) {
   if (g4) {
     sym_bwd_pk4_launch<D, GQ, B0>(gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
+    return;
+  }
+  if (batching()) {
+    const SymEntry e{a, sc, M, g.nG, g.L, slab, stride, part, nparts, grid.x, grid.y};
+    if (gt && raw) batch_record(sym_bwd_pk_batch_flush<D, GQ, B0, true, true>, e);
+    else if (gt) batch_record(sym_bwd_pk_batch_flush<D, GQ, B0, true, false>, e);
+    else if (raw) batch_record(sym_bwd_pk_batch_flush<D, GQ, B0, false, true>, e);
+    else batch_record(sym_bwd_pk_batch_flush<D, GQ, B0, false, false>, e);
     return;
   }
   if (gt && raw)
@@ -1003,17 +1085,16 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
     }
     const dim3 mg((unsigned)((M * D + 255) / 256));
     if (g4 && nparts > 1)
-      sym_merge_kernel<D, true, D, kSymG4><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
-                                                                     part, nparts, zs, zr0, zn, gd);
+      sym_merge_launch<D, true, D, kSymG4>(mg, st, slab, stride1, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs,
+                                           zr0, zn, gd);
     else if (g4)
-      sym_merge_kernel<D, false, D, kSymG4><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
-                                                                      0, 1, zs, zr0, zn, gd);
+      sym_merge_launch<D, false, D, kSymG4>(mg, st, slab, stride1, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0,
+                                            zn, gd);
     else if (nparts > 1)
-      sym_merge_kernel<D, true, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
-                                                             part, nparts, zs, zr0, zn, gd);
+      sym_merge_launch<D, true, D>(mg, st, slab, stride1, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn,
+                                   gd);
     else
-      sym_merge_kernel<D, false, D><<<mg, dim3(256), 0, st>>>(slab, stride1, M, g.nG, g.L, sc.s, a.scale, o,
-                                                              0, 1, zs, zr0, zn, gd);
+      sym_merge_launch<D, false, D>(mg, st, slab, stride1, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
     return check_launch("ode_self_bwd(sym gp merge)");
   }
   const int64_t stride = M * 2 * D;
@@ -1024,7 +1105,10 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
       sym_bwd_pk_launch<D, true, true>(g4, gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
     else if (pk)
       sym_bwd_pk_launch<D, true, false>(g4, gt, raw, grid, st, a, sc, M, g, slab, stride, part, nparts);
-    else
+    else if (batching()) {
+      set_error("ode_self_bwd(sym): the scalar symmetric VJP (bwd_alg 2) has no batched form");
+      return DICP_ERR_UNSUPPORTED;
+    } else
       sym_bwd_kernel<D><<<dim3((unsigned)g.Kmax, (unsigned)nq_own), dim3(256), 0, st>>>(
           a, sc, M, g.nG, g.L, slab, stride, part, nparts);
     int rc = check_launch("ode_self_bwd(sym)");
@@ -1033,17 +1117,15 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   const int64_t n = M * 2 * D;
   const dim3 mgn((unsigned)((n + 255) / 256));
   if (g4 && nparts > 1)
-    sym_merge_kernel<D, true, 2 * D, kSymG4><<<mgn, dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn, gd);
+    sym_merge_launch<D, true, 2 * D, kSymG4>(mgn, st, slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs,
+                                             zr0, zn, gd);
   else if (g4)
-    sym_merge_kernel<D, false, 2 * D, kSymG4><<<mgn, dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
+    sym_merge_launch<D, false, 2 * D, kSymG4>(mgn, st, slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0,
+                                              zn, gd);
   else if (nparts > 1)
-    sym_merge_kernel<D, true><<<mgn, dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn, gd);
+    sym_merge_launch<D, true>(mgn, st, slab, stride, M, g.nG, g.L, sc.s, a.scale, o, part, nparts, zs, zr0, zn, gd);
   else
-    sym_merge_kernel<D, false><<<mgn, dim3(256), 0, st>>>(
-        slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
+    sym_merge_launch<D, false>(mgn, st, slab, stride, M, g.nG, g.L, sc.s, a.scale, o, 0, 1, zs, zr0, zn, gd);
   return check_launch("ode_self_bwd(sym merge)");
 }
 

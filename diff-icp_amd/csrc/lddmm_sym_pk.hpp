@@ -309,7 +309,7 @@ __host__ __device__ constexpr int plane_width(int m) {
 template <class P>
 __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, int L,
                                             float* __restrict__ slab, int64_t slot_stride, int qoff,
-                                            int qstride) {
+                                            int qstride, unsigned bx, unsigned by) {
   using S = typename P::S;
   using LY = rec_layout<P>;
   constexpr int CW = S::CW, NP = LY::kPlanes, W = P::W;
@@ -318,7 +318,7 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
   const typename P::Prm prm = P::params(a, sc);
 
-  const int Q = qoff + qstride * (int)blockIdx.y, kc = blockIdx.x;
+  const int Q = qoff + qstride * (int)by, kc = (int)bx;
   const int B0 = kSymQ * Q + kc * L;
   if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
   const int B1 = min(B0 + L, nG);
@@ -482,7 +482,7 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 template <class P>
 __device__ __forceinline__ void sym_pk4_body(Args a, Scal sc, int64_t M, int nG, int L,
                                              float* __restrict__ slab, int64_t slot_stride, int qoff,
-                                             int qstride) {
+                                             int qstride, unsigned bx, unsigned by) {
   using S = typename P::S;
   using LY = rec_layout<P>;
   constexpr int G = kSymG4;
@@ -492,7 +492,7 @@ __device__ __forceinline__ void sym_pk4_body(Args a, Scal sc, int64_t M, int nG,
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
   const typename P::Prm prm = P::params(a, sc);
 
-  const int Q = qoff + qstride * (int)blockIdx.y, kc = blockIdx.x;
+  const int Q = qoff + qstride * (int)by, kc = (int)bx;
   const int B0 = kSymQ * Q + kc * L;
   if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
   const int B1 = min(B0 + L, nG);
@@ -633,14 +633,42 @@ template <int D, bool GQ, bool B0, bool GT, bool RAW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD4_WMIN, 4))) void sym_bwd_pk4_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
-  sym_pk4_body<SymBwdPk<D, GQ, B0, GT, RAW>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk4_body<SymBwdPk<D, GQ, B0, GT, RAW>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride, blockIdx.x,
+                                             blockIdx.y);
 }
 
 template <int D, bool GQ, bool B0, bool GT, bool RAW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, DICP_SYMBWD_PK_WMAX))) void sym_bwd_pk_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride, int qoff,
     int qstride) {
-  sym_pk_body<SymBwdPk<D, GQ, B0, GT, RAW>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdPk<D, GQ, B0, GT, RAW>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride, blockIdx.x,
+                                            blockIdx.y);
+}
+
+// batched forms (batch.hpp): blockIdx.z = the recorded call (SymEntry, lddmm_sym.hpp)
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD_PK_WMIN, DICP_SYMBWD_PK_WMAX))) void sym_bwd_pk_batch_kernel(
+    BatchTab<SymEntry> t) {
+  const SymEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
+  sym_pk_body<SymBwdPk<D, GQ, B0, GT, RAW>>(e.a, e.sc, e.M, e.nG, e.L, e.slab, e.slot_stride, e.qoff, e.qstride,
+                                            blockIdx.x, blockIdx.y);
+}
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMBWD4_WMIN, 4))) void sym_bwd_pk4_batch_kernel(
+    BatchTab<SymEntry> t) {
+  const SymEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
+  sym_pk4_body<SymBwdPk<D, GQ, B0, GT, RAW>>(e.a, e.sc, e.M, e.nG, e.L, e.slab, e.slot_stride, e.qoff, e.qstride,
+                                             blockIdx.x, blockIdx.y);
+}
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+int sym_bwd_pk_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<SymEntry>(sym_bwd_pk_batch_kernel<D, GQ, B0, GT, RAW>, es, st, "sym_bwd_pk");
+}
+template <int D, bool GQ, bool B0, bool GT, bool RAW>
+int sym_bwd_pk4_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<SymEntry>(sym_bwd_pk4_batch_kernel<D, GQ, B0, GT, RAW>, es, st, "sym_bwd_pk4");
 }
 
 // Packed-FP32 rows of the eta != 0 symmetric VJP (lddmm_sym.hpp SymBwdEta, the logdet /
@@ -795,7 +823,7 @@ template <int D, bool GQ, bool B0>
 __global__ __launch_bounds__(256) void sym_bwd_eta_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,
                                                              float* __restrict__ slab, int64_t slot_stride,
                                                              int qoff, int qstride) {
-  sym_pk_body<SymBwdEtaPk<D, GQ, B0>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride);
+  sym_pk_body<SymBwdEtaPk<D, GQ, B0>>(a, sc, M, nG, L, slab, slot_stride, qoff, qstride, blockIdx.x, blockIdx.y);
 }
 
 // Packed-FP32 rows of the symmetric (pair-once) eta = 0 forward (lddmm_sym.hpp SymFwd): the
@@ -869,7 +897,7 @@ struct SymFwdPk {
 template <int D, bool DIV>
 __global__ __launch_bounds__(256) void sym_fwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,
                                                          float* __restrict__ slab, int64_t slot_stride) {
-  sym_pk_body<SymFwdPk<D, DIV>>(a, sc, M, nG, L, slab, slot_stride, 0, 1);
+  sym_pk_body<SymFwdPk<D, DIV>>(a, sc, M, nG, L, slab, slot_stride, 0, 1, blockIdx.x, blockIdx.y);
 }
 
 }  // namespace dicp

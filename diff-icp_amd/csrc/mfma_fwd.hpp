@@ -370,6 +370,7 @@ template <int D, bool DIV>
 int launch_mfma_fwd(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                     const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st,
                     const int* order = nullptr) {
+  if (int rc = no_batch("ode_self_fwd(mfma)")) return rc;
   using Op = MfFwd<D, DIV>;
   if (M <= 0) return DICP_OK;
   const int S = mfma_fwd_splits<D, DIV>(M, N);

@@ -200,9 +200,11 @@ int pk_rp(int64_t M, int64_t N) {
   return (pk_rp_pref<Op>::value >= 2 && M >= DICP_PK_RP2_ROWS && N >= DICP_PK_RP2_COLS) ? 2 : 1;
 }
 
+// The body of rowred_pk_kernel for block (bx, by) of a grid with S column splits (by < S;
+// S > 1: partial slabs, S = 1: the epilogue) -- shared by the plain and the batched kernel.
 template <class Op, int RP>
-__global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
-                                                           int64_t chunk, Outs outs) {
+__device__ __forceinline__ void rowred_pk_body(Args args, Scal sc, int64_t M, int64_t N, int64_t chunk,
+                                               const Outs& outs, unsigned bx, unsigned by, unsigned S) {
   using Base = typename Op::Base;
   constexpr int CW4 = Op::CW4;
   constexpr int NACC = Op::NACC;
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
   if (sc.dev0 != nullptr) sc.aux0 = sc.dev0[0];
 
   const int tid = threadIdx.x;
-  const int64_t ibase = (int64_t)blockIdx.x * (kBlock * 2 * RP) + tid;
+  const int64_t ibase = (int64_t)bx * (kBlock * 2 * RP) + tid;
   typename Base::Row brow[RP][2];
   typename Op::Row2 row[RP];
 #pragma unroll
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
 #pragma unroll
     for (int k = 0; k < NACC; ++k) tot[h][k] = splat(0.f);
 
-  const int64_t j0 = (int64_t)blockIdx.y * chunk;
+  const int64_t j0 = (int64_t)by * chunk;
   int64_t j1 = j0 + chunk;
   if (j1 > N) j1 = N;
 
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
     cnt = cntn;
   }
 
-  const bool split = gridDim.y > 1;
+  const bool split = S > 1;
 #pragma unroll
   for (int h = 0; h < RP; ++h) {
 #pragma unroll
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
         float* base = outs.ptr[k];
         if (base != nullptr) {
           if (split) {
-            float* dst = base + (int64_t)blockIdx.y * M * w + i * w;
+            float* dst = base + (int64_t)by * M * w + i * w;
 #pragma unroll
             for (int e = 0; e < w; ++e) dst[e] = vals[off + e];
           } else {
@@ -312,6 +314,31 @@ __global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args
       }
     }
   }
+}
+
+template <class Op, int RP>
+__global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_kernel(Args args, Scal sc, int64_t M, int64_t N,
+                                                           int64_t chunk, Outs outs) {
+  rowred_pk_body<Op, RP>(args, sc, M, N, chunk, outs, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// batched form (batch.hpp): blockIdx.z = the recorded call
+struct PkEntry {
+  Args a;
+  Scal sc;
+  Outs outs;
+  int64_t M, N, chunk;
+  unsigned gx, gy;
+};
+template <class Op, int RP>
+__global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_batch_kernel(BatchTab<PkEntry> t) {
+  const PkEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
+  rowred_pk_body<Op, RP>(e.a, e.sc, e.M, e.N, e.chunk, e.outs, blockIdx.x, blockIdx.y, e.gy);
+}
+template <class Op, int RP>
+int rowred_pk_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<PkEntry>(rowred_pk_batch_kernel<Op, RP>, es, st, "rowred_pk");
 }
 
 template <class Op, int RP>
@@ -360,6 +387,10 @@ int launch_rowred_pk_rp(const char* name, const Args& a, const Scal& sc, int64_t
   const int64_t bx = (M + (int64_t)kBlock * 2 * RP - 1) / ((int64_t)kBlock * 2 * RP);
   dim3 grid((unsigned)bx, (unsigned)S, 1), block(kBlock, 1, 1);
   if (S == 1) {
+    if (batching()) {
+      const int rc = batch_record(rowred_pk_batch_flush<Op, RP>, PkEntry{a, sc, fin, M, N, chunk, grid.x, grid.y});
+      return rc ? rc : check_launch(name);
+    }
     rowred_pk_kernel<Op, RP><<<grid, block, 0, st>>>(a, sc, M, N, chunk, fin);
     return check_launch(name);
   }
@@ -374,8 +405,14 @@ int launch_rowred_pk_rp(const char* name, const Args& a, const Scal& sc, int64_t
     part.ptr[k] = fin.ptr[k] ? cur : nullptr;
     cur += (int64_t)S * M * Base::kOutW[k];
   }
-  rowred_pk_kernel<Op, RP><<<grid, block, 0, st>>>(a, sc, M, N, chunk, part);
-  int rc = check_launch(name);
+  int rc;
+  if (batching()) {
+    rc = batch_record(rowred_pk_batch_flush<Op, RP>, PkEntry{a, sc, part, M, N, chunk, grid.x, grid.y});
+    if (!rc) rc = check_launch(name);
+  } else {
+    rowred_pk_kernel<Op, RP><<<grid, block, 0, st>>>(a, sc, M, N, chunk, part);
+    rc = check_launch(name);
+  }
   if (rc) return rc;
   MergeSet ms;
   int nk = 0;
@@ -390,6 +427,10 @@ int launch_rowred_pk_rp(const char* name, const Args& a, const Scal& sc, int64_t
   }
   if (nk > 0) {
     const int64_t nb = (nmax + kBlock - 1) / kBlock;
+    if (batching()) {
+      rc = batch_record(merge_slabs_batch_flush, MergeEntry{ms, fin, S, (unsigned)nb, (unsigned)nk});
+      return rc ? rc : check_launch(name);
+    }
     merge_slabs_kernel<false><<<dim3((unsigned)nb, (unsigned)nk), dim3(kBlock), 0, st>>>(ms, fin, S);
     rc = check_launch(name);
     if (rc) return rc;

@@ -376,6 +376,27 @@ int dicp_get_option(const char* name, int* value);
 /* Number of column splits the library will use for an M x N pass (diagnostics/bench). */
 int dicp_num_splits(int kind, int64_t M, int64_t N);
 
+/* ----------------------------------------------------------------------------------
+ * Launch batching (no reference counterpart; replaces the per-frame launches of the atlas'
+ * independent frames, PSR.py:528-569, by one grid over all of them).
+ * dicp_batch_begin: from now on, the calling host thread's calls of the dicp_lddmm_ode_self_*
+ * / dicp_lddmm_euler_* entry points validate their arguments and RECORD their kernel launches
+ * (each call with its own arguments, outputs and workspace) instead of issuing them; they return
+ * DICP_OK without touching the device.  The calls of one batch must be independent (no call
+ * reads another's outputs) and their buffers must stay allocated until the batch has run.
+ * dicp_batch_end(stream): issue everything recorded on `stream`, stage by stage (every call's
+ * first launch, then every call's second launch, ...), one batched launch per kernel
+ * instantiation and stage (blockIdx.z = the call, up to 12 calls per launch).  Each call
+ * computes bitwise what it computes alone (same geometry, same order of summation).  Returns
+ * DICP_ERR_UNSUPPORTED, and issues nothing, if a recorded call took a path whose kernels have
+ * no batched form -- the batchable paths are the packed eta = 0 forward passes (fwd_alg 2,
+ * with or without the divergence rows) and the packed symmetric eta = 0 VJPs (bwd_alg 3: full,
+ * zero mG cotangent, gp only, 2 or 4 rows per lane, scaled or raw coordinates) with their
+ * merges.  dicp_batch_abort: discard an open batch.  One open batch per host thread. */
+int dicp_batch_begin(void);
+int dicp_batch_end(dicp_stream_t stream);
+int dicp_batch_abort(void);
+
 #ifdef __cplusplus
 }
 #endif
