@@ -176,7 +176,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "fwd_alg")) {
-    if (value < 0 || value > 4) return DICP_ERR_INVALID;
+    if (value < 0 || value > 5) return DICP_ERR_INVALID;
     g_fwd_alg = value;
     return DICP_OK;
   }
@@ -333,9 +333,9 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   scale_coords(a, sc, sigma);
   const bool raw = tl_coord_raw != 0;   // the packed kernels below; the others stay scaled
   if (zs != nullptr) {
-    // divergence rows out through the (unused) h slot: the packed ordered pass only
-    if (eta != 0.0 || o.ptr[3] != nullptr || (o.ptr[1] != nullptr && g_fwd_alg != 2)) {
-      set_error("ode_self_fwd: divergence rows (zs) need eta = 0, no h output and fwd_alg 2");
+    // divergence rows out through the (unused) h slot: the packed passes only
+    if (eta != 0.0 || o.ptr[3] != nullptr || (o.ptr[1] != nullptr && g_fwd_alg != 2 && g_fwd_alg != 5)) {
+      set_error("ode_self_fwd: divergence rows (zs) need eta = 0, no h output and fwd_alg 2 or 5");
       return DICP_ERR_INVALID;
     }
     Outs oz = o;
@@ -343,6 +343,7 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     oz.base[3] = oz.add[3] = nullptr;
     oz.accumulate[3] = 0;
     oz.alpha[3] = 1.f;
+    if (g_fwd_alg == 5 && all && !raw) return launch_sym_fwd4<D, true>(a, sc, M, oz, ws, wsb, st, true);
     if (o.ptr[1] == nullptr)
       return launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
                                                                            M, oz, ws, wsb, st);
@@ -368,7 +369,10 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     return o.ptr[2] != nullptr
                ? launch_mfma_fwd<D, true>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order)
                : launch_mfma_fwd<D, false>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order);
-  if (g_fwd_alg == 2 || g_fwd_alg == 4)
+  if (g_fwd_alg == 5 && all && !raw)   // symmetric pair-once, 4 rows per lane
+    return o.ptr[2] != nullptr ? launch_sym_fwd4<D, true>(a, sc, M, o, ws, wsb, st, false)
+                               : launch_sym_fwd4<D, false>(a, sc, M, o, ws, wsb, st, false);
+  if (g_fwd_alg == 2 || g_fwd_alg == 4 || g_fwd_alg == 5)
     return o.ptr[2] != nullptr
                ? launch_fwd_pk<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_fwd_pk<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st);

@@ -889,6 +889,123 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   return check_launch("ode_self_fwd(sym merge)");
 }
 
+// ---- the symmetric forward with 4 rows per lane (fwd_alg 5, lddmm_sym_pk.hpp SymFwdPk4) ----
+// Merge: one thread per row sums its slots in slot order (8 loads in flight, the additions
+// sequential) and applies the epilogue to v = V, mG = sa Gs, g = -sa p.Z and either h = p.V / 2
+// or (ZS) the divergence rows zs = Z' / alpha (original units, as OpOdeSelfFwdZs) in the h slot.
+template <int D, bool DIV, bool ZS>
+__device__ __forceinline__ void sym_fwd4_merge_body(const float* __restrict__ slab, int64_t slot_stride,
+                                                    int64_t M, int nG, int L, const float* __restrict__ p,
+                                                    float sa, float ia, const Outs& o, unsigned bx) {
+  constexpr int W = SymFwd<D, DIV>::W;
+  const int64_t i = (int64_t)bx * 256 + threadIdx.x;
+  if (i >= M) return;
+  const int ns = sym_nslots((int)(i / 256), nG, L);
+  float t[W];
+  const float* src = slab + i * W;
+#pragma unroll
+  for (int k = 0; k < W; ++k) t[k] = src[k];
+  int u = 1;
+  for (; u + 4 <= ns; u += 4) {
+    float v[4][W];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < W; ++k) v[c][k] = src[(int64_t)(u + c) * slot_stride + k];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < W; ++k) t[k] += v[c][k];
+  }
+  for (; u < ns; ++u) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) t[k] += src[(int64_t)u * slot_stride + k];
+  }
+  float pv = 0.f, pz = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float pd = p[i * D + d];
+    pv = fmaf(pd, t[d], pv);
+    if (DIV) pz = fmaf(pd, t[2 * D + d], pz);
+    o.ptr[0][i * D + d] = epilogue(o, 0, i * D + d, t[d]);
+    if (o.ptr[1]) o.ptr[1][i * D + d] = epilogue(o, 1, i * D + d, sa * t[D + d]);
+    if (ZS) o.ptr[3][i * D + d] = ia * t[2 * D + d];
+  }
+  if (o.ptr[2]) o.ptr[2][i] = epilogue(o, 2, i, DIV ? -sa * pz : 0.f);
+  if (!ZS && o.ptr[3]) o.ptr[3][i] = epilogue(o, 3, i, 0.5f * pv);
+}
+template <int D, bool DIV, bool ZS>
+__global__ __launch_bounds__(256) void sym_fwd4_merge_kernel(const float* __restrict__ slab, int64_t slot_stride,
+                                                             int64_t M, int nG, int L, const float* __restrict__ p,
+                                                             float sa, float ia, Outs o) {
+  sym_fwd4_merge_body<D, DIV, ZS>(slab, slot_stride, M, nG, L, p, sa, ia, o, blockIdx.x);
+}
+struct SymFwdMergeEntry {
+  const float* slab;
+  int64_t slot_stride, M;
+  int nG, L;
+  const float* p;
+  float sa, ia;
+  Outs o;
+  unsigned gx, gy;
+};
+template <int D, bool DIV, bool ZS>
+__global__ __launch_bounds__(256) void sym_fwd4_merge_batch_kernel(BatchTab<SymFwdMergeEntry> t) {
+  const SymFwdMergeEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx) return;
+  sym_fwd4_merge_body<D, DIV, ZS>(e.slab, e.slot_stride, e.M, e.nG, e.L, e.p, e.sa, e.ia, e.o, blockIdx.x);
+}
+template <int D, bool DIV, bool ZS>
+int sym_fwd4_merge_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<SymFwdMergeEntry>(sym_fwd4_merge_batch_kernel<D, DIV, ZS>, es, st, "sym_fwd4_merge");
+}
+
+template <int D, bool DIV>
+__global__ void sym_fwd_pk4_kernel(Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab,
+                                   int64_t slot_stride);
+template <int D, bool DIV>
+int sym_fwd_pk4_batch_flush(const std::vector<const void*>& es, hipStream_t st);
+
+// zs: the divergence rows out through the h slot (o.ptr[3], M x D), DIV required
+template <int D, bool DIV>
+int launch_sym_fwd4(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                    hipStream_t st, bool zs) {
+  using S = SymFwd<D, DIV>;
+  if (M <= 0) return DICP_OK;
+  const SymGeom g = sym_geom(M, 1, 256);
+  const size_t need = sym_ws_bytes(M, S::W);
+  if (ws == nullptr || wsb < need) {
+    set_error("ode_self_fwd(sym4): workspace too small (%zu < %zu bytes)", wsb, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  if (o.ptr[0] == nullptr || (zs && (!DIV || o.ptr[3] == nullptr))) {
+    set_error("ode_self_fwd(sym4): v is required, zs needs the divergence sums");
+    return DICP_ERR_INVALID;
+  }
+  float* slab = reinterpret_cast<float*>(ws);
+  const int64_t stride = M * S::W;
+  const dim3 grid((unsigned)g.Kmax, (unsigned)g.nQ), mg((unsigned)((M + 255) / 256));
+  const float ia = 1.f / a.scale;
+  if (batching()) {
+    int rc = batch_record(sym_fwd_pk4_batch_flush<D, DIV>,
+                          SymEntry{a, sc, M, g.nG, g.L, slab, stride, 0, 1, grid.x, grid.y});
+    if (!rc) rc = check_launch("ode_self_fwd(sym4)");
+    if (rc) return rc;
+    const SymFwdMergeEntry e{slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o, mg.x, 1u};
+    rc = zs ? batch_record(sym_fwd4_merge_batch_flush<D, DIV, true>, e)
+            : batch_record(sym_fwd4_merge_batch_flush<D, DIV, false>, e);
+    return rc ? rc : check_launch("ode_self_fwd(sym4 merge)");
+  }
+  sym_fwd_pk4_kernel<D, DIV><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride);
+  int rc = check_launch("ode_self_fwd(sym4)");
+  if (rc) return rc;
+  if (zs)
+    sym_fwd4_merge_kernel<D, DIV, true><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
+  else
+    sym_fwd4_merge_kernel<D, DIV, false><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
+  return check_launch("ode_self_fwd(sym4 merge)");
+}
+
 // packed-FP32 rows of the eta != 0 VJP (lddmm_sym_pk.hpp); GQ = false: gp half only, B0: zero
 // cotangent on mG
 template <int D, bool GQ, bool B0>

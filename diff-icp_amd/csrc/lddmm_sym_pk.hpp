@@ -470,9 +470,6 @@ __device__ __forceinline__ void sym_pk_body(Args a, Scal sc, int64_t M, int nG, 
 // the column record and the DPP rotation of the column sums are shared by the 4 rows, and a
 // column group is staged as 256 records (four 64-column quarters).  Slots and merge are those
 // of the 128 form with G = 256 (sym_merge_kernel<..., kSymG4>).
-#ifndef DICP_SYMBWD4_PK_CT
-#define DICP_SYMBWD4_PK_CT 1   // column sums over the 4 rows in packed form (SymBwdPk::pair_sym4)
-#endif
 #ifndef DICP_SYMBWD4_UNROLL
 #define DICP_SYMBWD4_UNROLL 2
 #endif
@@ -578,18 +575,10 @@ __device__ __forceinline__ void sym_pk4_body(Args a, Scal sc, int64_t M, int nG,
           const int col = h * 64 + ((l + k2) & 63);
           float rec[4 * CW + NP];
           ldrec(col, rec);
-#if DICP_SYMBWD4_PK_CT
           float ct[W];
           P::pair_sym4(prm, row[0], row[1], rec, racc[0], racc[1], ct);
 #pragma unroll
           for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
-#else
-          float ct0[W], ct1[W];   // each row pair's column sums in scalar form, then added
-          P::pair_sym(prm, row[0], rec, racc[0], ct0);
-          P::pair_sym(prm, row[1], rec, racc[1], ct1);
-#pragma unroll
-          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + (ct0[k] + ct1[k]);
-#endif
         }
 #pragma unroll
         for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
@@ -893,6 +882,107 @@ struct SymFwdPk {
     }
   }
 };
+
+// The symmetric eta = 0 forward with 4 rows per lane (sym_pk4_body; fwd_alg 5): per unordered
+// pair the row side of each row pair as SymFwdPk, and the column side of the 4 rows (K p_i,
+// -Kpp z, -K z) chained over the two row pairs in packed form, so that only one scalar add per
+// accumulator (and one DPP rotation, shared by the 4 rows) remains per column: per step 56 v_pk
+// + 9 adds + 9 DPP + 4 exp for 8 ordered pair-equivalents, against 76 v_pk + 8 exp of the
+// ordered 4-row forward.  D = 3 records as planes [q (3) | q_z] [p (3) | p_z] (z components as
+// aligned register pairs, as SymBwdPk).
+template <int D, bool DIV>
+struct SymFwdPk4 {
+  using S = SymFwd<D, DIV>;
+  static constexpr int W = S::W;
+  static constexpr bool kRec3 = D == 3;
+  static constexpr int kPlanes = kRec3 ? 2 : S::CW;
+  static constexpr bool kDupW = kRec3;
+  __host__ __device__ static constexpr int slot(int i) { return kRec3 ? (i / 3) * 4 + i % 3 : i; }
+  struct Prm {};
+  __device__ static Prm params(const Args&, const Scal&) { return Prm{}; }
+  using Row2 = typename SymFwdPk<D, DIV>::Row2;
+  __device__ static void pack(const typename S::Row& r0, const typename S::Row& r1, Row2& r) {
+    SymFwdPk<D, DIV>::pack(r0, r1, r);
+  }
+  __device__ static void colvec(const float* rec, f2* cv) {
+#pragma unroll
+    for (int i = 0; i < 2 * D; ++i) cv[i] = splat(rec[i]);
+    if constexpr (kDupW) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) cv[3 * m + 2] = f2{rec[3 * m + 2], rec[4 * S::CW + m]};
+    }
+  }
+  struct Sh {
+    f2 z[D];
+    f2 K, Kpp;
+  };
+  __device__ static void shared(const Row2& r, const f2* cv, Sh& t) {
+    f2 r2 = splat(0.f);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      t.z[d] = r.q[d] - cv[d];
+      r2 = pk_fma(t.z[d], t.z[d], r2);
+    }
+    t.K = f2{fast_exp2(-r2.x), fast_exp2(-r2.y)};
+    f2 pp = r.p[0] * cv[D];
+#pragma unroll
+    for (int d = 1; d < D; ++d) pp = pk_fma(r.p[d], cv[D + d], pp);
+    t.Kpp = t.K * pp;
+  }
+  __device__ static void row_side(const Sh& t, const f2* cv, f2* acc) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[d] = pk_fma(t.K, cv[D + d], acc[d]);
+      acc[D + d] = pk_fma(t.Kpp, t.z[d], acc[D + d]);
+      if (DIV) acc[2 * D + d] = pk_fma(t.K, t.z[d], acc[2 * D + d]);
+    }
+  }
+  __device__ static void pair_row(const Prm&, const Row2& r, const float* rec, f2* acc) {
+    f2 cv[2 * D];
+    colvec(rec, cv);
+    Sh t;
+    shared(r, cv, t);
+    row_side(t, cv, acc);
+  }
+  __device__ static void pair_sym4(const Prm&, const Row2& r0, const Row2& r1, const float* rec, f2* acc0,
+                                   f2* acc1, float* ct) {
+    f2 cv[2 * D];
+    colvec(rec, cv);
+    Sh t0, t1;
+    shared(r0, cv, t0);
+    shared(r1, cv, t1);
+    row_side(t0, cv, acc0);
+    row_side(t1, cv, acc1);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      // column j's side over the 4 rows, (i, j) -> (j, i) flips z
+      const f2 cV = pk_fma(t1.K, r1.p[d], t0.K * r0.p[d]);
+      ct[d] = cV.x + cV.y;
+      const f2 cG = pk_fma(t1.Kpp, t1.z[d], t0.Kpp * t0.z[d]);
+      ct[D + d] = -(cG.x + cG.y);
+      if (DIV) {
+        const f2 cZ = pk_fma(t1.K, t1.z[d], t0.K * t0.z[d]);
+        ct[2 * D + d] = -(cZ.x + cZ.y);
+      }
+    }
+  }
+};
+
+template <int D, bool DIV>
+__global__ __launch_bounds__(256) void sym_fwd_pk4_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+                                                          float* __restrict__ slab, int64_t slot_stride) {
+  sym_pk4_body<SymFwdPk4<D, DIV>>(a, sc, M, nG, L, slab, slot_stride, 0, 1, blockIdx.x, blockIdx.y);
+}
+template <int D, bool DIV>
+__global__ __launch_bounds__(256) void sym_fwd_pk4_batch_kernel(BatchTab<SymEntry> t) {
+  const SymEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
+  sym_pk4_body<SymFwdPk4<D, DIV>>(e.a, e.sc, e.M, e.nG, e.L, e.slab, e.slot_stride, 0, 1, blockIdx.x, blockIdx.y);
+}
+template <int D, bool DIV>
+int sym_fwd_pk4_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<SymEntry>(sym_fwd_pk4_batch_kernel<D, DIV>, es, st, "sym_fwd_pk4");
+}
 
 template <int D, bool DIV>
 __global__ __launch_bounds__(256) void sym_fwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L,

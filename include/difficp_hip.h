@@ -355,6 +355,9 @@ int dicp_supports_dim(int D);
  *   "pk_rp"        packed row passes: row pairs per thread, 0 automatic (2 for the eta = 0 fused
  *                  forward and the packed external-point / KRed passes from 32k rows and 8k
  *                  columns, else 1), 1 or 2 forced
+ *   "sym_rp"       packed symmetric eta = 0 VJP: row pairs per lane, 0 automatic (2, i.e. 4 rows
+ *                  in 256-point groups, from 64k points when a launch or row-split part has
+ *                  >= 2e9 pairs; else 1), 1 or 2 forced
  *   "red_alg"      KBase / KRedScal / KRed / GradKRed and the external-point forward: 0 never
  *                  the centred expansion, 1 automatic by size (default), 2 always
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)

@@ -219,3 +219,55 @@ def test_vjp_rows_automatic_rule(dev):
             with _srp(rp):
                 res[rp] = L.ode_self_bwd(qf, pf, a, a, None, SIG, 0.0)
         assert torch.equal(res[0][0], res[want][0]) and torch.equal(res[0][1], res[want][1]), M
+
+
+# --- the symmetric pair-once forward with 4 rows per lane (fwd_alg 5, SymFwdPk4) ---
+
+class _falg(_rp):
+    def __enter__(self):
+        L = _lib()
+        self.old = L.get_option("fwd_alg")
+        L.set_option("fwd_alg", self.v)
+
+    def __exit__(self, *a):
+        _lib().set_option("fwd_alg", self.old)
+
+
+@pytest.mark.parametrize("M,D", [(1, 3), (257, 3), (1023, 2), (1025, 3), (5000, 3), (33001, 3), (70001, 3)])
+def test_forward_sym4_vs_ordered(dev, M, D):
+    """fwd_alg 5 (each unordered pair once, 4 rows per lane, column sums rotated by DPP) against
+    the packed ordered forward (fwd_alg 2) for every forward form the shooting runs -- plain,
+    with the Hamiltonian rows, the Euler step writing the divergence rows, the mG-less last step
+    -- within fp32 summation order (2e-6; the divergence rows 1e-5), bitwise run to run, and
+    against the fp64 oracle's ODE (2e-5)."""
+    L = _lib()
+    q, p = _case(M, D, 3 * M + D)
+    qf, pf = q.float().to(dev), p.float().to(dev)
+    outs = {}
+    for alg in (2, 5, 5):
+        with _falg(alg):
+            zs = torch.empty(M, D, device=dev)
+            o = {"fwd": L.ode_self_fwd(qf, pf, SIG, 0.0, True),
+                 "fwd_h": L.ode_self_fwd(qf, pf, SIG, 0.0, True, want_h=True),
+                 "step_zs": L.euler_step(qf, pf, SIG, 0.0, 0.1, True, zs_out=zs) + (zs,),
+                 "step_nog": L.euler_step(qf, pf, SIG, 0.0, 0.1, True, want_p=False)}
+            torch.cuda.synchronize()
+            if alg in outs:
+                for k in o:
+                    for a, b in zip(o[k], outs[alg][k]):
+                        assert (a is None and b is None) or torch.equal(a, b), k
+            outs[alg] = o
+    for k in outs[2]:
+        for i, (a, b) in enumerate(zip(outs[5][k], outs[2][k])):
+            if a is None or b is None:
+                assert a is None and b is None, k
+                continue
+            tol = 1e-5 if (k == "step_zs" and i == 3) else 2e-6
+            assert rel_err(a.cpu(), b.cpu()) < tol, (k, i, rel_err(a.cpu(), b.cpu()))
+    if M > 5000:
+        return
+    m = R.LDDMM(SIG, D, 50.0, False, True)
+    v64, mG64, c64 = m.ODE(q, p, torch.zeros(1, dtype=torch.float64))
+    v, mG, g, h = outs[5]["fwd_h"]
+    assert rel_err(v.cpu(), v64) < 2e-5 and rel_err(mG.cpu(), mG64) < 2e-5
+    assert abs(float(g.double().sum().cpu() - c64.sum())) <= 2e-5 * max(1.0, float(c64.abs().sum()))

@@ -1,0 +1,52 @@
+"""The column groups per workgroup (dicp_set_option "sym_L") of the 4-row symmetric VJP at the
+sizes where it runs: automatic vs forced 2 / 4 / 8, adjoint step with divergence rows and the
+gp-only step, alternating in one process (HIP events).
+
+    SIZES=100000,200000 python tools/probes/sym_L_rows4.py
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.getcwd())
+from difficp_amd import _lib  # noqa: E402
+
+dev = torch.device("cuda:0")
+st = torch.cuda.current_stream()
+
+
+def timeit(fn, reps):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        fn()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+for M in [int(v) for v in os.environ.get("SIZES", "100000,200000").split(",")]:
+    g = torch.Generator().manual_seed(M)
+    q = torch.rand(M, 3, generator=g).to(dev)
+    p = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
+    ga = torch.randn(M, 3, generator=g).to(dev)
+    gb = torch.randn(M, 3, generator=g).to(dev)
+    gd = torch.ones(1, device=dev)
+    zs = torch.empty_like(q)
+    _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs)
+    fns = {"adj_zs": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs),
+           "adj_gp": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, want_lq=False, zs=zs)}
+    reps = max(2, int(2e10 / (M * M)))
+    row = {"M": M}
+    for name, fn in fns.items():
+        best = {}
+        for _ in range(3):
+            for L in (0, 2, 4, 8):
+                _lib.set_option("sym_L", L)
+                best[L] = min(best.get(L, 1e9), timeit(fn, reps))
+        _lib.set_option("sym_L", 0)
+        row[name] = {f"L{L}" if L else "auto": round(v, 4) for L, v in best.items()}
+    print(json.dumps(row), flush=True)
