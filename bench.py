@@ -336,6 +336,10 @@ def _main(out):
                     help="atlas workloads: the local frames' shooting launches in lockstep batches "
                          "(core/batching.py; auto = whenever the path allows), --concurrent-frames "
                          "groups of them on their own HIP streams")
+    ap.add_argument("--batch-share", type=int, default=1,
+                    help="atlas lockstep batches: kernel geometry per frame sized as if alone (1, "
+                         "results bitwise the sequential frame loop's) or for the frame's share of "
+                         "the chip (0 = the frames per group)")
     ap.add_argument("--lib-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="dicp_set_option before the run (A/B experiments; repeatable)")
     ap.add_argument("--replicas", action="store_true",
@@ -398,13 +402,14 @@ def _main(out):
         psr = workloads.build_atlas(K, wl["N"], wl["C"], dev, comm=comm, seed=0, S=wl["S"])
         psr.concurrent_frames = args.concurrent_frames
         psr.batch_frames = {"auto": None, "on": True, "off": False}[args.batch_frames]
+        psr.batch_share = args.batch_share
         cfg = {"workload": f"groupwise atlas {K} frames x {wl['S']} structures x {wl['N']} 3D points, "
                            f"C={wl['C']} per structure" + (" (BASELINE configs[3], fixed)" if fixed else ""),
                "frames_per_rank": (f"{K // world}-{-(-K // world)}" if fixed else wl["K_per_rank"]),
                "lddmm": "hybrid sigma=0.1 lambda=1e3 Euler nt=10 dense", "max_repeat_GMM": 10,
                "tol": 1e-3, "parallelism": f"frame-sharded dp{world} (RCCL suff-stat exchange)",
                "concurrent_frames": args.concurrent_frames or "auto",
-               "batch_frames": args.batch_frames}
+               "batch_frames": args.batch_frames, "batch_share": args.batch_share}
         scaling = "strong" if fixed else "weak"
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s")

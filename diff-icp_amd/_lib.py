@@ -152,23 +152,40 @@ def _zs_buf(zs, rows, D, dev, name="zs_out"):
     return zs
 
 
-class coord_mode:
-    """Context manager: the packed shooting kernels in original-unit coordinates (raw=True) or
-    in scaled ones (library option coord_raw, per host thread; DESIGN.md section 5)."""
+class thread_option:
+    """Context manager setting a per-host-thread library knob (_PER_THREAD) for a block."""
 
-    def __init__(self, raw: bool):
-        self.raw = int(bool(raw))
+    name = None
+
+    def __init__(self, value: int, name: str = None):
+        self.value = int(value)
+        if name is not None:
+            self.name = name
 
     def __enter__(self):
-        self.old = get_option("coord_raw")
-        if self.old != self.raw:
-            set_option("coord_raw", self.raw)
+        self.old = get_option(self.name)
+        if self.old != self.value:
+            set_option(self.name, self.value)
         return self
 
     def __exit__(self, *exc):
-        if self.old != self.raw:
-            set_option("coord_raw", self.old)
+        if self.old != self.value:
+            set_option(self.name, self.old)
 
+
+class coord_mode(thread_option):
+    """Context manager: the packed shooting kernels in original-unit coordinates (raw=True) or
+    in scaled ones (library option coord_raw, per host thread; DESIGN.md section 5)."""
+
+    name = "coord_raw"
+
+    def __init__(self, raw: bool):
+        super().__init__(int(bool(raw)))
+        self.raw = self.value
+
+
+# per-host-thread knobs (keyed separately by their users; workspace sizes never depend on them)
+_PER_THREAD = frozenset({"coord_raw", "batch_share"})
 
 # bumped by every set_option of a process-wide knob: a kernel-variant change (fwd_alg,
 # bwd_alg, pk_rp, split rounds, ...) makes results computed before it not bitwise what a
@@ -183,7 +200,7 @@ def option_epoch() -> int:
 def set_option(name: str, value: int):
     """Tuning knob (see include/difficp_hip.h dicp_set_option)."""
     _check_rc(lib().dicp_set_option(name.encode(), int(value)), f"set_option({name})")
-    if name != "coord_raw":     # every other knob may change a workspace size
+    if name not in _PER_THREAD:     # every process-wide knob may change a workspace size
         _WS_BYTES.clear()
         _OPTION_EPOCH[0] += 1
 

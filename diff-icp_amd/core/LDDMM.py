@@ -321,8 +321,21 @@ class LDDMMModel:
             last_eval["p1_missing"] = getattr(shoot, "p1_missing", False)
             return self.trajloss(shoot) + dataloss(last)
 
+        lossgrad = None
+        if getattr(_lib._tl, "batcher", None) is not None and not is_x:
+            # a frame of a lockstep launch batch (core/batching.py): the shooting's adjoint must
+            # run on this thread (autograd would run it on the engine's device thread, every
+            # frame in turn), so the closure forms loss and gradient directly -- bitwise the
+            # values of lossfunc(p0).backward()
+            from .shooting import shoot_loss_grad
+
+            def lossgrad(p0):
+                L, g, shoot = shoot_loss_grad(self, dataloss, q0, p0)
+                last_eval["p0"], last_eval["shoot"] = p0.detach().clone(), shoot
+                last_eval["p1_missing"] = getattr(shoot, "p1_missing", False)
+                return L, [g]
         p0, _, nsteps, change = LBFGS_optimization([p0], lossfunc, nmax=nmax, tol=tol,
-                                                   errthresh=errthresh)
+                                                   errthresh=errthresh, lossgrad=lossgrad)
         p0 = p0[0]
         with torch.no_grad():
             # final shoot (LDDMM.py:390): the kernels are deterministic, so when L-BFGS's

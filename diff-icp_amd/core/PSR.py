@@ -240,6 +240,9 @@ class DiffPSR(MultiPSR):
         self.a0 = [None] * self.K
         self.concurrent_frames = None   # Reg_opt host threads / HIP streams (None = automatic)
         self.batch_frames = None        # Reg_opt lockstep launch batches (None = automatic)
+        # the frames' kernel geometry in a batch: 1 = each launch sized as if alone (results
+        # bitwise the sequential loop's), 0 = for its share of the chip (the group size)
+        self.batch_share = 1
         self.initialize_a0()
 
     def initialize_a0(self, **v2p_args):
@@ -390,9 +393,12 @@ class DiffPSR(MultiPSR):
             batchers.append(b)
         owner = {k: batchers[i] for i, g in enumerate(groups) for k in g}
 
+        share = int(getattr(self, "batch_share", 1))
+        share = per if share == 0 else max(1, share)     # 0 = the group size
+
         def work(k):
             b = owner[k]
-            with frame_thread(b, k):
+            with frame_thread(b, k, share):
                 out = self._optimize_frame(k, nmax, tol)
             b.stream.synchronize()       # results are consumed on `main` afterwards
             return k, out

@@ -4,14 +4,17 @@ The atlas optimises every frame's LDDMM registration independently (one L-BFGS r
 ~20k points a frame's pair kernels are too small to keep the chip busy to the end of each
 launch, and the frames' host work (L-BFGS logic, launches) is serialised by the GIL.  A
 LaunchBatcher runs the frames of a group in lockstep at the level of the library's launches:
-each frame keeps its own host thread and its own, unchanged code path (Optimize, ShootFn, the
+each frame keeps its own host thread and its own code path (Optimize, ShootFn's forward and
 exact adjoint, CompactLBFGS), but its batchable launches (the packed eta = 0 shooting passes,
 _lib.BATCHABLE) are handed to the batcher, which waits until every running frame of the group
 has posted one, then records them all inside ONE dicp_batch_begin / dicp_batch_end scope (the
 C-ABI issues one grid over all the frames per kernel instantiation and stage) and releases
 the frames.  Each recorded call keeps its own arguments, geometry and workspace, so every
 frame's results are bitwise those of the sequential frame loop; only the launch count and the
-tails change.
+tails change.  One change of route is needed for that: autograd runs every CUDA backward on
+its engine's device thread, one frame after another, so under a batcher Optimize's closure
+forms the loss gradient with ShootFn's adjoint called on the frame's own thread
+(shooting.shoot_loss_grad: the same cotangents, hence the same bits).
 
 Deadlock freedom: a frame waits only inside submit(); the batch fires as soon as every frame
 still registered is waiting there, and a frame that finishes (or fails) unregisters, which
@@ -54,7 +57,8 @@ class LaunchBatcher:
     # ---- the per-launch barrier (called by _lib._launch on a frame thread) ----
     def submit(self, name, pairs, nbytes, fn):
         slot = {"key": getattr(_lib._tl, "frame_key", 0), "name": name, "pairs": int(pairs),
-                "nbytes": int(nbytes), "fn": fn, "raw": _lib.get_option("coord_raw"), "done": False}
+                "nbytes": int(nbytes), "fn": fn, "raw": _lib.get_option("coord_raw"),
+                "share": _lib.get_option("batch_share"), "done": False}
         with self._cv:
             self._pending.append(slot)
             if len(self._pending) >= self._active:
@@ -76,7 +80,8 @@ class LaunchBatcher:
             e0 = e1 = None
             with _lib.batch(handle):
                 for s in items:
-                    with _lib.coord_mode(s["raw"]):
+                    # the submitting frame's per-thread knobs (coordinates, geometry hint)
+                    with _lib.coord_mode(s["raw"]), _lib.thread_option(s["share"], "batch_share"):
                         r = s["fn"]()
                     if r:
                         raise RuntimeError(f"dicp batch: recording {s['name']} failed: "
@@ -114,14 +119,19 @@ class LaunchBatcher:
 class frame_thread:
     """Context manager run by a frame's host thread: its batchable launches go through
     `batcher` (keyed by `key` for a deterministic order inside a batch) on the batcher's
-    stream; on exit the frame leaves the group (its registration was made up front)."""
+    stream; on exit the frame leaves the group (its registration was made up front).
+    share > 1: the library's geometry hint "batch_share" for this thread (each launch sized
+    for 1/share of the chip, csrc/batch.hpp) -- fixed for the whole run of the frame, so its
+    results do not depend on how the batches happen to be composed."""
 
-    def __init__(self, batcher: LaunchBatcher, key: int):
-        self.batcher, self.key = batcher, key
+    def __init__(self, batcher: LaunchBatcher, key: int, share: int = 1):
+        self.batcher, self.key, self.share = batcher, key, int(share)
 
     def __enter__(self):
         _lib._tl.batcher = self.batcher
         _lib._tl.frame_key = self.key
+        self._opt = _lib.thread_option(self.share, "batch_share")
+        self._opt.__enter__()
         self._st = torch.cuda.stream(self.batcher.stream)
         self._st.__enter__()
         return self
@@ -129,6 +139,7 @@ class frame_thread:
     def __exit__(self, *exc):
         try:
             self._st.__exit__(*exc)
+            self._opt.__exit__(*exc)
         finally:
             _lib._tl.batcher = None
             self.batcher.unregister()

@@ -323,7 +323,7 @@ class ShootFn(torch.autograd.Function):
         # cached trajectory would not be bitwise what the new variant computes)
         params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
                   None if split is None else (split.rank, split.world), skip, use_zs, ctx.raw,
-                  _lib.option_epoch())
+                  _lib.option_epoch(), _lib.get_option("batch_share"))
         hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
         if hit is not None:
             ctx.split = split if (split is not None and not has_x and scheme == "Euler"
@@ -644,6 +644,60 @@ class ShootFn(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             lq = None
         return lq, lp, (lx if has_x else None), None, None, None, None, None, None, None, None, None, None
+
+
+class ManualCtx:
+    """Stand-in for the autograd context when ShootFn's forward and backward are called
+    directly on the calling host thread (shoot_loss_grad) -- what autograd would do, minus
+    the engine's device thread, on which every frame's backward would otherwise run in turn."""
+
+    def __init__(self, needs_input_grad):
+        self.needs_input_grad = tuple(needs_input_grad)
+        self._saved = ()
+
+    def set_materialize_grads(self, value):
+        pass
+
+    def save_for_backward(self, *ts):
+        self._saved = ts
+
+    @property
+    def saved_tensors(self):
+        return self._saved
+
+
+def shoot_loss_grad(LM, dataloss, q0, p0):
+    """Optimize's loss at p0 -- trajloss + dataloss(q1) of a need_p1=False Euler shooting
+    (LDDMM.py:318-334, optim.py:41-47) -- and its gradient w.r.t. p0, with ShootFn's forward and
+    exact adjoint run on THIS thread instead of through autograd (whose CUDA backward runs on
+    the engine's device thread): the lockstep frame batches (core/batching.py) need every
+    frame's adjoint launches on the frame's own thread.  The cotangents handed to the adjoint
+    are exactly those autograd would hand it -- zeros but for dL/dq1 in gQ[nt], 1 in gC[nt], lam
+    for H0, none for P -- so loss and gradient are bitwise those of lossfunc(p0).backward().
+    Dense support, Euler, no row split.  Returns (loss (1,), grad_p0, shoot)."""
+    from .LDDMM import Shoot
+    nt = int(LM.nt)
+    ctx = ManualCtx((False, True, False) + (False,) * 10)
+    raw = LM._raw_for(q0)
+    outs = ShootFn.forward(ctx, q0.contiguous(), p0.detach().contiguous(), None, LM.Kernel.sigma,
+                           float(LM.eta), nt, LM.scheme, bool(LM.withlogdet), None,
+                           getattr(LM, "row_orders", None), getattr(LM, "shoot_cache", None), False, raw)
+    Q, P, C, H0 = outs
+    sh = Shoot(Q, P, C, None, H0)
+    sh.p1_missing = skip_p1(False, LM.scheme, False, float(LM.eta), None, nt)
+    if sh.p1_missing:
+        sh.raw, sh.q0_key = raw, q0.contiguous()
+    with torch.enable_grad():
+        q1 = Q[nt].detach().requires_grad_(True)
+        H0r = H0.detach().requires_grad_(True)
+        C1 = C.detach().requires_grad_(True)
+        L = LM.lam * H0r + C1[nt] + dataloss(q1)
+        gq1, gH, gC = torch.autograd.grad(L, (q1, H0r, C1), torch.ones_like(L))
+    gQ = torch.zeros_like(Q)
+    gQ[nt].copy_(gq1)
+    with _lib.coord_mode(raw):
+        grads = ShootFn._backward(ctx, gQ, None, gC, gH)
+    return L.detach(), grads[1], sh
 
 
 class HamiltonianFn(torch.autograd.Function):

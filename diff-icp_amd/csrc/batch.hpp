@@ -53,6 +53,15 @@ struct Recorder {
 
 extern thread_local Recorder* tl_batch;
 
+// PER HOST THREAD geometry hint (dicp_set_option "batch_share", default 1): the number of
+// equal-sized calls a launch shares the device with (the frames of a lockstep batch).  The
+// geometry rules then size each call for 1/share of the chip -- fewer column splits, more
+// column groups per workgroup, the 4-row forms where the BATCH is large enough -- which
+// changes only the fp32 summation order (a call made with the same share alone computes the
+// same bits).  Workspace sizes are always those of share 1 (the largest).
+extern thread_local int tl_batch_share;
+inline int batch_share() { return tl_batch_share > 1 ? tl_batch_share : 1; }
+
 // Entry-point guard: the outermost batchable entry point of a call opens a new lane.
 struct BatchCall {
   BatchCall() {

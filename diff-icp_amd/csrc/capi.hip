@@ -20,6 +20,7 @@ thread_local char g_err[512] = "";
 
 namespace dicp {
 thread_local Recorder* tl_batch = nullptr;
+thread_local int tl_batch_share = 1;
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -38,6 +39,12 @@ extern "C" const char* dicp_version(void) {
 }
 
 extern "C" size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D) {
+  // sized for share 1: the most splits / slots any geometry hint can ask for
+  struct ShareOne {
+    int saved = dicp::tl_batch_share;
+    ShareOne() { dicp::tl_batch_share = 1; }
+    ~ShareOne() { dicp::tl_batch_share = saved; }
+  } one;
   size_t b = 0;
   if (kind == DICP_WS_GRAD)
     b = dicp_grad_ws(M, N, D);

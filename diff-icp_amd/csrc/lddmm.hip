@@ -165,6 +165,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     force_splits() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "batch_share")) {   // PER HOST THREAD geometry hint (batch.hpp)
+    if (value < 1 || value > 4096) return DICP_ERR_INVALID;
+    tl_batch_share = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "sym_rp")) {   // packed eta = 0 VJP: row pairs per lane (1, 2), 0 = automatic
     if (value < 0 || value > 2) return DICP_ERR_INVALID;
     sym_rp() = value;
@@ -232,6 +237,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "force_splits")) { *value = force_splits(); return DICP_OK; }
   if (!strcmp(name, "pk_rp")) { *value = pk_rp_force(); return DICP_OK; }
   if (!strcmp(name, "sym_rp")) { *value = sym_rp(); return DICP_OK; }
+  if (!strcmp(name, "batch_share")) { *value = batch_share(); return DICP_OK; }
   if (!strcmp(name, "fwd_alg")) { *value = g_fwd_alg; return DICP_OK; }
   if (!strcmp(name, "mfma_rmax_x100")) { *value = mfma_rmax_x100(); return DICP_OK; }
   if (!strcmp(name, "bwd_eta_alg")) { *value = g_bwd_eta_alg; return DICP_OK; }

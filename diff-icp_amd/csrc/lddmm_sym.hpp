@@ -71,9 +71,11 @@ inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG) {
   if (L <= 0) {
     // L = 8 where the chip stays full with >= 4096 workgroups (100k points: 9.6k): time
     // within 0.3% of L = 4 (r02_ab_vjp_symL_100k.json) and ~25% fewer partial slots written
-    // and merged; otherwise L = 4, halved until a launch has >= 2048 workgroups
-    L = (double)g.nQ * g.nG / (2.0 * 8 * nparts) >= 4096.0 ? 8 : 4;
-    while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0) L /= 2;
+    // and merged; otherwise L = 4, halved until a launch has >= 2048 workgroups (the
+    // workgroup targets are this call's share of the chip: batch_share, batch.hpp)
+    const double sh = (double)batch_share();
+    L = (double)g.nQ * g.nG / (2.0 * 8 * nparts) >= 4096.0 / sh ? 8 : 4;
+    while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0 / sh) L /= 2;
   }
   g.L = L;
   g.Kmax = (g.nG + g.L - 1) / g.L;
@@ -1100,6 +1102,8 @@ inline int& sym_rp() {
 inline bool sym_use_rows4(int64_t M, int nparts) {
   if (sym_rp() == 1) return false;
   if (sym_rp() == 2) return true;
+  if (batch_share() > 1)   // a batch of calls: its total pairs decide (256-point groups kept full)
+    return M >= 8192 && (double)M * (double)M * batch_share() / (double)nparts >= DICP_SYM_ROWS4_MIN_PAIRS;
   return M >= DICP_SYM_ROWS4_MIN_M && (double)M * (double)M / (double)nparts >= DICP_SYM_ROWS4_MIN_PAIRS;
 }
 template <int D, bool GQ, bool B0, bool GT, bool RAW>

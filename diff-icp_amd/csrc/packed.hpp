@@ -197,7 +197,9 @@ constexpr int kPkRPMax = DICP_PK_RP_EXTRA ? 4 : 2;
 template <class Op>
 int pk_rp(int64_t M, int64_t N) {
   if (pk_rp_force() > 0) return pk_rp_force() > kPkRPMax ? kPkRPMax : pk_rp_force();
-  return (pk_rp_pref<Op>::value >= 2 && M >= DICP_PK_RP2_ROWS && N >= DICP_PK_RP2_COLS) ? 2 : 1;
+  // batch_share: the rows of the whole batch decide (the tail the 4-row form leaves is the
+  // batch's, not the call's)
+  return (pk_rp_pref<Op>::value >= 2 && M * batch_share() >= DICP_PK_RP2_ROWS && N >= DICP_PK_RP2_COLS) ? 2 : 1;
 }
 
 // The body of rowred_pk_kernel for block (bx, by) of a grid with S column splits (by < S;
@@ -367,6 +369,7 @@ int rowred_pk_splits(int64_t M, int64_t N) {
     case 2: cap = rowred_pk_capacity<SOp, 2>(); break;
     default: cap = rowred_pk_capacity<SOp, 1>(); break;
   }
+  cap = cap / batch_share() > 0 ? cap / batch_share() : 1;   // this call's share of the chip
   return num_splits_cap(M, N, 2 * RP, cap, round_rows_of<Base>::rows, round_rows_of<Base>::max);
 }
 

@@ -15,7 +15,7 @@ from .lbfgs import CompactLBFGS
 FALLBACK_SEED = 0x5EED
 
 
-def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator=None):
+def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator=None, lossgrad=None):
     """Returns (best_p list, best_L, nsteps, change) exactly as optim.py:10-110:
     L-BFGS(max_iter=20, max_eval=100, history_size=100, strong_wolfe) steps; on NaN /
     increase / > errthresh fall back to the best parameters seen (or a 1% random
@@ -26,7 +26,11 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator
     by default a dedicated one seeded with FALLBACK_SEED at the first fallback of this call:
     the result then does not depend on the global RNG state, ranks of a row split (which must
     stay in lockstep) draw the same numbers, and concurrent frames (one host thread each)
-    do not race on a shared generator."""
+    do not race on a shared generator.
+
+    lossgrad (extension): optional callable p -> (loss, [dL/dp]) computing the same loss and
+    gradient as lossfunc(*p).backward() without autograd's engine (core/shooting.py
+    shoot_loss_grad, used by the lockstep frame batches); the closure then sets p.grad itself."""
     p = [a.clone().contiguous().detach().requires_grad_(True) for a in p0]
     optimizer = CompactLBFGS(p, max_iter=20, max_eval=100, history_size=100,
                              line_search_fn="strong_wolfe")
@@ -35,6 +39,11 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator
 
     def closure():
         optimizer.zero_grad()
+        if lossgrad is not None:
+            L, grads = lossgrad(*p)
+            for a, g in zip(p, grads):
+                a.grad = g
+            return L
         L = lossfunc(*p)
         # backward is queued BEFORE the host reads the loss (optim.py:41-47 reads it first): the
         # gradient does not depend on the read and p is not modified by backward, so results are

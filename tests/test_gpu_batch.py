@@ -92,23 +92,29 @@ def test_batch_rejects_unbatchable_call(dev):
     assert torch.isfinite(qn2).all()
 
 
-@pytest.mark.parametrize("K,N,groups", [(6, 3000, 2), (5, 2500, 1)])
-def test_atlas_reg_opt_batched_bitwise_sequential(dev, K, N, groups):
+@pytest.mark.parametrize("K,N,groups,share", [(6, 3000, 2, 1), (5, 2500, 1, 1), (6, 20000, 2, 0)])
+def test_atlas_reg_opt_batched_bitwise_sequential(dev, K, N, groups, share):
     """DiffPSR.Reg_opt with the frames in lockstep launch batches == the sequential frame loop
-    (PSR.py:528-569) bitwise: momenta, final trajectories and losses of every frame."""
-    from difficp_amd import workloads
+    (PSR.py:528-569) bitwise: momenta, final trajectories and losses of every frame.
+    share 0: the batched launches sized for the group (geometry hint batch_share = frames per
+    group, csrc/batch.hpp) == the sequential loop run with the same per-thread hint."""
+    from difficp_amd import _lib, workloads
+    per = -(-K // groups)
     res = {}
     for mode in ("seq", "batched"):
         torch.manual_seed(0)
         psr = workloads.build_atlas(K, N, 64, dev, seed=3)
         if mode == "seq":
             psr.concurrent_frames = 1
+            psr.batch_frames = False
         else:
             psr.concurrent_frames = groups
             psr.batch_frames = True
+            psr.batch_share = share
         psr.GMM_opt(max_iterations=3, tol=1e-3)
         FE0 = psr.FE
-        psr.Reg_opt(tol=1e-3, nmax=2)
+        with _lib.thread_option(per if (share == 0 and mode == "seq") else 1, "batch_share"):
+            psr.Reg_opt(tol=1e-3, nmax=2)
         torch.cuda.synchronize()
         res[mode] = ([a.clone() for a in psr.a0], [s.Q.clone() for s in psr.shoot], list(psr.regloss),
                      psr.FE, FE0, getattr(psr, "batch_stats", None))

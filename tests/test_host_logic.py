@@ -470,3 +470,42 @@ def test_grid_support_3d_psr_iterations(fake):
             fes.append(P.FE)
     assert all(b <= a + 1e-6 * abs(a) for a, b in zip(fes[:-1], fes[1:])), fes
     assert len(P.shoot[0][-1]) == 4                  # (q, p, cost, x): data carried as external points
+
+
+@pytest.mark.parametrize("version", ["classic", "hybrid"])
+def test_shoot_loss_grad_bitwise_autograd(fake, version):
+    """shooting.shoot_loss_grad (the lockstep frame batches' closure: ShootFn's forward and
+    adjoint called on the calling thread with the cotangents autograd would pass) gives the
+    loss and dL/dp0 of Optimize's lossfunc(p0).backward() bitwise, and an L-BFGS run through
+    it (Optimize under a LaunchBatcher-like thread state) the same momenta and final shoot."""
+    from difficp_amd import _lib
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.shooting import shoot_loss_grad
+    g = torch.Generator().manual_seed(12)
+    M = 50
+    q0 = torch.rand(M, 2, generator=g)
+    p0 = 0.01 * torch.randn(M, 2, generator=g)
+    tgt = q0 + 0.05 * torch.rand(M, 2, generator=g)
+    dataloss = lambda q: ((q - tgt) ** 2).sum() / 0.02
+    LM = LDDMMModel(sigma=0.3, D=2, lambd=5.0, version=version, scheme="Euler", nt=5, spec=CPU)
+    LM.shoot_cache = None
+    p = p0.clone().requires_grad_(True)
+    sh = LM.Shoot(q0, p, need_p1=False)
+    L = LM.trajloss(sh) + dataloss(sh[-1][0])
+    L.backward()
+    L2, g2, sh2 = shoot_loss_grad(LM, dataloss, q0, p0.clone())
+    assert torch.equal(L.detach(), L2) and torch.equal(p.grad, g2)
+    assert torch.equal(sh.Q.detach(), sh2.Q) and sh2.p1_missing
+    # Optimize with the same-thread closure (what a frame under a LaunchBatcher runs)
+    res = {}
+    for mode in ("autograd", "manual"):
+        LM.shoot_cache = None
+        _lib._tl.batcher = object() if mode == "manual" else None
+        try:
+            pr, shoot, trajl, datal, nsteps, change = LM.Optimize(dataloss, q0, p0.clone(), nmax=3)
+        finally:
+            _lib._tl.batcher = None
+        res[mode] = (pr, shoot.Q, shoot.P, trajl, datal, nsteps)
+    a, b = res["autograd"], res["manual"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3:] == b[3:]
