@@ -1,7 +1,7 @@
 """Headline benchmark: diff-ICP PSR iterations/sec on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-                    [--workload two_set_100k|two_set_50k|two_set_200k|two_set_50k_exact|atlas_c4|atlas_c4_fixed|c5|c5_alt]
+                    [--workload two_set_100k|two_set_100k_2d|two_set_50k|two_set_200k|two_set_50k_exact|atlas_c4|atlas_c4_fixed|c5|c5_alt]
     (N > 1: one rank per GPU over RCCL.  Under torch.distributed.run WORLD_SIZE must equal N;
      started without it, bench.py starts `python -m torch.distributed.run --nproc-per-node N`
      on itself as a child process -- before anything touches the GPU -- and exits with the

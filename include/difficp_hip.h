@@ -345,7 +345,9 @@ int dicp_supports_dim(int D);
  *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
  *                  rows (default), 3 channel contraction on the matrix cores (opt-in; fp32
  *                  error bounded by the rows' spread: pass a spatial row_order), 4 symmetric
- *                  pair-once with packed-FP32 rows;
+ *                  pair-once with packed-FP32 rows, 5 symmetric pair-once with 4 packed rows
+ *                  per lane and packed column sums (whole passes in scaled coordinates; row
+ *                  slices and raw coordinates fall back to 2);
  *                  eta != 0: >= 2 packed-FP32 rows, otherwise ordered scalar rows
  *   "bwd_alg"      eta = 0 VJP: 0 / 1 ordered pair algebras, 2 symmetric pair-once, 3 symmetric
  *                  with packed-FP32 rows (default)
@@ -365,6 +367,11 @@ int dicp_supports_dim(int D);
  *                  units x 100) that takes the MFMA branch; >= 100000 always, 0 never (default 300)
  *   "ext_alg"      KRed and the external-point passes below the centred sizes: 0 generic
  *                  scalar rows, 1 packed-FP32 rows (default)
+ *   "batch_share"  PER HOST THREAD geometry hint, default 1: the number of equal calls a launch
+ *                  shares the device with (the frames of a launch batch); split counts, column
+ *                  groups per workgroup and the 4-row rules are then sized for 1/share of the
+ *                  chip.  Changes only the fp32 summation order; a call made alone with the same
+ *                  share computes the same bits.  Workspace sizes do not depend on it.
  *   "coord_raw"    PER HOST THREAD: 1 runs the default packed shooting kernels (fwd_alg 2,
  *                  bwd_alg 3) in original-unit coordinates -- exact pair differences at any
  *                  cloud extent, one packed multiply more per two pairs; 0 (default) scaled

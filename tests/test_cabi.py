@@ -70,3 +70,27 @@ def test_option_epoch_bumps_on_kernel_variant_change(lib):
     with _lib.coord_mode(True):
         pass
     assert _lib.option_epoch() == e0 + 1
+
+
+def test_batch_scope_host_contract(lib):
+    """dicp_batch_begin / dicp_batch_end / dicp_batch_abort (include/difficp_hip.h), host side
+    only: one open batch per thread, end without begin is an error, an empty batch issues
+    nothing, calls recorded with M = 0 record nothing, abort discards."""
+    import ctypes as C
+    lib.dicp_batch_end.argtypes = [C.c_void_p]
+    lib.dicp_last_error.restype = C.c_char_p
+    assert lib.dicp_batch_end(None) != 0                  # no open batch
+    assert lib.dicp_batch_begin() == 0
+    assert lib.dicp_batch_begin() != 0                    # already open on this thread
+    assert b"already open" in lib.dicp_last_error()
+    # an empty shooting step (M = 0) validates and records nothing
+    f = lib.dicp_lddmm_euler_step_zs_f32
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_double,
+                  C.c_double, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+    assert f(None, None, 0, 0, 0, 3, 0.1, 0.0, 0.1, None, None, None, None, None, None, 0, None) == 0
+    assert lib.dicp_batch_end(None) == 0                  # nothing recorded: nothing issued
+    assert lib.dicp_batch_begin() == 0
+    assert lib.dicp_batch_abort() == 0
+    assert lib.dicp_batch_end(None) != 0                  # the abort closed it
+    assert lib.dicp_batch_abort() == 0                    # no-op without a batch
