@@ -347,6 +347,12 @@ def _launch(name, pairs, nbytes, fn):
     b = getattr(_tl, "batcher", None)
     if b is not None and name in BATCHABLE:
         return b.submit(name, pairs, nbytes, fn)
+    keep = getattr(_tl, "batch_keep", None)
+    if keep is not None:
+        # a batch is open on this thread: the call's launches run at the batch's end, so every
+        # tensor the call captured (inputs, outputs the caller may drop, workspace) must stay
+        # allocated until then -- a freed block could be handed to the next call of the batch
+        keep.append(fn)
     if _prof is None:
         return fn()
     st = torch.cuda.current_stream()

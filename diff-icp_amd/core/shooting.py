@@ -362,9 +362,13 @@ class ShootFn(torch.autograd.Function):
         # per step and exchanged once after the loop (rank-ordered, as the staged path)
         direct = split is not None and M % split.world == 0
         if direct:
+            # the step writes this rank's new q and p rows side by side, ONE all-gather moves
+            # both (W x (2, n_l, D), rank order) and two copies unpack them into Q[t+1], P[t+1]
+            # -- one collective per forward step instead of two (latency-bound at large W)
             n_l = M // split.world
-            qs_l = torch.empty((n_l, D), device=dev, dtype=q0.dtype)
-            ps_l = torch.empty((n_l, D), device=dev, dtype=q0.dtype)
+            qp_l = torch.empty((2, n_l, D), device=dev, dtype=q0.dtype)
+            qs_l, ps_l = qp_l[0], qp_l[1]
+            qp_all = torch.empty((split.world, 2, n_l, D), device=dev, dtype=q0.dtype)
             dloc = torch.zeros(nt, device=dev, dtype=q0.dtype)
         for t in range(nt):
             q, p = Q[t], P[t]
@@ -377,11 +381,13 @@ class ShootFn(torch.autograd.Function):
                                                  p_out=None if last_skip else ps_l, order=order_l,
                                                  want_p=not last_skip,
                                                  zs_out=None if Zs is None else Zs[t])
-                split.gather_into(Q[t + 1], qs_l)
                 if last_skip:
+                    split.gather_into(Q[t + 1], qs_l)
                     P[t + 1].fill_(float("nan"))   # not formed: make any read loud
                 else:
-                    split.gather_into(P[t + 1], ps_l)
+                    split.gather_into(qp_all, qp_l)
+                    Q[t + 1].view(split.world, n_l, D).copy_(qp_all[:, 0])
+                    P[t + 1].view(split.world, n_l, D).copy_(qp_all[:, 1])
                 if g_l is not None:
                     torch.sum(g_l, 0, keepdim=True, out=dloc[t:t + 1])
                 continue

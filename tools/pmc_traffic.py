@@ -16,7 +16,8 @@ import os
 import sys
 
 NAMES = {"sym_fwd_pk_kernel": "ode_self_fwd_sym", "sym_fwd_kernel": "ode_self_fwd_sym",
-         "sym_bwd_pk_kernel": "ode_self_bwd", "sym_bwd_kernel": "ode_self_bwd", "sym_merge_kernel": "sym_merge",
+         "sym_fwd_pk4_kernel": "ode_self_fwd_sym4", "sym_fwd4_merge": "sym_fwd_merge",
+         "sym_bwd_pk4_kernel": "ode_self_bwd", "sym_bwd_pk_kernel": "ode_self_bwd", "sym_bwd_kernel": "ode_self_bwd", "sym_merge_kernel": "sym_merge",
          "OpOdeSelfBwd": "ode_self_bwd_ordered", "OpOdeSelfFwd": "ode_self_fwd",
          "OpGmmE": "gmm_estep", "OpGmmM": "gmm_mstep", "OpGmmTargets": "gmm_targets",
          "merge_slabs": "merge_slabs", "lse_finalize": "lse_finalize",
