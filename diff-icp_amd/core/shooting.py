@@ -305,6 +305,9 @@ class ShootFn(torch.autograd.Function):
         coord_raw, per host thread: set here around the forward's launches and again in the
         backward, which autograd may run on another thread)."""
         ctx.raw = bool(raw)
+        # the per-thread geometry hint (batch_share) of the forward applies to the backward
+        # too, which autograd may run on another thread
+        ctx.share = _lib.get_option("batch_share")
         with _lib.coord_mode(ctx.raw):
             return ShootFn._forward(ctx, q0, p0, x0, sigma, eta, nt, scheme, want_div, split, orders,
                                     cache, need_p1)
@@ -525,7 +528,7 @@ class ShootFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gQ, gP, gC, *rest):
-        with _lib.coord_mode(ctx.raw):
+        with _lib.coord_mode(ctx.raw), _lib.thread_option(getattr(ctx, "share", 1), "batch_share"):
             return ShootFn._backward(ctx, gQ, gP, gC, *rest)
 
     @staticmethod
@@ -701,7 +704,7 @@ def shoot_loss_grad(LM, dataloss, q0, p0):
         gq1, gH, gC = torch.autograd.grad(L, (q1, H0r, C1), torch.ones_like(L))
     gQ = torch.zeros_like(Q)
     gQ[nt].copy_(gq1)
-    with _lib.coord_mode(raw):
+    with _lib.coord_mode(raw), _lib.thread_option(ctx.share, "batch_share"):
         grads = ShootFn._backward(ctx, gQ, None, gC, gH)
     return L.detach(), grads[1], sh
 
