@@ -403,6 +403,10 @@ size_t ode_self_fwd_rows_ws(int64_t nrows, int64_t M) {
                    fwd_pk_ws<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(nrows, M),
                    mfma_fwd_ws_bytes<D, true>(nrows, M), mfma_fwd_ws_bytes<D, false>(nrows, M)})
     m = v > m ? v : m;
+  if (nrows == M) {   // a whole pass may run the symmetric 4-row forward (fwd_alg 5)
+    const size_t sy = sym_ws_bytes(M, 3 * D);
+    m = sy > m ? sy : m;
+  }
   return m;
 }
 

@@ -247,8 +247,10 @@ def test_forward_sym4_vs_ordered(dev, M, D):
     for alg in (2, 5, 5):
         with _falg(alg):
             zs = torch.empty(M, D, device=dev)
+            zs0 = torch.empty(M, D, device=dev)
             o = {"fwd": L.ode_self_fwd(qf, pf, SIG, 0.0, True),
                  "fwd_h": L.ode_self_fwd(qf, pf, SIG, 0.0, True, want_h=True),
+                 "first_zs": L.ode_self_fwd(qf, pf, SIG, 0.0, True, zs_out=zs0)[:3] + (zs0,),
                  "step_zs": L.euler_step(qf, pf, SIG, 0.0, 0.1, True, zs_out=zs) + (zs,),
                  "step_nog": L.euler_step(qf, pf, SIG, 0.0, 0.1, True, want_p=False)}
             torch.cuda.synchronize()
@@ -262,7 +264,7 @@ def test_forward_sym4_vs_ordered(dev, M, D):
             if a is None or b is None:
                 assert a is None and b is None, k
                 continue
-            tol = 1e-5 if (k == "step_zs" and i == 3) else 2e-6
+            tol = 1e-5 if (k in ("step_zs", "first_zs") and i == 3) else 2e-6
             assert rel_err(a.cpu(), b.cpu()) < tol, (k, i, rel_err(a.cpu(), b.cpu()))
     if M > 5000:
         return
