@@ -365,7 +365,7 @@ class DiffPSR(MultiPSR):
               and str(self.compspec.get("device", "cpu")).startswith("cuda"))
         if ok:
             from .. import _lib
-            ok = _lib.get_option("fwd_alg") in (2, 5) and _lib.get_option("bwd_alg") == 3
+            ok = _lib.get_option("fwd_alg") in (2, 5, 6) and _lib.get_option("bwd_alg") == 3
         if want is True and not ok:
             raise ValueError("batch_frames=True needs dense support, Euler, eta = 0, fwd_alg 2, "
                              "bwd_alg 3 and >= 2 local frames on a HIP device")

@@ -181,7 +181,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "fwd_alg")) {
-    if (value < 0 || value > 5) return DICP_ERR_INVALID;
+    if (value < 0 || value > 6) return DICP_ERR_INVALID;
     g_fwd_alg = value;
     return DICP_OK;
   }
@@ -323,6 +323,25 @@ extern "C" int dicp_radius_count_f32(const float* x, int64_t M, const float* y, 
 // ---------------------------------------------------------------------------------------
 namespace {
 
+// packed forward algorithms: 2 (default: ordered rows, the symmetric 4-row pass for whole
+// passes from DICP_SYM_FWD4_MIN_M points), 5 (symmetric 4-row wherever it applies), 6 (ordered
+// rows always)
+bool packed_fwd_alg() { return g_fwd_alg == 2 || g_fwd_alg == 5 || g_fwd_alg == 6; }
+#ifndef DICP_SYM_FWD4_MIN_M
+#define DICP_SYM_FWD4_MIN_M 75000
+#endif
+// The symmetric 4-row forward (SymFwdPk4) for this pass?  Whole passes (all rows) in scaled
+// coordinates only.  Automatic rule (fwd_alg 2), measured on MI355X (tools/probes/
+// fwd_sym4_ab.py, profiles/r04_ab_fwd_sym4.jsonl): Euler step with divergence rows 0.95x at
+// 20k, 0.90x at 50k, 1.10x at 100k and 200k -- from 75k points, or, in a launch batch
+// (batch_share > 1), when the batch has >= 2e9 pairs (as the 4-row VJP).
+bool use_sym_fwd4(int64_t M, bool all, bool raw) {
+  if (!all || raw || g_fwd_alg == 6 || !(g_fwd_alg == 2 || g_fwd_alg == 5)) return false;
+  if (g_fwd_alg == 5) return true;
+  if (batch_share() > 1) return M >= 8192 && (double)M * (double)M * batch_share() >= 2.0e9;
+  return M >= DICP_SYM_FWD4_MIN_M;
+}
+
 // rows [row0, row0 + nrows) of the pass against all M columns (row-split over ranks);
 // nrows < 0: all rows.  Output pointers in `o` address the row slice.
 // order: optional nrows int32 row indices (a permutation of the slice's rows) that groups
@@ -340,8 +359,8 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   const bool raw = tl_coord_raw != 0;   // the packed kernels below; the others stay scaled
   if (zs != nullptr) {
     // divergence rows out through the (unused) h slot: the packed passes only
-    if (eta != 0.0 || o.ptr[3] != nullptr || (o.ptr[1] != nullptr && g_fwd_alg != 2 && g_fwd_alg != 5)) {
-      set_error("ode_self_fwd: divergence rows (zs) need eta = 0, no h output and fwd_alg 2 or 5");
+    if (eta != 0.0 || o.ptr[3] != nullptr || (o.ptr[1] != nullptr && !packed_fwd_alg())) {
+      set_error("ode_self_fwd: divergence rows (zs) need eta = 0, no h output and fwd_alg 2, 5 or 6");
       return DICP_ERR_INVALID;
     }
     Outs oz = o;
@@ -349,7 +368,7 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     oz.base[3] = oz.add[3] = nullptr;
     oz.accumulate[3] = 0;
     oz.alpha[3] = 1.f;
-    if (g_fwd_alg == 5 && all && !raw) return launch_sym_fwd4<D, true>(a, sc, M, oz, ws, wsb, st, true);
+    if (use_sym_fwd4(M, all, raw)) return launch_sym_fwd4<D, true>(a, sc, M, oz, ws, wsb, st, true);
     if (o.ptr[1] == nullptr)
       return launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
                                                                            M, oz, ws, wsb, st);
@@ -375,10 +394,10 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     return o.ptr[2] != nullptr
                ? launch_mfma_fwd<D, true>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order)
                : launch_mfma_fwd<D, false>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order);
-  if (g_fwd_alg == 5 && all && !raw)   // symmetric pair-once, 4 rows per lane
+  if (use_sym_fwd4(M, all, raw))   // symmetric pair-once, 4 rows per lane
     return o.ptr[2] != nullptr ? launch_sym_fwd4<D, true>(a, sc, M, o, ws, wsb, st, false)
                                : launch_sym_fwd4<D, false>(a, sc, M, o, ws, wsb, st, false);
-  if (g_fwd_alg == 2 || g_fwd_alg == 4 || g_fwd_alg == 5)
+  if (g_fwd_alg == 2 || g_fwd_alg == 4 || g_fwd_alg == 5 || g_fwd_alg == 6)
     return o.ptr[2] != nullptr
                ? launch_fwd_pk<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
                : launch_fwd_pk<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st);

@@ -343,11 +343,13 @@ int dicp_supports_dim(int D);
 /* Tuning / A-B knobs (process-wide unless stated; results of every setting agree to fp32
  * summation order):
  *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
- *                  rows (default), 3 channel contraction on the matrix cores (opt-in; fp32
- *                  error bounded by the rows' spread: pass a spatial row_order), 4 symmetric
- *                  pair-once with packed-FP32 rows, 5 symmetric pair-once with 4 packed rows
- *                  per lane and packed column sums (whole passes in scaled coordinates; row
- *                  slices and raw coordinates fall back to 2);
+ *                  (default: ordered packed rows, and for whole passes from 75k points -- or a
+ *                  launch batch of >= 2e9 pairs -- the symmetric pass of 5), 3 channel
+ *                  contraction on the matrix cores (opt-in; fp32 error bounded by the rows'
+ *                  spread: pass a spatial row_order), 4 symmetric pair-once with packed-FP32
+ *                  rows, 5 symmetric pair-once with 4 packed rows per lane and packed column
+ *                  sums wherever it applies (whole passes in scaled coordinates; row slices and
+ *                  raw coordinates run the ordered rows), 6 ordered packed rows always;
  *                  eta != 0: >= 2 packed-FP32 rows, otherwise ordered scalar rows
  *   "bwd_alg"      eta = 0 VJP: 0 / 1 ordered pair algebras, 2 symmetric pair-once, 3 symmetric
  *                  with packed-FP32 rows (default)

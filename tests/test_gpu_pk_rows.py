@@ -236,7 +236,7 @@ class _falg(_rp):
 @pytest.mark.parametrize("M,D", [(1, 3), (257, 3), (1023, 2), (1025, 3), (5000, 3), (33001, 3), (70001, 3)])
 def test_forward_sym4_vs_ordered(dev, M, D):
     """fwd_alg 5 (each unordered pair once, 4 rows per lane, column sums rotated by DPP) against
-    the packed ordered forward (fwd_alg 2) for every forward form the shooting runs -- plain,
+    the packed ordered forward (fwd_alg 6) for every forward form the shooting runs -- plain,
     with the Hamiltonian rows, the Euler step writing the divergence rows, the mG-less last step
     -- within fp32 summation order (2e-6; the divergence rows 1e-5), bitwise run to run, and
     against the fp64 oracle's ODE (2e-5)."""
@@ -244,7 +244,7 @@ def test_forward_sym4_vs_ordered(dev, M, D):
     q, p = _case(M, D, 3 * M + D)
     qf, pf = q.float().to(dev), p.float().to(dev)
     outs = {}
-    for alg in (2, 5, 5):
+    for alg in (6, 5, 5):
         with _falg(alg):
             zs = torch.empty(M, D, device=dev)
             zs0 = torch.empty(M, D, device=dev)
@@ -259,8 +259,8 @@ def test_forward_sym4_vs_ordered(dev, M, D):
                     for a, b in zip(o[k], outs[alg][k]):
                         assert (a is None and b is None) or torch.equal(a, b), k
             outs[alg] = o
-    for k in outs[2]:
-        for i, (a, b) in enumerate(zip(outs[5][k], outs[2][k])):
+    for k in outs[6]:
+        for i, (a, b) in enumerate(zip(outs[5][k], outs[6][k])):
             if a is None or b is None:
                 assert a is None and b is None, k
                 continue
@@ -273,3 +273,19 @@ def test_forward_sym4_vs_ordered(dev, M, D):
     v, mG, g, h = outs[5]["fwd_h"]
     assert rel_err(v.cpu(), v64) < 2e-5 and rel_err(mG.cpu(), mG64) < 2e-5
     assert abs(float(g.double().sum().cpu() - c64.sum())) <= 2e-5 * max(1.0, float(c64.abs().sum()))
+
+
+def test_forward_automatic_rule(dev):
+    """fwd_alg 2 (default) runs the ordered rows below 75k points and the symmetric 4-row pass
+    from 75k on (whole passes): bitwise fwd_alg 6 / fwd_alg 5 on each side."""
+    L = _lib()
+    for M, want in ((50000, 6), (100000, 5)):
+        q, p = _case(M, 3, M)
+        qf, pf = q.float().to(dev), p.float().to(dev)
+        res = {}
+        for alg in (2, want):
+            with _falg(alg):
+                zs = torch.empty(M, 3, device=dev)
+                res[alg] = L.euler_step(qf, pf, SIG, 0.0, 0.1, True, zs_out=zs) + (zs,)
+        for a, b in zip(res[2], res[want]):
+            assert torch.equal(a, b), M
