@@ -332,14 +332,14 @@ def _main(out):
     ap.add_argument("--concurrent-frames", type=int, default=None,
                     help="atlas workloads: frames optimised concurrently (host threads / HIP "
                          "streams); default automatic (4), 1 = the reference's sequential loop")
-    ap.add_argument("--batch-frames", choices=["auto", "on", "off"], default="auto",
+    ap.add_argument("--batch-frames", choices=["on", "off"], default="off",
                     help="atlas workloads: the local frames' shooting launches in lockstep batches "
-                         "(core/batching.py; auto = whenever the path allows), --concurrent-frames "
-                         "groups of them on their own HIP streams")
+                         "(core/batching.py, opt-in), --concurrent-frames groups of them on their own "
+                         "HIP streams")
     ap.add_argument("--batch-share", type=int, default=1,
-                    help="atlas lockstep batches: kernel geometry per frame sized as if alone (1, "
-                         "results bitwise the sequential frame loop's) or for the frame's share of "
-                         "the chip (0 = the frames per group)")
+                    help="atlas: kernel geometry per frame sized as if alone (1, results bitwise the "
+                         "sequential frame loop's) or for the frame's share of the chip (0 = the "
+                         "frames per batch group / the concurrent frames)")
     ap.add_argument("--lib-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="dicp_set_option before the run (A/B experiments; repeatable)")
     ap.add_argument("--replicas", action="store_true",
@@ -401,7 +401,7 @@ def _main(out):
         comm = True if world > 1 else None
         psr = workloads.build_atlas(K, wl["N"], wl["C"], dev, comm=comm, seed=0, S=wl["S"])
         psr.concurrent_frames = args.concurrent_frames
-        psr.batch_frames = {"auto": None, "on": True, "off": False}[args.batch_frames]
+        psr.batch_frames = args.batch_frames == "on"
         psr.batch_share = args.batch_share
         cfg = {"workload": f"groupwise atlas {K} frames x {wl['S']} structures x {wl['N']} 3D points, "
                            f"C={wl['C']} per structure" + (" (BASELINE configs[3], fixed)" if fixed else ""),

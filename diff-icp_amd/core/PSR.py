@@ -239,9 +239,10 @@ class DiffPSR(MultiPSR):
         self.q0 = self.allx0
         self.a0 = [None] * self.K
         self.concurrent_frames = None   # Reg_opt host threads / HIP streams (None = automatic)
-        self.batch_frames = None        # Reg_opt lockstep launch batches (None = automatic)
-        # the frames' kernel geometry in a batch: 1 = each launch sized as if alone (results
-        # bitwise the sequential loop's), 0 = for its share of the chip (the group size)
+        self.batch_frames = None        # Reg_opt lockstep launch batches (opt-in: True)
+        # the frames' kernel geometry when several run at once: 1 = each launch sized as if
+        # alone (results bitwise the sequential loop's), 0 = for its share of the chip (the
+        # frames per batch group, or the concurrent frames), n = for 1/n of the chip
         self.batch_share = 1
         self.initialize_a0()
 
@@ -336,12 +337,16 @@ class DiffPSR(MultiPSR):
         lock = threading.Lock()
         free = list(streams)
 
+        from .. import _lib
+        share = int(getattr(self, "batch_share", 1))
+        share = nconc if share == 0 else max(1, share)     # 0 = the concurrent frames
+
         def work(k):
             st = getattr(local, "stream", None)
             if st is None:
                 with lock:
                     st = local.stream = free.pop()
-            with torch.cuda.stream(st):
+            with torch.cuda.stream(st), _lib.thread_option(share, "batch_share"):
                 out = self._optimize_frame(k, nmax, tol)
             st.synchronize()            # results are consumed on `main` afterwards
             return k, out
@@ -351,12 +356,12 @@ class DiffPSR(MultiPSR):
 
     def _batch_frames_ok(self, nframes):
         """Whether Reg_opt runs the local frames in lockstep launch batches (core/batching.py):
-        `batch_frames` True / False, or None (default) = automatically when every frame's
-        shooting takes the batchable path -- dense support (no external points), Euler, the
-        eta = 0 models (classic / hybrid) on the packed kernels (fwd_alg 2, bwd_alg 3) -- on a
-        HIP device with at least 2 local frames."""
+        `batch_frames` True (opt-in; None / False = off), when every frame's shooting takes the
+        batchable path -- dense support (no external points), Euler, the eta = 0 models
+        (classic / hybrid) on the packed kernels (fwd_alg 2/5/6, bwd_alg 3) -- on a HIP device
+        with at least 2 local frames."""
         want = getattr(self, "batch_frames", None)
-        if want is False:
+        if not want:     # opt-in (None = off): measured slower than per-frame streams, DESIGN §6
             return False
         ok = (nframes >= 2 and self.support_scheme is None and self.LMi.scheme == "Euler"
               and self.LMi.eta == 0 and self.LMi.row_split is None
