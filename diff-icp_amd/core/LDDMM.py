@@ -329,8 +329,11 @@ class LDDMMModel:
             # values of lossfunc(p0).backward()
             from .shooting import shoot_loss_grad
 
+            batcher = _lib._tl.batcher
+
             def lossgrad(p0):
-                L, g, shoot = shoot_loss_grad(self, dataloss, q0, p0)
+                with batcher.closure():   # a member of the launch batches while it evaluates
+                    L, g, shoot = shoot_loss_grad(self, dataloss, q0, p0)
                 last_eval["p0"], last_eval["shoot"] = p0.detach().clone(), shoot
                 last_eval["p1_missing"] = getattr(shoot, "p1_missing", False)
                 return L, [g]

@@ -393,9 +393,7 @@ class DiffPSR(MultiPSR):
         for g in groups:
             st = torch.cuda.Stream()
             st.wait_stream(main)
-            b = LaunchBatcher(st)
-            b.register(len(g))     # up front: the first batch waits for every frame
-            batchers.append(b)
+            batchers.append(LaunchBatcher(st))
         owner = {k: batchers[i] for i, g in enumerate(groups) for k in g}
 
         share = int(getattr(self, "batch_share", 1))

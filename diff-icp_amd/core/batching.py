@@ -16,10 +16,11 @@ its engine's device thread, one frame after another, so under a batcher Optimize
 forms the loss gradient with ShootFn's adjoint called on the frame's own thread
 (shooting.shoot_loss_grad: the same cotangents, hence the same bits).
 
-Deadlock freedom: a frame waits only inside submit(); the batch fires as soon as every frame
-still registered is waiting there, and a frame that finishes (or fails) unregisters, which
-fires a batch the others may be waiting for.  A frame doing host work or a device read
-(.item()) will eventually post or finish: the device work it waits for was issued before.
+Deadlock freedom: a frame waits only inside submit(); a batch fires as soon as every member
+(a frame inside a closure, or one whose launch outside a closure is pending) is waiting
+there; a frame inside a closure does no device read (it only launches and queues small torch
+ops), so it will post or leave; leaving (also on an exception) fires a batch the others may be
+waiting for.  Frames between closures (L-BFGS host logic, loss reads) are not waited for.
 """
 from __future__ import annotations
 
@@ -31,40 +32,76 @@ from .. import _lib
 
 
 class LaunchBatcher:
-    """Lockstep launch barrier over the frames (host threads) of one group; see the module
-    docstring.  All frames of a group run on ONE HIP stream (`stream`), so the batched launch
-    is ordered after every frame's previous work and before its next."""
+    """Launch barrier over the frames (host threads) of one group; see the module docstring.
+    All frames of a group run on ONE HIP stream (`stream`), so the batched launch is ordered
+    after every frame's previous work and before its next.
 
-    def __init__(self, stream: torch.cuda.Stream):
+    Members: a frame is waited for only while it is inside a loss/gradient evaluation
+    (`closure()`, Optimize's closures) -- between closures it runs its L-BFGS host logic and
+    the others' batches go on without it -- and, outside closures, while one of its launches
+    is pending.  A batch fires when every member has a launch pending.  With the default
+    geometry (batch_share 1) a call's result does not depend on which calls share its batch,
+    so the timing-dependent composition of the batches changes no result."""
+
+    def __init__(self, stream):
         self.stream = stream
         self._cv = threading.Condition()
-        self._active = 0
+        self._members = 0
         self._pending = []
         self.batches = 0        # statistics: batched flushes and calls recorded
         self.calls = 0
 
-    # ---- frame membership ----
-    def register(self, n: int = 1):
+    # ---- membership: a frame inside a closure ----
+    def enter(self):
         with self._cv:
-            self._active += n
+            self._members += 1
 
-    def unregister(self):
+    def leave(self):
         with self._cv:
-            self._active -= 1
-            if self._pending and len(self._pending) >= self._active:
-                self._flush()
+            self._members -= 1
+            self._maybe_flush()
+
+    class _Closure:
+        def __init__(self, b):
+            self.b = b
+
+        def __enter__(self):
+            self.prev = getattr(_lib._tl, "in_closure", False)
+            _lib._tl.in_closure = True
+            if not self.prev:
+                self.b.enter()
+            return self
+
+        def __exit__(self, *exc):
+            _lib._tl.in_closure = self.prev
+            if not self.prev:
+                self.b.leave()
+            return False
+
+    def closure(self):
+        """Context manager around one loss/gradient evaluation of a frame."""
+        return LaunchBatcher._Closure(self)
+
+    def _maybe_flush(self):
+        if self._pending and len(self._pending) >= self._members:
+            self._flush()
 
     # ---- the per-launch barrier (called by _lib._launch on a frame thread) ----
     def submit(self, name, pairs, nbytes, fn):
         slot = {"key": getattr(_lib._tl, "frame_key", 0), "name": name, "pairs": int(pairs),
                 "nbytes": int(nbytes), "fn": fn, "raw": _lib.get_option("coord_raw"),
                 "share": _lib.get_option("batch_share"), "done": False}
+        transient = not getattr(_lib._tl, "in_closure", False)
         with self._cv:
+            if transient:           # a launch outside a closure: a member until it is issued
+                self._members += 1
             self._pending.append(slot)
-            if len(self._pending) >= self._active:
-                self._flush()
+            self._maybe_flush()
             while not slot["done"]:
                 self._cv.wait()
+            if transient:
+                self._members -= 1
+                self._maybe_flush()
         if slot.get("error") is not None:
             raise slot["error"]
         return slot["rc"]
@@ -119,10 +156,8 @@ class LaunchBatcher:
 class frame_thread:
     """Context manager run by a frame's host thread: its batchable launches go through
     `batcher` (keyed by `key` for a deterministic order inside a batch) on the batcher's
-    stream; on exit the frame leaves the group (its registration was made up front).
-    share > 1: the library's geometry hint "batch_share" for this thread (each launch sized
-    for 1/share of the chip, csrc/batch.hpp) -- fixed for the whole run of the frame, so its
-    results do not depend on how the batches happen to be composed."""
+    stream.  share > 1: the library's geometry hint "batch_share" for this thread (each launch
+    sized for 1/share of the chip, csrc/batch.hpp), fixed for the whole run of the frame."""
 
     def __init__(self, batcher: LaunchBatcher, key: int, share: int = 1):
         self.batcher, self.key, self.share = batcher, key, int(share)
@@ -130,6 +165,7 @@ class frame_thread:
     def __enter__(self):
         _lib._tl.batcher = self.batcher
         _lib._tl.frame_key = self.key
+        _lib._tl.in_closure = False
         self._opt = _lib.thread_option(self.share, "batch_share")
         self._opt.__enter__()
         self._st = torch.cuda.stream(self.batcher.stream)
@@ -142,5 +178,4 @@ class frame_thread:
             self._opt.__exit__(*exc)
         finally:
             _lib._tl.batcher = None
-            self.batcher.unregister()
         return False

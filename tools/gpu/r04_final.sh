@@ -1,6 +1,6 @@
-# round 4, final build: full GPU suite, headline bench (with the CPU baseline), rocprofv3 kernel
-# stats of the same bench command, PMC traffic (FETCH_SIZE / WRITE_SIZE, separate passes) and
-# the SQ/GRBM issue pass, and the secondary workloads
+# round 4, final build (1/2): full GPU suite, headline bench (with the CPU baseline), rocprofv3
+# kernel stats of the same bench command, PMC traffic (FETCH_SIZE / WRITE_SIZE, separate
+# passes), the SQ/GRBM issue pass, and the driver-form headline (20 steps after 5 warmups)
 set -e
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=gpurun_out/r04f
@@ -8,14 +8,11 @@ mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread > $O/gpu_tests.log 2>&1
 tail -2 $O/gpu_tests.log
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err
-tail -c 300 $O/bench.json
+tail -c 200 $O/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 -u bench.py --no-cpu-baseline > $O/bench_rocprof.json 2> $O/bench_rocprof.err
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc -o fetch --output-format csv -- python3 tools/pmc_probe.py > $O/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc -o write --output-format csv -- python3 tools/pmc_probe.py > $O/pmc_write.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY -d $O/pmc_issue -o issue --output-format csv -- python3 tools/pmc_probe.py > $O/pmc_issue.log 2>&1
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_driver_form.json 2> $O/bench_driver_form.err
-for w in two_set_50k two_set_200k two_set_50k_exact two_set_100k_2d atlas_c4 atlas_c4_fixed c5; do
-  timeout -k 10 400 python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_$w.json 2> $O/bench_$w.err
-  tail -c 150 $O/bench_$w.json
-done
+tail -c 200 $O/bench_driver_form.json
 echo done
