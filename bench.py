@@ -483,7 +483,11 @@ def _main(out):
             dom = max(summ, key=lambda k: summ[k]["ms"])
             d = summ[dom]
             avg_s = d["ms"] / d["launches"] * 1e-3
-            flops_per_launch = d["flops"] / d["launches"]
+            Dw = wl.get("D", 3)
+            fpp = _lib.flops_per_pair(dom, Dw)     # the D = 3 table, rescaled for 2D workloads
+            flops_per_launch = d["pairs"] / d["launches"] * fpp if fpp else d["flops"] / d["launches"]
+            # executed-instruction figure: counted from the D = 3 hot loop only
+            efpp = _lib.EXEC_FLOPS_PER_PAIR.get(dom, _lib.FLOPS_PER_PAIR.get(dom)) if Dw == 3 else None
             achieved = flops_per_launch / avg_s / 1e12
             # committed PMC summary: whole-size single-device launches of the default workload
             # (tools/pmc_probe.py); not the pair-subset launches of a row split
@@ -499,12 +503,13 @@ def _main(out):
                     "traffic": traffic, "kernel": dom, "launches": d["launches"],
                     "avg_launch_ms": round(d["ms"] / d["launches"], 4),
                     "pairs_per_launch": d["pairs"] / d["launches"],
-                    "flops_per_pair": _lib.FLOPS_PER_PAIR.get(dom),
-                    "flops_source": "SURVEY.md 8(d) per-unit figure x ordered pairs (M^2)",
-                    "exec_flops_per_pair": _lib.EXEC_FLOPS_PER_PAIR.get(dom, _lib.FLOPS_PER_PAIR.get(dom)),
-                    "frac_executed": round(achieved / FP32_PEAK_TFLOPS *
-                                           _lib.EXEC_FLOPS_PER_PAIR.get(dom, _lib.FLOPS_PER_PAIR.get(dom))
-                                           / _lib.FLOPS_PER_PAIR.get(dom), 4),
+                    "flops_per_pair": round(fpp, 3) if fpp else fpp,
+                    "flops_source": ("SURVEY.md 8(d) per-unit figure x ordered pairs (M^2)" if Dw == 3 else
+                                     f"SURVEY.md 8(d) per-unit figure (D = 3) rescaled to D = {Dw} by the "
+                                     "operator's term count in D (_lib.flops_per_pair) x ordered pairs"),
+                    "exec_flops_per_pair": efpp,
+                    "frac_executed": (round(achieved / FP32_PEAK_TFLOPS * efpp / fpp, 4)
+                                      if efpp and fpp else None),
                     "alg_bytes_per_launch": d["bytes"] / d["launches"],
                     "alg_hbm_GBps": round(d["bytes"] / d["launches"] / avg_s / 1e9, 3),
                     "share_of_step_time": round(d["ms"] / prof_iters * 1e-3 / (elapsed / args.steps), 3),

@@ -301,6 +301,21 @@ FLOPS_PER_PAIR["ode_self_bwd_eta_b0"] = round(120 * 56 / 98)
 FLOPS_PER_PAIR["ode_self_fwd_eta_nog"] = round(70 * 14 / 39)
 
 
+def flops_per_pair(name: str, D: int = 3) -> float:
+    """The algorithmic figure of `name` at dimension D.  The table above is for D = 3; every
+    term of the pair operators is a D-vector operation, counted from SURVEY.md Appendix A
+    (FMA = 2): the fused forward (v, G, g) is 11 D flop per pair (33 at D = 3), KRed 5 D (15),
+    the fused VJP's Appendix A.3 terms 31 D + 2 written out (95 at D = 3, which the table's
+    ~70 prices with shared subexpressions) -- so the VJP family scales by (31 D + 2) / 95 and
+    every other figure by D / 3."""
+    f = FLOPS_PER_PAIR.get(name)
+    if f is None or D == 3:
+        return f
+    if name.startswith("ode_self_bwd"):
+        return f * (31 * D + 2) / 95.0
+    return f * D / 3.0
+
+
 class KernelProfile:
     """Context manager collecting (name, pairs, flops, bytes, start, end[, share]) per launch;
     a batched launch over several calls (LaunchBatcher) is one record per kernel name, whose

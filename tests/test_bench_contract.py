@@ -101,3 +101,13 @@ def test_two_set_2d_workload_is_declared():
     b = _bench()
     wl = b.WORKLOADS["two_set_100k_2d"]
     assert wl["kind"] == "two_set" and wl["D"] == 2 and wl["N"] == 100000
+
+
+def test_flops_per_pair_dimension_scaling():
+    """2D workloads price the pair operators at D = 2 (SURVEY Appendix A term counts)."""
+    from difficp_amd import _lib
+    assert _lib.flops_per_pair("ode_self_bwd", 3) == _lib.FLOPS_PER_PAIR["ode_self_bwd"]
+    assert _lib.flops_per_pair("ode_self_fwd", 2) == pytest.approx(22.0)    # 11 D
+    assert _lib.flops_per_pair("gauss_red", 2) == pytest.approx(10.0)       # 5 D
+    assert _lib.flops_per_pair("ode_self_bwd", 2) == pytest.approx(70 * 64 / 95)
+    assert _lib.flops_per_pair("no_such_kernel", 2) is None

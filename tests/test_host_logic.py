@@ -472,6 +472,15 @@ def test_grid_support_3d_psr_iterations(fake):
     assert len(P.shoot[0][-1]) == 4                  # (q, p, cost, x): data carried as external points
 
 
+
+class _StubBatcher:
+    """Selects Optimize's manual-adjoint closure; no launch is batched (none is submitted:
+    _lib._launch batches only on a frame thread's GPU path)."""
+
+    def closure(self):
+        import contextlib
+        return contextlib.nullcontext()
+
 @pytest.mark.parametrize("version", ["classic", "hybrid"])
 def test_shoot_loss_grad_bitwise_autograd(fake, version):
     """shooting.shoot_loss_grad (the lockstep frame batches' closure: ShootFn's forward and
@@ -500,7 +509,7 @@ def test_shoot_loss_grad_bitwise_autograd(fake, version):
     res = {}
     for mode in ("autograd", "manual"):
         LM.shoot_cache = None
-        _lib._tl.batcher = object() if mode == "manual" else None
+        _lib._tl.batcher = _StubBatcher() if mode == "manual" else None
         try:
             pr, shoot, trajl, datal, nsteps, change = LM.Optimize(dataloss, q0, p0.clone(), nmax=3)
         finally:

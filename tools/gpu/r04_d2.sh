@@ -5,7 +5,7 @@ set -e
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 O=gpurun_out/r04d
 mkdir -p $O
-for cfg in "off 4 1" "off 4 0" "off 4 2" "on 4 0"; do
+for cfg in "off 4 1" "off 4 0" "off 4 2" "on 4 1" "on 1 1" "on 1 0" "on 4 0"; do
   set -- $cfg
   timeout -k 10 240 python -u bench.py --workload atlas_c4_fixed --steps 2 --warmup 1 --no-cpu-baseline --batch-frames $1 --concurrent-frames $2 --batch-share $3 > $O/c4fixed_$1_$2_$3.json 2> $O/c4fixed_$1_$2_$3.err
   tail -c 200 $O/c4fixed_$1_$2_$3.json
