@@ -53,6 +53,8 @@ _SIGNATURES = {
                                          _P, _SZ, _P],
     "dicp_lddmm_euler_step_rows_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P,
                                        _P, _SZ, _P],
+    "dicp_lddmm_euler_step_cols_f32": [_P, _P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _DBL, _INT, _P, _P,
+                                       _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_fwd_ord_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
                                         _P, _SZ, _P],
     "dicp_lddmm_euler_step_ord_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P, _P,
@@ -832,6 +834,45 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
                                                             nb, _stream(dev)))
     _check_rc(rc, "euler_step_rows")
     return qn, pn, g
+
+
+def euler_step_cols(q_rows, p_rows, q_cols, p_cols, sigma: float, eta: float, dt: float,
+                    q_out, p_out=None, g_out=None, zs_out=None, with_base: bool = False,
+                    add=None):
+    """One column phase of a row-split Euler step (dicp_lddmm_euler_step_cols_f32): the rows
+    (q_rows, p_rows) against the columns (q_cols, p_cols) only, out = dt * sums (+ the rows if
+    with_base) (+ add) for q_out / p_out, sums (+ add) for g_out / zs_out.  add: optional
+    (add_q, add_p, add_g, add_zs), each None or the previous phase's output (may be the same
+    tensor as the output).  p_out / g_out / zs_out None: not formed."""
+    q_rows = _dev(q_rows, "q_rows")
+    p_rows = _dev(p_rows, "p_rows")
+    q_cols = _dev(q_cols, "q_cols")
+    p_cols = _dev(p_cols, "p_cols")
+    nrows, D = q_rows.shape
+    ncols = q_cols.shape[0]
+    dev = q_rows.device
+    adds = tuple(add) if add is not None else (None, None, None, None)
+    for t, name, shape in ((q_out, "q_out", (nrows, D)), (p_out, "p_out", (nrows, D)),
+                           (g_out, "g_out", (nrows,)), (zs_out, "zs_out", (nrows, D))) + tuple(
+            (a, "add", sh) for a, sh in zip(adds, ((nrows, D), (nrows, D), (nrows,), (nrows, D)))):
+        if t is None:
+            continue
+        if not t.is_contiguous() or tuple(t.shape) != shape or t.dtype != torch.float32:
+            raise ValueError(f"{name} must be a contiguous float32 {shape} tensor")
+    if q_out is None:
+        raise ValueError("q_out is required")
+    if nrows == 0:
+        return q_out
+    ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, ncols, D, dev)
+    name = ("ode_self_fwd_eta" if eta else "ode_self_fwd") + ("" if p_out is not None else "_nog")
+    rc = _launch(name, nrows * ncols, 4 * (nrows * (4 * D + 1) + 2 * ncols * D),
+                 lambda: lib().dicp_lddmm_euler_step_cols_f32(
+                     _ptr(q_rows), _ptr(p_rows), nrows, _ptr(q_cols), _ptr(p_cols), ncols, D,
+                     float(sigma), float(eta), float(dt), 1 if with_base else 0,
+                     _ptr(adds[0]), _ptr(adds[1]), _ptr(adds[2]), _ptr(adds[3]),
+                     _ptr(q_out), _ptr(p_out), _ptr(g_out), _ptr(zs_out), _ptr(ws), nb, _stream(dev)))
+    _check_rc(rc, "euler_step_cols")
+    return q_out
 
 
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma: float, eta: float, part: int, nparts: int,

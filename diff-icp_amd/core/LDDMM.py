@@ -87,16 +87,18 @@ class LDDMMModel:
         # again (shooting.ShootCache: the first closure of each Reg_opt L-BFGS run)
         self.shoot_cache = ShootCache()
 
-    def set_row_split(self, group=None, enable=True, exact_reduce=None, verify=None):
+    def set_row_split(self, group=None, enable=True, exact_reduce=None, verify=None, overlap=None):
         """Split every dense Euler shooting of this model over the ranks of a torch.distributed
         group (extension; core/rowsplit.py): all ranks must make the same
         calls (the host logic runs replicated).  enable=False restores single-device shooting.
-        exact_reduce / verify: see RowSplit (rank-ordered VJP sums / cross-rank bit checks).
+        exact_reduce / verify / overlap: see RowSplit (rank-ordered VJP sums / cross-rank bit
+        checks / forward steps in column phases overlapping the all-gathers).
         The L-BFGS divergence fallback draws from a generator seeded identically on every rank
         (tools/optim.py), so the replicated iterates stay in lockstep whatever each rank's
         global RNG state is."""
         from .rowsplit import RowSplit
-        self.row_split = RowSplit(group, exact_reduce=exact_reduce, verify=verify) if enable else None
+        self.row_split = (RowSplit(group, exact_reduce=exact_reduce, verify=verify, overlap=overlap)
+                          if enable else None)
 
     def set_integration_scheme(self, scheme: str):
         self.scheme = scheme

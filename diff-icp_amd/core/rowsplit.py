@@ -6,7 +6,9 @@ Here every rank keeps the full support state (q, p): M x 2D floats, 2.4 MB at 10
 and per ODE evaluation
   * forward (Euler step): rank r computes the rows [r0, r1) of the fused step against all M
     columns (dicp_lddmm_euler_step_rows_f32), then ONE all-gather exchanges the new row
-    slices (+ each rank's divergence partial sum);
+    slices (+ each rank's divergence partial sum).  With `overlap` (W | M) the step runs in
+    column phases (dicp_lddmm_euler_step_cols_f32): the rank's rows against its own slice
+    while the previous step's all-gather is in flight, then against the other slices;
   * adjoint step: rank r computes its part of the symmetric pair-once VJP (the quads
     Q = r mod W, dicp_lddmm_ode_self_bwd_part_f32) for all rows, then ONE all-reduce sums the
     parts (M x 2D floats).
@@ -26,13 +28,17 @@ class RowSplit:
     """Rank / world of a torch.distributed process group (RCCL over xGMI on the GPU box,
     gloo in the CPU tests) and the two collectives the split shooting needs."""
 
-    def __init__(self, group=None, exact_reduce=None, verify=None):
+    def __init__(self, group=None, exact_reduce=None, verify=None, overlap=None):
         """exact_reduce: sum the per-step VJP parts by all-gather + rank-ordered sum instead of
         an all-reduce (bitwise identical on every rank by construction, W x the bytes; default
         from DICP_ROWSPLIT_EXACT, off).  verify: after every all-reduce, all-gather a float64
         checksum of the result and raise if the ranks disagree (one host sync per call; default
         from DICP_ROWSPLIT_VERIFY, off) -- the check that the replicated L-BFGS cannot diverge
-        because a collective returned different bits on different ranks."""
+        because a collective returned different bits on different ranks.  overlap: run each
+        forward step in column phases so that the all-gather of the previous step's rows
+        overlaps the rank's rows against its own slice (ShootFn, split_step_phased; default
+        from DICP_ROWSPLIT_OVERLAP, on) -- a different fp32 summation order than the one-pass
+        step, the same bits on every rank."""
         import os
         self.group = group
         self.rank = dist.get_rank(group)
@@ -42,6 +48,7 @@ class RowSplit:
         self.exact_reduce = bool(int(env("DICP_ROWSPLIT_EXACT", "0"))) if exact_reduce is None \
             else bool(exact_reduce)
         self.verify = bool(int(env("DICP_ROWSPLIT_VERIFY", "0"))) if verify is None else bool(verify)
+        self.overlap = bool(int(env("DICP_ROWSPLIT_OVERLAP", "1"))) if overlap is None else bool(overlap)
         self.verified_calls = 0
 
     def rows(self, M: int):
@@ -72,6 +79,18 @@ class RowSplit:
         else:
             dist.all_gather(list(flat.chunk(self.world)), local.reshape(-1), group=self.group)
         return out
+
+    def gather_into_async(self, out: torch.Tensor, local: torch.Tensor):
+        """gather_into without waiting: returns the work handle, whose wait() makes the current
+        stream wait for the collective (RCCL; gloo: blocks the host).  `out` and `local` must
+        stay untouched until then (local may be read)."""
+        flat = out.view(-1)
+        if flat.numel() != self.world * local.numel():
+            raise ValueError("gather_into_async: out must hold W x local elements")
+        if self._gather_base:
+            return dist.all_gather_into_tensor(flat, local.reshape(-1), group=self.group, async_op=True)
+        return dist.all_gather(list(flat.chunk(self.world)), local.reshape(-1), group=self.group,
+                               async_op=True)
 
     def sum_ordered(self, t: torch.Tensor) -> torch.Tensor:
         """Cross-rank sum as all-gather + a sum in rank order: the same bits on every rank

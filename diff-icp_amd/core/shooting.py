@@ -264,6 +264,44 @@ def skip_p1(need_p1, scheme, has_x, eta, split, nt):
     return (not need_p1) and scheme == "Euler" and not has_x and nt >= 2
 
 
+def phased_split(split, M, order=None):
+    """Whether a row-split shooting runs its fused steps t >= 1 in column phases
+    (split_step_phased): W | M (the direct path), RowSplit.overlap, natural row order."""
+    return (split is not None and split.world > 1 and M % split.world == 0
+            and getattr(split, "overlap", False) and order is None)
+
+
+def split_step_phased(split, Qt, Pt, q_loc, p_loc, sigma, eta, dt, want_div, q_out, p_out=None,
+                      zs_out=None, before_remote=None):
+    """This rank's rows of the Euler step from (Qt, Pt) in column phases
+    (dicp_lddmm_euler_step_cols_f32): the rows against their own slice (q_loc, p_loc: the rows'
+    values, which the rank holds before the all-gather of the step's input has landed), then
+    before_remote() (wait for that all-gather, unpack into Qt, Pt), then against the slices
+    before and after this rank's; the last phase adds the rows themselves.  Every step of a
+    phased shooting and its completion (complete_p1) go through here, so a step's bits do not
+    depend on which of the two formed it.  Returns the slice's divergence rows g (or None)."""
+    M, D = Qt.shape
+    r0, n, _ = split.rows(M)
+    dev, dtp = Qt.device, Qt.dtype
+    want_g = bool(want_div) or eta != 0
+    part = (torch.empty((n, D), device=dev, dtype=dtp),
+            torch.empty((n, D), device=dev, dtype=dtp) if p_out is not None else None,
+            torch.empty(n, device=dev, dtype=dtp) if want_g else None,
+            torch.empty((n, D), device=dev, dtype=dtp) if zs_out is not None else None)
+    _lib.euler_step_cols(q_loc, p_loc, q_loc, p_loc, sigma, eta, dt, part[0], part[1], part[2], part[3])
+    if before_remote is not None:
+        before_remote()
+    ranges = [(c0, c1) for c0, c1 in ((0, r0), (r0 + n, M)) if c1 > c0]
+    g_out = torch.empty(n, device=dev, dtype=dtp) if want_g else None
+    rows_q, rows_p = Qt[r0:r0 + n], Pt[r0:r0 + n]
+    for k, (c0, c1) in enumerate(ranges):
+        last = k == len(ranges) - 1
+        outs = (q_out, p_out, g_out, zs_out) if last else part
+        _lib.euler_step_cols(rows_q, rows_p, Qt[c0:c1], Pt[c0:c1], sigma, eta, dt, outs[0], outs[1],
+                             outs[2], outs[3], with_base=last, add=part)
+    return g_out
+
+
 def complete_p1(Q, P, sigma, eta, want_div, nt, order=None, split=None):
     """Form P[nt] of a trajectory shot with need_p1=False: the last Euler step again, by the
     same fused pass a full shooting uses (bitwise the P[nt] it would have produced; row split:
@@ -272,6 +310,14 @@ def complete_p1(Q, P, sigma, eta, want_div, nt, order=None, split=None):
         if split is not None:
             M = Q.shape[1]
             r0, n, _ = split.rows(M)
+            if phased_split(split, M, order):   # the phased shooting's own step
+                D = Q.shape[2]
+                pn_l = torch.empty((n, D), device=Q.device, dtype=Q.dtype)
+                split_step_phased(split, Q[nt - 1], P[nt - 1], Q[nt - 1][r0:r0 + n],
+                                  P[nt - 1][r0:r0 + n], sigma, eta, 1.0 / nt, want_div,
+                                  torch.empty_like(pn_l), pn_l)
+                split.gather_into(P[nt], pn_l)
+                return
             _, pn_l, _ = _lib.euler_step_rows(Q[nt - 1], P[nt - 1], r0, n, sigma, eta, 1.0 / nt,
                                               want_div, order=order)
             (pn,), _ = split.gather_rows([pn_l], M)
@@ -325,7 +371,8 @@ class ShootFn(torch.autograd.Function):
         # option_epoch: a set_option of a kernel variant between two shootings is a miss (the
         # cached trajectory would not be bitwise what the new variant computes)
         params = (float(sigma), float(eta), int(nt), scheme, bool(want_div),
-                  None if split is None else (split.rank, split.world), skip, use_zs, ctx.raw,
+                  None if split is None else (split.rank, split.world, getattr(split, "overlap", False)),
+                  skip, use_zs, ctx.raw,
                   _lib.option_epoch(), _lib.get_option("batch_share"))
         hit = cache.lookup(q0, p0, x0, params) if cache is not None else None
         if hit is not None:
@@ -373,10 +420,41 @@ class ShootFn(torch.autograd.Function):
             qs_l, ps_l = qp_l[0], qp_l[1]
             qp_all = torch.empty((split.world, 2, n_l, D), device=dev, dtype=q0.dtype)
             dloc = torch.zeros(nt, device=dev, dtype=q0.dtype)
+        # column phases (split_step_phased): the all-gather of step t's rows stays in flight
+        # while step t+1 runs the rank's rows against its own slice; `pend` = that gather
+        phased = direct and phased_split(split, M, order_l)
+        pend = None
+
+        def land(t_in):
+            # the all-gather of the rows of Q[t_in], P[t_in] has landed: unpack (rank order)
+            nonlocal pend
+            if pend is not None:
+                pend.wait()
+                pend = None
+                Q[t_in].view(split.world, n_l, D).copy_(qp_all[:, 0])
+                P[t_in].view(split.world, n_l, D).copy_(qp_all[:, 1])
+
         for t in range(nt):
             q, p = Q[t], P[t]
             x = X[t] if has_x else None
             first = t == 0
+            if phased and not first:
+                r0, n, _ = split.rows(M)
+                last_skip = skip and t == nt - 1
+                # the rank's own rows of (Q[t], P[t]): the send buffer until the gather lands
+                q_loc, p_loc = (qs_l, ps_l) if pend is not None else (q[r0:r0 + n], p[r0:r0 + n])
+                g_l = split_step_phased(split, q, p, q_loc, p_loc, sigma, eta, dt, want_div, qs_l,
+                                        None if last_skip else ps_l,
+                                        None if Zs is None else Zs[t],
+                                        before_remote=lambda t=t: land(t))
+                if last_skip:
+                    split.gather_into(Q[t + 1], qs_l)
+                    P[t + 1].fill_(float("nan"))   # not formed: make any read loud
+                else:
+                    pend = split.gather_into_async(qp_all, qp_l)
+                if g_l is not None:
+                    torch.sum(g_l, 0, keepdim=True, out=dloc[t:t + 1])
+                continue
             if split is not None and direct and not first:
                 r0, n, _ = split.rows(M)
                 last_skip = skip and t == nt - 1
@@ -488,6 +566,8 @@ class ShootFn(torch.autograd.Function):
                 if has_x:
                     X[t + 1].copy_(x + (0.25 * dt) * (vx + 3.0 * vx2))
                 mids.append((qi, pi, xi))
+        if phased:
+            land(nt)
         if direct and nt > 1:
             # cost of the steps t >= 1: their divergence partials summed in rank order (one
             # all-gather), then C[t+1] = C[t] + dt div_t as the staged path

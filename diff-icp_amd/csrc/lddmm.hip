@@ -931,6 +931,90 @@ extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int
                                       nullptr, ws, ws_bytes, stream);
 }
 
+// One column phase of a row-split Euler step (core/shooting.py, RowSplit overlap): rows
+// (q_rows, p_rows) against the columns (q_cols, p_cols) only, each output formed by the
+// epilogue  out = alpha * sum + base + add  with alpha = dt for q and p (1 for g, zs),
+// base = the rows themselves when with_base (the phase that completes the step), and add = the
+// previous phase's output (may alias out: element-wise).  A step whose columns arrive in pieces
+// -- this rank's own slice first (before the all-gather of the new rows has landed), then the
+// others -- chains its phases through `add`.  The pair operators' stores are linear in the
+// column sums, so the phases add up to the whole step (a different fp32 summation order).
+// Ordered packed passes (fwd_alg 2, 5, 6); zs (divergence rows) needs eta = 0.
+namespace {
+template <int D>
+int euler_step_cols_d(const float* qr, const float* pr, int64_t nrows, const float* qc, const float* pc,
+                      int64_t ncols, double sigma, double eta, const Outs& o, void* ws, size_t wsb,
+                      hipStream_t st) {
+  Args a = {qr, pr, nullptr, nullptr, qc, pc, nullptr, nullptr, 0.f};
+  Scal sc = make_scal(sigma, eta);
+  scale_coords(a, sc, sigma);   // origin: this phase's first column point
+  const bool raw = tl_coord_raw != 0;
+  const bool mg = o.ptr[1] != nullptr, div = o.ptr[2] != nullptr;
+  if (o.ptr[3] != nullptr)
+    return mg ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, true, true>, OpOdeSelfFwdPk<D, true, false, true, true, true>>(raw, "ode_self_fwd(pk, zs, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
+              : launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
+  if (eta != 0.0)
+    return mg ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, true>, OpOdeSelfFwdPk<D, true, true, true, false, true>>(raw, "ode_self_fwd_eta(pk, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
+              : launch_fwd_pk<OpOdeSelfFwdPk<D, true, true, false>, OpOdeSelfFwdPk<D, true, true, false, false, true>>(raw, "ode_self_fwd_eta(pk, no mG, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
+  if (!mg)
+    return div ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false>, OpOdeSelfFwdPk<D, true, false, false, false, true>>(raw, "ode_self_fwd(pk, no mG, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
+               : launch_fwd_pk<OpOdeSelfFwdPk<D, false, false, false>, OpOdeSelfFwdPk<D, false, false, false, false, true>>(raw, "ode_self_fwd(pk, no mG, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
+  return div ? launch_fwd_pk<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw, "ode_self_fwd(pk, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
+             : launch_fwd_pk<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(raw, "ode_self_fwd(pk, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
+}
+}  // namespace
+
+extern "C" int dicp_lddmm_euler_step_cols_f32(const float* q_rows, const float* p_rows, int64_t nrows,
+                                              const float* q_cols, const float* p_cols, int64_t ncols,
+                                              int D, double sigma, double eta, double dt, int with_base,
+                                              const float* add_q, const float* add_p, const float* add_g,
+                                              const float* add_zs, float* q_next, float* p_next, float* g,
+                                              float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  auto overlaps = [](const float* out, int64_t n_out, const float* in, int64_t n_in) {
+    return out && in && out < in + n_in && in < out + n_out;
+  };
+  bool bad = nrows < 0 || ncols < 0 || !(sigma > 0) || (nrows > 0 && (!q_rows || !p_rows || !q_next)) ||
+             (ncols > 0 && (!q_cols || !p_cols)) || (add_p && !p_next) || (add_g && !g) ||
+             (add_zs && !zs) || (zs && eta != 0.0);
+  // outputs must not overlap the rows or the columns (they may alias their own `add`)
+  const float* outs_[4] = {q_next, p_next, g, zs};
+  const int64_t w_[4] = {D, D, 1, D};
+  for (int k = 0; k < 4 && !bad; ++k) {
+    const int64_t n = nrows * w_[k];
+    bad = overlaps(outs_[k], n, q_rows, nrows * D) || overlaps(outs_[k], n, p_rows, nrows * D) ||
+          overlaps(outs_[k], n, q_cols, ncols * D) || overlaps(outs_[k], n, p_cols, ncols * D);
+  }
+  if (bad) {
+    set_error("dicp_lddmm_euler_step_cols_f32: invalid arguments (outputs must not overlap the rows or columns; zs needs eta = 0)");
+    return DICP_ERR_INVALID;
+  }
+  if (!packed_fwd_alg()) {
+    set_error("dicp_lddmm_euler_step_cols_f32: needs an ordered packed forward (fwd_alg 2, 5 or 6)");
+    return DICP_ERR_UNSUPPORTED;
+  }
+  if (nrows == 0) return DICP_OK;
+  Outs o = make_outs(q_next, p_next, g, zs);
+  o.alpha[0] = o.alpha[1] = (float)dt;
+  if (with_base) {
+    o.base[0] = q_rows;
+    o.base[1] = p_next ? p_rows : nullptr;
+  }
+  o.add[0] = add_q;
+  o.add[1] = add_p;
+  o.add[2] = add_g;
+  o.add[3] = add_zs;
+  if (ncols == 0) {
+    set_error("dicp_lddmm_euler_step_cols_f32: no columns");
+    return DICP_ERR_INVALID;
+  }
+  switch (D) {
+    case 2: return euler_step_cols_d<2>(q_rows, p_rows, nrows, q_cols, p_cols, ncols, sigma, eta, o, ws, ws_bytes, st);
+    case 3: return euler_step_cols_d<3>(q_rows, p_rows, nrows, q_cols, p_cols, ncols, sigma, eta, o, ws, ws_bytes, st);
+    default: set_error("euler_step_cols: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+  }
+}
+
 extern "C" int dicp_lddmm_ode_self_bwd_part_zs_f32(const float* q, const float* p, const float* gv,
                                                    const float* gmG, const float* gdiv, int64_t M,
                                                    int D, double sigma, double eta, int part,

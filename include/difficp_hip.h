@@ -220,6 +220,26 @@ int dicp_lddmm_euler_step_zs_f32(const float* q, const float* p, int64_t M, int6
                                  float* g, float* zs, void* ws, size_t ws_bytes,
                                  dicp_stream_t stream);
 
+/* One COLUMN PHASE of a row-split Euler step (replaces nothing in the reference, which has no
+ * multi-device path; the step itself is LDDMM.py:194-227 + integrators.py:20-51): rows
+ * (q_rows, p_rows) [nrows] against the columns (q_cols, p_cols) [ncols] only, each output
+ * formed as  out = alpha * (column sums) + base + add  with alpha = dt for q_next / p_next and
+ * 1 for g / zs, base = the rows themselves when with_base != 0, add = the previous phase's
+ * output (NULL: none; may alias the output, element-wise).  A rank of a row split runs its own
+ * row slice against itself first (while the all-gather of the step's new rows is in flight),
+ * then against the other ranks' slices, the last phase with_base: the phases sum to
+ * dicp_lddmm_euler_step_zs_f32 of the slice up to fp32 summation order.  p_next NULL: the
+ * momentum update is not formed; g, zs NULL: not formed (zs needs eta = 0).  Outputs must not
+ * overlap the rows or columns.  Workspace: DICP_WS_ODE_SELF_FWD_ROWS with (M = nrows,
+ * N = ncols).  Ordered packed forward only (fwd_alg 2, 5, 6; DICP_ERR_UNSUPPORTED otherwise).
+ * Not batchable. */
+int dicp_lddmm_euler_step_cols_f32(const float* q_rows, const float* p_rows, int64_t nrows,
+                                   const float* q_cols, const float* p_cols, int64_t ncols, int D,
+                                   double sigma, double eta, double dt, int with_base,
+                                   const float* add_q, const float* add_p, const float* add_g,
+                                   const float* add_zs, float* q_next, float* p_next, float* g,
+                                   float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream);
+
 /* dicp_lddmm_ode_self_fwd_ord_f32 with zs (nrows, D) in place of h (the first ODE evaluation of
  * a shooting: v, mG, g as the plain form, bitwise; H = sum_i p_i.v_i / 2 is then formed by the
  * caller).  Same requirements as above. */

@@ -293,6 +293,28 @@ def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_o
     return qn, pn, g
 
 
+def euler_step_cols(q_rows, p_rows, q_cols, p_cols, sigma, eta, dt, q_out, p_out=None, g_out=None,
+                    zs_out=None, with_base=False, add=None):
+    """One column phase (dicp_lddmm_euler_step_cols_f32): the rows' terms against the given
+    columns only, out = dt sums (+ rows) (+ add) for q / p, sums (+ add) for g / zs."""
+    qr, pr, qc, pc = _d(q_rows), _d(p_rows), _d(q_cols), _d(p_cols)
+    v = R.KRed(qr, qc, pc, sigma) - eta * R.GradKRed(qr, qc, sigma)
+    G = R.GenDKRed(qr, qc, pc, pr, sigma)      # (x, y, column field b, row field c)
+    if eta != 0:
+        G = G - eta * R.HessKRed(qr, qc, pc, pr, sigma) - eta ** 2 * R.GradLapKRed(qr, qc, sigma)
+    g = (pr * R.GradKRed(qr, qc, sigma)).sum(-1) + eta * R.LapKRed(qr, qc, sigma)
+    zs = -sigma ** 2 * R.GradKRed(qr, qc, sigma)
+    adds = tuple(add) if add is not None else (None,) * 4
+    vals = (dt * v + (qr if with_base else 0), dt * (-G) + (pr if with_base else 0), g, zs)
+    for out, val, a in zip((q_out, p_out, g_out, zs_out), vals, adds):
+        if out is None:
+            continue
+        if a is not None:
+            val = val + _d(a)
+        out.copy_(val.to(out.dtype))
+    return q_out
+
+
 def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=True, zs=None, zrow0=0,
                       gq_out=None, gp_out=None):
     """Row-slice decomposition (the kernels' eta != 0 split): part r holds the full VJP of
@@ -317,7 +339,7 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=Tru
     return (gq if want_gq else None), gp
 
 
-_ENTRIES = ("gauss_red_grad", "ode_self_fwd_rows", "euler_step_rows", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+_ENTRIES = ("gauss_red_grad", "ode_self_fwd_rows", "euler_step_rows", "euler_step_cols", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 

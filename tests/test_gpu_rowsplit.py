@@ -79,6 +79,68 @@ def test_bwd_parts_sum(dev, M, W, eta):
     assert torch.equal(one[0], gq) and torch.equal(one[1], gp)
 
 
+def _phased(L, q, p, r0, n, sigma, eta, dt, want_p, want_zs, raw=False):
+    """This slice's Euler step in column phases (own slice, then before / after), as
+    core/shooting.split_step_phased runs it."""
+    M, D = q.shape
+    dev = q.device
+    mk = lambda *sh: torch.empty(sh, device=dev)
+    part = (mk(n, D), mk(n, D) if want_p else None, mk(n), mk(n, D) if want_zs else None)
+    rq, rp = q[r0:r0 + n].clone(), p[r0:r0 + n].clone()
+    with L.coord_mode(raw):
+        L.euler_step_cols(rq, rp, rq, rp, sigma, eta, dt, *part)
+        ranges = [(c0, c1) for c0, c1 in ((0, r0), (r0 + n, M)) if c1 > c0]
+        fin = (mk(n, D), mk(n, D) if want_p else None, mk(n), mk(n, D) if want_zs else None)
+        for k, (c0, c1) in enumerate(ranges):
+            last = k == len(ranges) - 1
+            L.euler_step_cols(q[r0:r0 + n], p[r0:r0 + n], q[c0:c1], p[c0:c1], sigma, eta, dt,
+                              *(fin if last else part), with_base=last, add=part)
+    return fin
+
+
+@pytest.mark.parametrize("M", [130, 3000, 50000])
+@pytest.mark.parametrize("W", [2, 3, 8])
+@pytest.mark.parametrize("eta,want_p,want_zs,raw", [(0.0, True, True, False), (0.0, False, True, False),
+                                                    (0.0, True, False, True), (0.02, True, False, False),
+                                                    (0.02, False, False, False)])
+def test_step_column_phases_sum(dev, M, W, eta, want_p, want_zs, raw):
+    """dicp_lddmm_euler_step_cols_f32: a slice's step in column phases (the row split's
+    overlap of the all-gather) = the one-pass slice step (dicp_lddmm_euler_step_zs_f32), fp32
+    summation order only; every rank's slice, incl. the first and last (one remote range)."""
+    L = _lib()
+    q, p, _, _ = _state(M, 3 * M + W, dev)
+    per = -(-M // W)
+    for r in range(W):
+        r0 = min(per * r, M)
+        n = min(r0 + per, M) - r0
+        if n == 0:
+            continue
+        with L.coord_mode(raw):
+            zs_ref = torch.empty((n, 3), device=dev) if want_zs else None
+            qn, pn, g = L.euler_step_rows(q, p, r0, n, 0.1, eta, 0.1, True, want_p=want_p, zs_out=zs_ref)
+        fq, fp, fg, fz = _phased(L, q, p, r0, n, 0.1, eta, 0.1, want_p, want_zs, raw)
+        assert rel_err(fq, qn) < 2e-6, (r, rel_err(fq, qn))
+        assert rel_err(fg, g) < 2e-5, (r, rel_err(fg, g))
+        if want_p:
+            assert rel_err(fp, pn) < 2e-6, (r, rel_err(fp, pn))
+        if want_zs:
+            assert rel_err(fz, zs_ref) < 2e-5, (r, rel_err(fz, zs_ref))
+    # run to run: the same bits
+    again = _phased(L, q, p, 0, per, 0.1, eta, 0.1, want_p, want_zs, raw)
+    first = _phased(L, q, p, 0, per, 0.1, eta, 0.1, want_p, want_zs, raw)
+    assert all(a is None or torch.equal(a, b) for a, b in zip(again, first))
+
+
+def test_step_columns_rejects_overlap(dev):
+    L = _lib()
+    q, p, _, _ = _state(64, 5, dev)
+    with pytest.raises(RuntimeError):
+        L.euler_step_cols(q[:32], p[:32], q, p, 0.1, 0.0, 0.1, q[:32])   # out = rows
+    with pytest.raises(RuntimeError):
+        L.euler_step_cols(q[:32], p[:32], q, p, 0.1, 0.02, 0.1, torch.empty((32, 3), device=dev),
+                          zs_out=torch.empty((32, 3), device=dev))      # zs needs eta = 0
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -59,6 +59,31 @@ def _run(split, mode=None):
     res["opt_Q1"] = sh_opt.Q[-1].detach().clone()
     with torch.no_grad():   # a fresh full shooting at the returned p0 (cache off): same bits
         res["opt_P1_ref"] = LM.Shoot(q0, p_opt)[-1][1].detach().clone()
+    # 1c. W | M (the direct path): forward steps in column phases (RowSplit.overlap, the
+    # all-gather of step t in flight during step t+1's local phase) against one-pass steps
+    from difficp_amd import _lib
+    calls = [0]
+    inner = _lib.euler_step_cols
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return inner(*a, **k)
+    _lib.euler_step_cols = counted
+    q0e, p0e, tgte = q0[:96].clone(), p0[:96].clone(), tgt[:96].clone()
+    for ov in (True, False):
+        LMe = LDDMMModel(sigma=0.2, D=3, lambd=100.0, version="hybrid", scheme="Euler", nt=5, spec=spec)
+        if split:
+            LMe.set_row_split(exact_reduce=mode == "exact", overlap=ov)
+        pe = p0e.clone().requires_grad_(True)
+        she = LMe.Shoot(q0e, pe)
+        Le = LMe.trajloss(she) + ((she[-1][0] - tgte) ** 2).sum()
+        Le.backward()
+        res[f"ov{int(ov)}_q1"] = she[-1][0].detach().clone()
+        res[f"ov{int(ov)}_p1"] = she[-1][1].detach().clone()
+        res[f"ov{int(ov)}_grad"] = pe.grad.clone()
+        if ov:
+            res["phase_calls"] = torch.tensor(float(calls[0]))
+    _lib.euler_step_cols = inner
     # 2. one diff-ICP iteration of a small two-set match (GMM_opt + Reg_opt(nmax=1))
     psr = workloads.build_two_set(120, torch.device("cpu"), seed=2, nt=5)
     if split:
@@ -88,6 +113,7 @@ def _worker(rank, world, port, q, mode):
 def test_rowsplit_matches_single_process(world, mode):
     import numpy as np
     single = {k: v.numpy() for k, v in _run(False).items()}
+    single.pop("phase_calls", None)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -102,6 +128,13 @@ def test_rowsplit_matches_single_process(world, mode):
     for rank, res in out:
         if mode == "verify":
             assert float(res.pop("verified")) > 0
+        # W | 96: 4 fused steps x (1 local + 1 or 2 remote phases) per shooting
+        assert float(res.pop("phase_calls")) >= 4 * 2
+        for key in ("q1", "p1", "grad"):   # phased and one-pass steps: summation order only
+            a, b = res[f"ov1_{key}"], res[f"ov0_{key}"]
+            assert np.abs(a - b).max() <= 2e-5 * max(1e-12, np.abs(b).max()), (key, world)
+            ref = single[f"ov1_{key}"]
+            assert np.abs(a - ref).max() <= 2e-5 * max(1e-12, np.abs(ref).max()), (key, world)
         # a0 comes out of L-BFGS, which amplifies the fp32 rounding of a different summation
         # order of the gradient (sum of per-rank parts)
         assert np.isfinite(res["opt_P1"]).all()
