@@ -22,7 +22,8 @@ KBASE, KREDSCAL, KRED, GRADK, GRADK_REV, DDK, GENDK, HESSK, LAPK, GRADLAPK, GRAD
     GRADLAPKSCAL, MIN_SQDIST, MIN_SQDIST_OTHER = range(14)
 # enum dicp_ws_kind
 WS_RED, WS_ODE_SELF_FWD, WS_ODE_SELF_BWD, WS_ODE_EXT_FWD, WS_ODE_EXT_BWD, WS_GMM_ESTEP, \
-    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG, WS_ODE_SELF_FWD_ROWS, WS_ODE_SELF_BWD_PART, WS_GRAD = range(12)
+    WS_GMM_MSTEP, WS_GMM_TARGETS, WS_RIDGE_CG, WS_ODE_SELF_FWD_ROWS, WS_ODE_SELF_BWD_PART, WS_GRAD, \
+    WS_ODE_SELF_FWD_PHASED = range(13)
 # enum dicp_grad_kind
 GRAD_HESSW, GRAD_HESSWP, GRAD_ZDOTV, GRAD_HESS3, GRAD_GRADLAP3 = range(5)
 
@@ -53,8 +54,8 @@ _SIGNATURES = {
                                          _P, _SZ, _P],
     "dicp_lddmm_euler_step_rows_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P,
                                        _P, _SZ, _P],
-    "dicp_lddmm_euler_step_cols_f32": [_P, _P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _DBL, _INT, _P, _P,
-                                       _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
+    "dicp_lddmm_euler_step_phase_f32": [_INT, _P, _P, _P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL,
+                                        _P, _P, _P, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_fwd_ord_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
                                         _P, _SZ, _P],
     "dicp_lddmm_euler_step_ord_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _DBL, _P, _P, _P, _P,
@@ -836,25 +837,35 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
     return qn, pn, g
 
 
-def euler_step_cols(q_rows, p_rows, q_cols, p_cols, sigma: float, eta: float, dt: float,
-                    q_out, p_out=None, g_out=None, zs_out=None, with_base: bool = False,
-                    add=None):
-    """One column phase of a row-split Euler step (dicp_lddmm_euler_step_cols_f32): the rows
-    (q_rows, p_rows) against the columns (q_cols, p_cols) only, out = dt * sums (+ the rows if
-    with_base) (+ add) for q_out / p_out, sums (+ add) for g_out / zs_out.  add: optional
-    (add_q, add_p, add_g, add_zs), each None or the previous phase's output (may be the same
-    tensor as the output).  p_out / g_out / zs_out None: not formed."""
-    q_rows = _dev(q_rows, "q_rows")
-    p_rows = _dev(p_rows, "p_rows")
-    q_cols = _dev(q_cols, "q_cols")
-    p_cols = _dev(p_cols, "p_cols")
-    nrows, D = q_rows.shape
-    ncols = q_cols.shape[0]
-    dev = q_rows.device
-    adds = tuple(add) if add is not None else (None, None, None, None)
+def euler_step_phase_ws(nrows: int, M: int, D: int, device):
+    """A workspace for the two calls of euler_step_phase (the partial slots of phase 0 must
+    survive until phase 1 has merged them)."""
+    return _workspace(WS_ODE_SELF_FWD_PHASED, nrows, M, D, device)[0]
+
+
+def euler_step_phase(phase: int, q_loc, p_loc, q, p, row0: int, nrows: int, sigma: float, eta: float,
+                     dt: float, q_out, p_out=None, g_out=None, zs_out=None, ws=None):
+    """One of the two column phases of a row-split Euler step of rows [row0, row0 + nrows)
+    (dicp_lddmm_euler_step_phase_f32): phase 0 = the rows (q_loc, p_loc) against themselves,
+    partial sums into ws; phase 1 = the rows of (q, p) against the other points, then
+    q_out = q_row + dt v, p_out = p_row + dt mG (None: not formed), g_out, zs_out (None: not
+    formed) -- the one-pass slice step up to fp32 summation order.  Both calls take the same
+    output tensors and the same ws (euler_step_phase_ws)."""
+    ref = q_loc if phase == 0 else q
+    ref = _dev(ref, "q")
+    D = ref.shape[1]
+    dev = ref.device
+    if phase == 0:
+        q_loc, p_loc = _dev(q_loc, "q_loc"), _dev(p_loc, "p_loc")
+        if q is not None:
+            q, p = _dev(q, "q"), _dev(p, "p")
+    else:
+        q, p = _dev(q, "q"), _dev(p, "p")
+    M = q.shape[0] if q is not None else None
+    if M is None:
+        raise ValueError("euler_step_phase: q (M, D) is needed for the sizes")
     for t, name, shape in ((q_out, "q_out", (nrows, D)), (p_out, "p_out", (nrows, D)),
-                           (g_out, "g_out", (nrows,)), (zs_out, "zs_out", (nrows, D))) + tuple(
-            (a, "add", sh) for a, sh in zip(adds, ((nrows, D), (nrows, D), (nrows,), (nrows, D)))):
+                           (g_out, "g_out", (nrows,)), (zs_out, "zs_out", (nrows, D))):
         if t is None:
             continue
         if not t.is_contiguous() or tuple(t.shape) != shape or t.dtype != torch.float32:
@@ -863,15 +874,17 @@ def euler_step_cols(q_rows, p_rows, q_cols, p_cols, sigma: float, eta: float, dt
         raise ValueError("q_out is required")
     if nrows == 0:
         return q_out
-    ws, nb = _workspace(WS_ODE_SELF_FWD_ROWS, nrows, ncols, D, dev)
+    if ws is None:
+        raise ValueError("euler_step_phase: pass the same ws (euler_step_phase_ws) to both phases")
+    nb = ws.numel()
     name = ("ode_self_fwd_eta" if eta else "ode_self_fwd") + ("" if p_out is not None else "_nog")
+    ncols = nrows if phase == 0 else M - nrows
     rc = _launch(name, nrows * ncols, 4 * (nrows * (4 * D + 1) + 2 * ncols * D),
-                 lambda: lib().dicp_lddmm_euler_step_cols_f32(
-                     _ptr(q_rows), _ptr(p_rows), nrows, _ptr(q_cols), _ptr(p_cols), ncols, D,
-                     float(sigma), float(eta), float(dt), 1 if with_base else 0,
-                     _ptr(adds[0]), _ptr(adds[1]), _ptr(adds[2]), _ptr(adds[3]),
-                     _ptr(q_out), _ptr(p_out), _ptr(g_out), _ptr(zs_out), _ptr(ws), nb, _stream(dev)))
-    _check_rc(rc, "euler_step_cols")
+                 lambda: lib().dicp_lddmm_euler_step_phase_f32(
+                     int(phase), _ptr(q_loc), _ptr(p_loc), _ptr(q), _ptr(p), M, int(row0), int(nrows), D,
+                     float(sigma), float(eta), float(dt), _ptr(q_out), _ptr(p_out), _ptr(g_out),
+                     _ptr(zs_out), _ptr(ws), nb, _stream(dev)))
+    _check_rc(rc, f"euler_step_phase({phase})")
     return q_out
 
 

@@ -7,8 +7,8 @@ and per ODE evaluation
   * forward (Euler step): rank r computes the rows [r0, r1) of the fused step against all M
     columns (dicp_lddmm_euler_step_rows_f32), then ONE all-gather exchanges the new row
     slices (+ each rank's divergence partial sum).  With `overlap` (W | M) the step runs in
-    column phases (dicp_lddmm_euler_step_cols_f32): the rank's rows against its own slice
-    while the previous step's all-gather is in flight, then against the other slices;
+    two column phases (dicp_lddmm_euler_step_phase_f32): the rank's rows against its own
+    slice while the previous step's all-gather is in flight, then against the other points;
   * adjoint step: rank r computes its part of the symmetric pair-once VJP (the quads
     Q = r mod W, dicp_lddmm_ode_self_bwd_part_f32) for all rows, then ONE all-reduce sums the
     parts (M x 2D floats).

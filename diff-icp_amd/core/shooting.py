@@ -273,32 +273,23 @@ def phased_split(split, M, order=None):
 
 def split_step_phased(split, Qt, Pt, q_loc, p_loc, sigma, eta, dt, want_div, q_out, p_out=None,
                       zs_out=None, before_remote=None):
-    """This rank's rows of the Euler step from (Qt, Pt) in column phases
-    (dicp_lddmm_euler_step_cols_f32): the rows against their own slice (q_loc, p_loc: the rows'
-    values, which the rank holds before the all-gather of the step's input has landed), then
-    before_remote() (wait for that all-gather, unpack into Qt, Pt), then against the slices
-    before and after this rank's; the last phase adds the rows themselves.  Every step of a
-    phased shooting and its completion (complete_p1) go through here, so a step's bits do not
-    depend on which of the two formed it.  Returns the slice's divergence rows g (or None)."""
+    """This rank's rows of the Euler step from (Qt, Pt) in two column phases
+    (dicp_lddmm_euler_step_phase_f32): the rows against their own slice (q_loc, p_loc: the
+    rows' values, which the rank holds before the all-gather of the step's input has landed),
+    then before_remote() (wait for that all-gather, unpack into Qt, Pt), then against the other
+    points and one merge.  Every step of a phased shooting and its completion (complete_p1) go
+    through here, so a step's bits do not depend on which of the two formed it.  Returns the
+    slice's divergence rows g (or None)."""
     M, D = Qt.shape
     r0, n, _ = split.rows(M)
-    dev, dtp = Qt.device, Qt.dtype
     want_g = bool(want_div) or eta != 0
-    part = (torch.empty((n, D), device=dev, dtype=dtp),
-            torch.empty((n, D), device=dev, dtype=dtp) if p_out is not None else None,
-            torch.empty(n, device=dev, dtype=dtp) if want_g else None,
-            torch.empty((n, D), device=dev, dtype=dtp) if zs_out is not None else None)
-    _lib.euler_step_cols(q_loc, p_loc, q_loc, p_loc, sigma, eta, dt, part[0], part[1], part[2], part[3])
+    g_out = torch.empty(n, device=Qt.device, dtype=Qt.dtype) if want_g else None
+    ws = _lib.euler_step_phase_ws(n, M, D, Qt.device)
+    outs = (q_out, p_out, g_out, zs_out)
+    _lib.euler_step_phase(0, q_loc, p_loc, Qt, Pt, r0, n, sigma, eta, dt, *outs, ws=ws)
     if before_remote is not None:
         before_remote()
-    ranges = [(c0, c1) for c0, c1 in ((0, r0), (r0 + n, M)) if c1 > c0]
-    g_out = torch.empty(n, device=dev, dtype=dtp) if want_g else None
-    rows_q, rows_p = Qt[r0:r0 + n], Pt[r0:r0 + n]
-    for k, (c0, c1) in enumerate(ranges):
-        last = k == len(ranges) - 1
-        outs = (q_out, p_out, g_out, zs_out) if last else part
-        _lib.euler_step_cols(rows_q, rows_p, Qt[c0:c1], Pt[c0:c1], sigma, eta, dt, outs[0], outs[1],
-                             outs[2], outs[3], with_base=last, add=part)
+    _lib.euler_step_phase(1, q_loc, p_loc, Qt, Pt, r0, n, sigma, eta, dt, *outs, ws=ws)
     return g_out
 
 

@@ -931,87 +931,140 @@ extern "C" int dicp_lddmm_euler_step_ord_f32(const float* q, const float* p, int
                                       nullptr, ws, ws_bytes, stream);
 }
 
-// One column phase of a row-split Euler step (core/shooting.py, RowSplit overlap): rows
-// (q_rows, p_rows) against the columns (q_cols, p_cols) only, each output formed by the
-// epilogue  out = alpha * sum + base + add  with alpha = dt for q and p (1 for g, zs),
-// base = the rows themselves when with_base (the phase that completes the step), and add = the
-// previous phase's output (may alias out: element-wise).  A step whose columns arrive in pieces
-// -- this rank's own slice first (before the all-gather of the new rows has landed), then the
-// others -- chains its phases through `add`.  The pair operators' stores are linear in the
-// column sums, so the phases add up to the whole step (a different fp32 summation order).
-// Ordered packed passes (fwd_alg 2, 5, 6); zs (divergence rows) needs eta = 0.
+// A row-split Euler step in two column phases (core/shooting.py, RowSplit.overlap): phase 0
+// runs the rank's rows against its own slice -- the rows' values, which the rank holds before
+// the all-gather of the step's input has landed -- into the first partial slots of `ws`;
+// phase 1 runs them against the other M - nrows points (the wrapped column range from
+// row0 + nrows) into the remaining slots and merges all slots once, with the Euler epilogue.
+// The two calls must see the same sizes, output pointers (which select the pass) and `ws`.
+// The pair operators' stores are linear in the column sums, so the result is the one-pass
+// step's up to fp32 summation order (and the coordinate origin of each phase: its first
+// column point).  Ordered packed passes (fwd_alg 2, 5, 6); zs needs eta = 0.
 namespace {
-template <int D>
-int euler_step_cols_d(const float* qr, const float* pr, int64_t nrows, const float* qc, const float* pc,
-                      int64_t ncols, double sigma, double eta, const Outs& o, void* ws, size_t wsb,
-                      hipStream_t st) {
-  Args a = {qr, pr, nullptr, nullptr, qc, pc, nullptr, nullptr, 0.f};
-  Scal sc = make_scal(sigma, eta);
-  scale_coords(a, sc, sigma);   // origin: this phase's first column point
-  const bool raw = tl_coord_raw != 0;
-  const bool mg = o.ptr[1] != nullptr, div = o.ptr[2] != nullptr;
-  if (o.ptr[3] != nullptr)
-    return mg ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, true, true>, OpOdeSelfFwdPk<D, true, false, true, true, true>>(raw, "ode_self_fwd(pk, zs, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
-              : launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
-  if (eta != 0.0)
-    return mg ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, true>, OpOdeSelfFwdPk<D, true, true, true, false, true>>(raw, "ode_self_fwd_eta(pk, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
-              : launch_fwd_pk<OpOdeSelfFwdPk<D, true, true, false>, OpOdeSelfFwdPk<D, true, true, false, false, true>>(raw, "ode_self_fwd_eta(pk, no mG, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
+template <class Op>
+int step_phase_op(const char* name, int phase, const Args& a0, const Args& a1, const Scal& sc, int64_t nrows,
+                  int64_t M, int64_t coff, const Outs& o, void* ws, size_t wsb, hipStream_t st) {
+  return launch_pk_phase<Op>(name, phase, phase == 0 ? a0 : a1, sc, nrows, nrows, M - nrows, coff, M, o, ws, wsb, st);
+}
+
+struct PhaseGo {
+  int phase;
+  const Args &a0, &a1;
+  const Scal& sc;
+  int64_t nrows, M, coff;
+  const Outs& o;
+  void* ws;
+  size_t wsb;
+  hipStream_t st;
+  template <class OpS, class OpR>
+  int run(bool raw) const {
+    return raw ? step_phase_op<OpR>("ode_self_fwd(pk, phase)", phase, a0, a1, sc, nrows, M, coff, o, ws, wsb, st)
+               : step_phase_op<OpS>("ode_self_fwd(pk, phase)", phase, a0, a1, sc, nrows, M, coff, o, ws, wsb, st);
+  }
+};
+
+// the pass (and its raw-coordinate twin) for these outputs: f.run<OpScaled, OpRaw>(raw)
+template <int D, class F>
+int step_phase_pick(bool raw, bool zs, bool eta, bool mg, bool div, const F& f) {
+  if (zs)
+    return mg ? f.template run<OpOdeSelfFwdPk<D, true, false, true, true>, OpOdeSelfFwdPk<D, true, false, true, true, true>>(raw)
+              : f.template run<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw);
+  if (eta)
+    return mg ? f.template run<OpOdeSelfFwdPk<D, true, true>, OpOdeSelfFwdPk<D, true, true, true, false, true>>(raw)
+              : f.template run<OpOdeSelfFwdPk<D, true, true, false>, OpOdeSelfFwdPk<D, true, true, false, false, true>>(raw);
   if (!mg)
-    return div ? launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false>, OpOdeSelfFwdPk<D, true, false, false, false, true>>(raw, "ode_self_fwd(pk, no mG, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
-               : launch_fwd_pk<OpOdeSelfFwdPk<D, false, false, false>, OpOdeSelfFwdPk<D, false, false, false, false, true>>(raw, "ode_self_fwd(pk, no mG, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
-  return div ? launch_fwd_pk<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw, "ode_self_fwd(pk, cols)", a, sc, nrows, ncols, o, ws, wsb, st)
-             : launch_fwd_pk<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(raw, "ode_self_fwd(pk, cols)", a, sc, nrows, ncols, o, ws, wsb, st);
+    return div ? f.template run<OpOdeSelfFwdPk<D, true, false, false>, OpOdeSelfFwdPk<D, true, false, false, false, true>>(raw)
+               : f.template run<OpOdeSelfFwdPk<D, false, false, false>, OpOdeSelfFwdPk<D, false, false, false, false, true>>(raw);
+  return div ? f.template run<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw)
+             : f.template run<OpOdeSelfFwdPk<D, false>, OpOdeSelfFwdPk<D, false, false, true, false, true>>(raw);
+}
+
+template <int D>
+int euler_step_phase_d(int phase, const float* q_loc, const float* p_loc, const float* q, const float* p, int64_t M,
+                       int64_t row0, int64_t nrows, double sigma, double eta, const Outs& o, void* ws, size_t wsb,
+                       hipStream_t st) {
+  Scal sc0 = make_scal(sigma, eta), sc1 = sc0;
+  // phase 0: rows = columns = the local slice; phase 1: rows = the slice of (q, p), columns =
+  // all of (q, p) read from row0 + nrows on (wrapping), M - nrows of them
+  Args a0 = {q_loc, p_loc, nullptr, nullptr, q_loc, p_loc, nullptr, nullptr, 0.f};
+  Args a1 = {q ? q + row0 * D : nullptr, p ? p + row0 * D : nullptr, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
+  const bool raw = tl_coord_raw != 0;
+  scale_coords(a0, sc0, sigma);
+  scale_coords(a1, sc1, sigma);
+  if (raw) {
+    raw_coords(a0, sc0);
+    raw_coords(a1, sc1);
+  }
+  const Scal& sc = phase == 0 ? sc0 : sc1;
+  const int64_t coff = row0 + nrows < M ? row0 + nrows : 0;
+  const PhaseGo go{phase, a0, a1, sc, nrows, M, coff, o, ws, wsb, st};
+  return step_phase_pick<D>(raw, o.ptr[3] != nullptr, eta != 0.0, o.ptr[1] != nullptr, o.ptr[2] != nullptr, go);
+}
+
+template <int D>
+size_t euler_step_phase_ws(int64_t nrows, int64_t M) {
+  size_t m = 0;
+  for (size_t v : {pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, true, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, true, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, true, true, false, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, true, false>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, true, false, false, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, false>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, false, false, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, false, false, false>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, false, false, false, false, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, true, false, true, false, true>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, false>>(nrows, nrows, M - nrows),
+                   pk_phase_ws_bytes<OpOdeSelfFwdPk<D, false, false, true, false, true>>(nrows, nrows, M - nrows)})
+    m = v > m ? v : m;
+  return m;
 }
 }  // namespace
 
-extern "C" int dicp_lddmm_euler_step_cols_f32(const float* q_rows, const float* p_rows, int64_t nrows,
-                                              const float* q_cols, const float* p_cols, int64_t ncols,
-                                              int D, double sigma, double eta, double dt, int with_base,
-                                              const float* add_q, const float* add_p, const float* add_g,
-                                              const float* add_zs, float* q_next, float* p_next, float* g,
-                                              float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream) {
+extern "C" int dicp_lddmm_euler_step_phase_f32(int phase, const float* q_loc, const float* p_loc, const float* q,
+                                               const float* p, int64_t M, int64_t row0, int64_t nrows, int D,
+                                               double sigma, double eta, double dt, float* q_next, float* p_next,
+                                               float* g, float* zs, void* ws, size_t ws_bytes,
+                                               dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   auto overlaps = [](const float* out, int64_t n_out, const float* in, int64_t n_in) {
     return out && in && out < in + n_in && in < out + n_out;
   };
-  bool bad = nrows < 0 || ncols < 0 || !(sigma > 0) || (nrows > 0 && (!q_rows || !p_rows || !q_next)) ||
-             (ncols > 0 && (!q_cols || !p_cols)) || (add_p && !p_next) || (add_g && !g) ||
-             (add_zs && !zs) || (zs && eta != 0.0);
-  // outputs must not overlap the rows or the columns (they may alias their own `add`)
+  bool bad = (phase != 0 && phase != 1) || M < 0 || row0 < 0 || nrows < 0 || row0 + nrows > M ||
+             (nrows > 0 && nrows == M) || !(sigma > 0) || (nrows > 0 && !q_next) || (zs && eta != 0.0) ||
+             (nrows > 0 && phase == 0 && (!q_loc || !p_loc)) || (nrows > 0 && phase == 1 && (!q || !p));
+  // outputs (phase 1 writes them) must not overlap (q, p); they may be the local slice's
+  // buffers, which only phase 0 reads
   const float* outs_[4] = {q_next, p_next, g, zs};
   const int64_t w_[4] = {D, D, 1, D};
-  for (int k = 0; k < 4 && !bad; ++k) {
+  for (int k = 0; k < 4 && !bad && phase == 1; ++k) {
     const int64_t n = nrows * w_[k];
-    bad = overlaps(outs_[k], n, q_rows, nrows * D) || overlaps(outs_[k], n, p_rows, nrows * D) ||
-          overlaps(outs_[k], n, q_cols, ncols * D) || overlaps(outs_[k], n, p_cols, ncols * D);
+    bad = overlaps(outs_[k], n, q, M * D) || overlaps(outs_[k], n, p, M * D);
   }
   if (bad) {
-    set_error("dicp_lddmm_euler_step_cols_f32: invalid arguments (outputs must not overlap the rows or columns; zs needs eta = 0)");
+    set_error("dicp_lddmm_euler_step_phase_f32: invalid arguments (phase 0/1, 0 <= nrows < M, outputs must "
+              "not overlap the inputs, zs needs eta = 0)");
     return DICP_ERR_INVALID;
   }
   if (!packed_fwd_alg()) {
-    set_error("dicp_lddmm_euler_step_cols_f32: needs an ordered packed forward (fwd_alg 2, 5 or 6)");
+    set_error("dicp_lddmm_euler_step_phase_f32: needs an ordered packed forward (fwd_alg 2, 5 or 6)");
     return DICP_ERR_UNSUPPORTED;
   }
   if (nrows == 0) return DICP_OK;
   Outs o = make_outs(q_next, p_next, g, zs);
   o.alpha[0] = o.alpha[1] = (float)dt;
-  if (with_base) {
-    o.base[0] = q_rows;
-    o.base[1] = p_next ? p_rows : nullptr;
-  }
-  o.add[0] = add_q;
-  o.add[1] = add_p;
-  o.add[2] = add_g;
-  o.add[3] = add_zs;
-  if (ncols == 0) {
-    set_error("dicp_lddmm_euler_step_cols_f32: no columns");
-    return DICP_ERR_INVALID;
+  if (phase == 1) {
+    o.base[0] = q + row0 * D;
+    o.base[1] = p_next ? p + row0 * D : nullptr;
   }
   switch (D) {
-    case 2: return euler_step_cols_d<2>(q_rows, p_rows, nrows, q_cols, p_cols, ncols, sigma, eta, o, ws, ws_bytes, st);
-    case 3: return euler_step_cols_d<3>(q_rows, p_rows, nrows, q_cols, p_cols, ncols, sigma, eta, o, ws, ws_bytes, st);
-    default: set_error("euler_step_cols: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
+    case 2: return euler_step_phase_d<2>(phase, q_loc, p_loc, q, p, M, row0, nrows, sigma, eta, o, ws, ws_bytes, st);
+    case 3: return euler_step_phase_d<3>(phase, q_loc, p_loc, q, p, M, row0, nrows, sigma, eta, o, ws, ws_bytes, st);
+    default: set_error("euler_step_phase: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
 
@@ -1084,6 +1137,9 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
     case DICP_WS_ODE_EXT_BWD: return D == 2 ? ode_ext_bwd_ws<2>(N, M) : ode_ext_bwd_ws<3>(N, M);
     case DICP_WS_ODE_SELF_FWD_ROWS:
       return D == 2 ? ode_self_fwd_rows_ws<2>(M, N) : ode_self_fwd_rows_ws<3>(M, N);
+    case DICP_WS_ODE_SELF_FWD_PHASED:
+      if (M <= 0 || M >= N) return 0;
+      return D == 2 ? euler_step_phase_ws<2>(M, N) : euler_step_phase_ws<3>(M, N);
     case DICP_WS_ODE_SELF_BWD_PART: {
       const int np = N < 1 ? 1 : (int)N;
       return D == 2 ? ode_self_bwd_part_ws<2>(M, np) : ode_self_bwd_part_ws<3>(M, np);

@@ -204,9 +204,18 @@ int pk_rp(int64_t M, int64_t N) {
 
 // The body of rowred_pk_kernel for block (bx, by) of a grid with S column splits (by < S;
 // S > 1: partial slabs, S = 1: the epilogue) -- shared by the plain and the batched kernel.
-template <class Op, int RP>
+// WRAP (the row split's column phases): column j is read at (coff + j) mod ntot.
+template <class Op, int RP, bool WRAP = false>
 __device__ __forceinline__ void rowred_pk_body(Args args, Scal sc, int64_t M, int64_t N, int64_t chunk,
-                                               const Outs& outs, unsigned bx, unsigned by, unsigned S) {
+                                               const Outs& outs, unsigned bx, unsigned by, unsigned S,
+                                               int64_t coff = 0, int64_t ntot = 0) {
+  auto col = [&](int64_t j) {
+    if constexpr (WRAP) {
+      j += coff;
+      if (j >= ntot) j -= ntot;
+    }
+    return j;
+  };
   using Base = typename Op::Base;
   constexpr int CW4 = Op::CW4;
   constexpr int NACC = Op::NACC;
@@ -239,7 +248,7 @@ __device__ __forceinline__ void rowred_pk_body(Args args, Scal sc, int64_t M, in
   float pre[CW4 * 4];
   int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
   if (cnt > 0 && tid < cnt) {
-    pk_load_col<Op>(args, sc, j0 + tid, pre);
+    pk_load_col<Op>(args, sc, col(j0 + tid), pre);
 #pragma unroll
     for (int k = 0; k < CW4; ++k)
       lds[0][tid * CW4 + k] = make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
@@ -250,7 +259,7 @@ __device__ __forceinline__ void rowred_pk_body(Args args, Scal sc, int64_t M, in
     const int64_t jn = jt + kTile;
     const int cntn = jn < j1 ? (int)((j1 - jn) < kTile ? (j1 - jn) : kTile) : 0;
     if (tid < cntn) {
-      pk_load_col<Op>(args, sc, jn + tid, pre);
+      pk_load_col<Op>(args, sc, col(jn + tid), pre);
 #pragma unroll
       for (int k = 0; k < CW4; ++k)
         lds[buf ^ 1][tid * CW4 + k] =
@@ -439,6 +448,97 @@ int launch_rowred_pk_rp(const char* name, const Args& a, const Scal& sc, int64_t
     if (rc) return rc;
   }
   return DICP_OK;
+}
+
+// ---- column phases of a row-split step (dicp_lddmm_euler_step_phase_f32) ----
+// Phase 0: the nrows rows against n0 columns (the rank's own slice, Args columns), partial
+// slabs into slots [0, S0) of the workspace; phase 1: against the n1 columns (coff + j) mod
+// ntot, slots [S0, S0 + S1), then ONE merge of all S0 + S1 slots with the epilogue `fin`.
+// Both phases compute S0 and S1 the same way (pk_phase_splits), so the slab layout agrees.
+template <class Op, int RP>
+__global__ __launch_bounds__(kBlock) DICP_FWD_PK_ATTR void rowred_pk_phase_kernel(Args args, Scal sc, int64_t M, int64_t N,
+                                                                 int64_t chunk, Outs slabs, int64_t coff,
+                                                                 int64_t ntot) {
+  // S = 2: always the slab store (a phase never applies the epilogue itself)
+  rowred_pk_body<Op, RP, true>(args, sc, M, N, chunk, slabs, blockIdx.x, blockIdx.y, 2u, coff, ntot);
+}
+
+template <class Op>
+inline void pk_phase_splits(int64_t nrows, int64_t n0, int64_t n1, int& S0, int& S1) {
+  S0 = n0 > 0 ? rowred_pk_splits<Op>(nrows, n0) : 0;
+  S1 = n1 > 0 ? rowred_pk_splits<Op>(nrows, n1) : 0;
+}
+
+template <class Op>
+size_t pk_phase_ws_bytes(int64_t nrows, int64_t n0, int64_t n1) {
+  int S0, S1;
+  pk_phase_splits<Op>(nrows, n0, n1, S0, S1);
+  return (size_t)(S0 + S1) * (size_t)nrows * (size_t)total_out_width<typename Op::Base>() * sizeof(float);
+}
+
+template <class Op, int RP>
+int launch_pk_phase_rp(const char* name, const Args& a, const Scal& sc, int64_t nrows, int64_t ncols,
+                       int64_t coff, int64_t ntot, int slot0, int S, const Outs& slabs, hipStream_t st) {
+  const int64_t chunk = chunk_of(ncols, S);
+  const int64_t bx = (nrows + (int64_t)kBlock * 2 * RP - 1) / ((int64_t)kBlock * 2 * RP);
+  Outs part = slabs;
+  for (int k = 0; k < Op::Base::kNOut; ++k)
+    if (part.ptr[k]) part.ptr[k] += (int64_t)slot0 * nrows * Op::Base::kOutW[k];
+  rowred_pk_phase_kernel<Op, RP><<<dim3((unsigned)bx, (unsigned)S, 1), dim3(kBlock), 0, st>>>(a, sc, nrows, ncols, chunk,
+                                                                                           part, coff, ntot);
+  return check_launch(name);
+}
+
+// phase 0: (a: rows and the n0 local columns); phase 1: (a: rows and the whole column array
+// of ntot points, read from coff on, n1 of them), then the merge into `fin`.
+template <class Op>
+int launch_pk_phase(const char* name, int phase, const Args& a, const Scal& sc, int64_t nrows, int64_t n0,
+                    int64_t n1, int64_t coff, int64_t ntot, const Outs& fin, void* ws, size_t ws_bytes,
+                    hipStream_t st) {
+  using Base = typename Op::Base;
+  if (nrows <= 0) return DICP_OK;
+  if (int rc = no_batch(name)) return rc;
+  int S0, S1;
+  pk_phase_splits<Op>(nrows, n0, n1, S0, S1);
+  const size_t need = pk_phase_ws_bytes<Op>(nrows, n0, n1);
+  if (ws == nullptr || ws_bytes < need) {
+    set_error("%s: workspace too small (%zu < %zu bytes)", name, ws_bytes, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  const int S = S0 + S1;
+  Outs slabs = fin;
+  float* cur = reinterpret_cast<float*>(ws);
+  for (int k = 0; k < Base::kNOut; ++k) {
+    slabs.ptr[k] = fin.ptr[k] ? cur : nullptr;
+    cur += (int64_t)S * nrows * Base::kOutW[k];
+  }
+  const int64_t ncols = phase == 0 ? n0 : n1;
+  const int slot0 = phase == 0 ? 0 : S0;
+  const int Sp = phase == 0 ? S0 : S1;
+  if (Sp > 0) {
+    int rc;
+    switch (pk_rp<Op>(nrows, ncols)) {
+      case 2: rc = launch_pk_phase_rp<Op, 2>(name, a, sc, nrows, ncols, coff, ntot, slot0, Sp, slabs, st); break;
+      default: rc = launch_pk_phase_rp<Op, 1>(name, a, sc, nrows, ncols, coff, ntot, slot0, Sp, slabs, st); break;
+    }
+    if (rc) return rc;
+  }
+  if (phase == 0) return DICP_OK;
+  MergeSet ms;
+  int nk = 0;
+  int64_t nmax = 0;
+  for (int k = 0; k < Base::kNOut; ++k) {
+    if (!fin.ptr[k]) continue;
+    ms.slab[nk] = slabs.ptr[k];
+    ms.n[nk] = nrows * Base::kOutW[k];
+    ms.k[nk] = k;
+    nmax = ms.n[nk] > nmax ? ms.n[nk] : nmax;
+    ++nk;
+  }
+  if (nk == 0) return DICP_OK;
+  const int64_t nb = (nmax + kBlock - 1) / kBlock;
+  merge_slabs_kernel<false><<<dim3((unsigned)nb, (unsigned)nk), dim3(kBlock), 0, st>>>(ms, fin, S);
+  return check_launch(name);
 }
 
 template <class Op>

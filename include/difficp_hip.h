@@ -220,25 +220,27 @@ int dicp_lddmm_euler_step_zs_f32(const float* q, const float* p, int64_t M, int6
                                  float* g, float* zs, void* ws, size_t ws_bytes,
                                  dicp_stream_t stream);
 
-/* One COLUMN PHASE of a row-split Euler step (replaces nothing in the reference, which has no
- * multi-device path; the step itself is LDDMM.py:194-227 + integrators.py:20-51): rows
- * (q_rows, p_rows) [nrows] against the columns (q_cols, p_cols) [ncols] only, each output
- * formed as  out = alpha * (column sums) + base + add  with alpha = dt for q_next / p_next and
- * 1 for g / zs, base = the rows themselves when with_base != 0, add = the previous phase's
- * output (NULL: none; may alias the output, element-wise).  A rank of a row split runs its own
- * row slice against itself first (while the all-gather of the step's new rows is in flight),
- * then against the other ranks' slices, the last phase with_base: the phases sum to
- * dicp_lddmm_euler_step_zs_f32 of the slice up to fp32 summation order.  p_next NULL: the
- * momentum update is not formed; g, zs NULL: not formed (zs needs eta = 0).  Outputs must not
- * overlap the rows or columns.  Workspace: DICP_WS_ODE_SELF_FWD_ROWS with (M = nrows,
- * N = ncols).  Ordered packed forward only (fwd_alg 2, 5, 6; DICP_ERR_UNSUPPORTED otherwise).
- * Not batchable. */
-int dicp_lddmm_euler_step_cols_f32(const float* q_rows, const float* p_rows, int64_t nrows,
-                                   const float* q_cols, const float* p_cols, int64_t ncols, int D,
-                                   double sigma, double eta, double dt, int with_base,
-                                   const float* add_q, const float* add_p, const float* add_g,
-                                   const float* add_zs, float* q_next, float* p_next, float* g,
-                                   float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream);
+/* A row-split Euler step in two COLUMN PHASES (no reference counterpart: the reference has no
+ * multi-device path; the step itself is LDDMM.py:194-227 + integrators.py:20-51).  Rows
+ * [row0, row0 + nrows) of (q, p) (M points), 0 < nrows < M:
+ *   phase 0: the rows against their own slice, given as (q_loc, p_loc) (nrows, D) -- the values
+ *            a rank of a row split holds before the all-gather of the step's input (q, p) has
+ *            landed; partial sums into the first slots of `ws` (outputs not written; q, p may
+ *            be NULL);
+ *   phase 1: the rows of (q, p) against the other M - nrows points (from row0 + nrows on,
+ *            wrapping), into the remaining slots, then one merge of all slots with the Euler
+ *            epilogue: q_next = q_row + dt v, p_next = p_row + dt mG, g, zs as
+ *            dicp_lddmm_euler_step_zs_f32 of the slice (fp32 summation order and each phase's
+ *            coordinate origin aside).
+ * Both calls take the same sizes, the same output pointers (their NULL pattern selects the
+ * pass: p_next NULL = no momentum update, g / zs NULL = not formed; zs needs eta = 0) and the
+ * same `ws`, untouched in between, on one stream.  Outputs must not overlap (q, p) (they may
+ * be the local slice's buffers: only phase 0 reads those).  Workspace kind DICP_WS_ODE_SELF_FWD_PHASED (M = nrows, N = M).  Ordered packed
+ * forward only (fwd_alg 2, 5, 6; DICP_ERR_UNSUPPORTED otherwise).  Not batchable. */
+int dicp_lddmm_euler_step_phase_f32(int phase, const float* q_loc, const float* p_loc, const float* q,
+                                    const float* p, int64_t M, int64_t row0, int64_t nrows, int D,
+                                    double sigma, double eta, double dt, float* q_next, float* p_next,
+                                    float* g, float* zs, void* ws, size_t ws_bytes, dicp_stream_t stream);
 
 /* dicp_lddmm_ode_self_fwd_ord_f32 with zs (nrows, D) in place of h (the first ODE evaluation of
  * a shooting: v, mG, g as the plain form, bitwise; H = sum_i p_i.v_i / 2 is then formed by the
@@ -352,7 +354,8 @@ enum dicp_ws_kind {
   DICP_WS_RIDGE_CG = 8,          /* M = points, N unused */
   DICP_WS_ODE_SELF_FWD_ROWS = 9, /* M = rows of the slice, N = all points (columns) */
   DICP_WS_ODE_SELF_BWD_PART = 10, /* M = points, N = nparts */
-  DICP_WS_GRAD = 11              /* dicp_gauss_red_grad_f32: M rows, N columns */
+  DICP_WS_GRAD = 11,             /* dicp_gauss_red_grad_f32: M rows, N columns */
+  DICP_WS_ODE_SELF_FWD_PHASED = 12 /* dicp_lddmm_euler_step_phase_f32: M = rows, N = points */
 };
 size_t dicp_workspace_bytes(int kind, int64_t M, int64_t N, int D);
 

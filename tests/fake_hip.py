@@ -293,25 +293,37 @@ def euler_step_rows(q, p, row0, nrows, sigma, eta, dt, want_div, q_out=None, p_o
     return qn, pn, g
 
 
-def euler_step_cols(q_rows, p_rows, q_cols, p_cols, sigma, eta, dt, q_out, p_out=None, g_out=None,
-                    zs_out=None, with_base=False, add=None):
-    """One column phase (dicp_lddmm_euler_step_cols_f32): the rows' terms against the given
-    columns only, out = dt sums (+ rows) (+ add) for q / p, sums (+ add) for g / zs."""
-    qr, pr, qc, pc = _d(q_rows), _d(p_rows), _d(q_cols), _d(p_cols)
+def _cross_terms(qr, pr, qc, pc, sigma, eta):
+    """(v, mG, g, zs) of the rows (qr, pr) against the columns (qc, pc) only."""
     v = R.KRed(qr, qc, pc, sigma) - eta * R.GradKRed(qr, qc, sigma)
     G = R.GenDKRed(qr, qc, pc, pr, sigma)      # (x, y, column field b, row field c)
     if eta != 0:
         G = G - eta * R.HessKRed(qr, qc, pc, pr, sigma) - eta ** 2 * R.GradLapKRed(qr, qc, sigma)
     g = (pr * R.GradKRed(qr, qc, sigma)).sum(-1) + eta * R.LapKRed(qr, qc, sigma)
     zs = -sigma ** 2 * R.GradKRed(qr, qc, sigma)
-    adds = tuple(add) if add is not None else (None,) * 4
-    vals = (dt * v + (qr if with_base else 0), dt * (-G) + (pr if with_base else 0), g, zs)
-    for out, val, a in zip((q_out, p_out, g_out, zs_out), vals, adds):
-        if out is None:
-            continue
-        if a is not None:
-            val = val + _d(a)
-        out.copy_(val.to(out.dtype))
+    return v, -G, g, zs
+
+
+def euler_step_phase_ws(nrows, M, D, device):
+    return {}
+
+
+def euler_step_phase(phase, q_loc, p_loc, q, p, row0, nrows, sigma, eta, dt, q_out, p_out=None,
+                     g_out=None, zs_out=None, ws=None):
+    """dicp_lddmm_euler_step_phase_f32: phase 0 = the rows against their own slice (kept in
+    ws), phase 1 = against the other points (wrapping from row0 + nrows), then the step."""
+    if phase == 0:
+        ws["part"] = _cross_terms(_d(q_loc), _d(p_loc), _d(q_loc), _d(p_loc), sigma, eta)
+        return q_out
+    M = q.shape[0]
+    idx = [(row0 + nrows + j) % M for j in range(M - nrows)]
+    Q, P = _d(q), _d(p)
+    rq, rp = Q[row0:row0 + nrows], P[row0:row0 + nrows]
+    rem = _cross_terms(rq, rp, Q[idx], P[idx], sigma, eta)
+    v, mG, g, zs = (a + b for a, b in zip(ws.pop("part"), rem))
+    for out, val in ((q_out, rq + dt * v), (p_out, rp + dt * mG), (g_out, g), (zs_out, zs)):
+        if out is not None:
+            out.copy_(val.to(out.dtype))
     return q_out
 
 
@@ -339,7 +351,7 @@ def ode_self_bwd_part(q, p, gv, gmG, gdiv, sigma, eta, part, nparts, want_gq=Tru
     return (gq if want_gq else None), gp
 
 
-_ENTRIES = ("gauss_red_grad", "ode_self_fwd_rows", "euler_step_rows", "euler_step_cols", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
+_ENTRIES = ("gauss_red_grad", "ode_self_fwd_rows", "euler_step_rows", "euler_step_phase", "euler_step_phase_ws", "ode_self_bwd_part", "kernel_ridge_cg", "euler_step", "euler_adjoint_step", "radius_count", "gauss_red", "ode_self_fwd", "ode_self_bwd", "ode_ext_fwd", "ode_ext_bwd",
             "gmm_estep", "gmm_mstep", "gmm_targets")
 
 

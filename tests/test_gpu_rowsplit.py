@@ -79,23 +79,28 @@ def test_bwd_parts_sum(dev, M, W, eta):
     assert torch.equal(one[0], gq) and torch.equal(one[1], gp)
 
 
-def _phased(L, q, p, r0, n, sigma, eta, dt, want_p, want_zs, raw=False):
-    """This slice's Euler step in column phases (own slice, then before / after), as
-    core/shooting.split_step_phased runs it."""
+def _split_of(rank, world):
+    import types
+
+    def rows(M):
+        per = -(-M // world)
+        r0 = min(per * rank, M)
+        return r0, min(r0 + per, M) - r0, per
+    return types.SimpleNamespace(rank=rank, world=world, rows=rows, overlap=True)
+
+
+def _phased(L, q, p, rank, W, sigma, eta, dt, want_p, want_zs, raw=False):
+    """This rank's slice step in the two column phases (core/shooting.split_step_phased)."""
+    from difficp_amd.core.shooting import split_step_phased
     M, D = q.shape
-    dev = q.device
-    mk = lambda *sh: torch.empty(sh, device=dev)
-    part = (mk(n, D), mk(n, D) if want_p else None, mk(n), mk(n, D) if want_zs else None)
-    rq, rp = q[r0:r0 + n].clone(), p[r0:r0 + n].clone()
+    sp = _split_of(rank, W)
+    r0, n, _ = sp.rows(M)
+    mk = lambda *sh: torch.empty(sh, device=q.device)
+    ql, pl = q[r0:r0 + n].clone(), p[r0:r0 + n].clone()
+    qo, po, zo = mk(n, D), mk(n, D) if want_p else None, mk(n, D) if want_zs else None
     with L.coord_mode(raw):
-        L.euler_step_cols(rq, rp, rq, rp, sigma, eta, dt, *part)
-        ranges = [(c0, c1) for c0, c1 in ((0, r0), (r0 + n, M)) if c1 > c0]
-        fin = (mk(n, D), mk(n, D) if want_p else None, mk(n), mk(n, D) if want_zs else None)
-        for k, (c0, c1) in enumerate(ranges):
-            last = k == len(ranges) - 1
-            L.euler_step_cols(q[r0:r0 + n], p[r0:r0 + n], q[c0:c1], p[c0:c1], sigma, eta, dt,
-                              *(fin if last else part), with_base=last, add=part)
-    return fin
+        g = split_step_phased(sp, q, p, ql, pl, sigma, eta, dt, True, qo, po, zo)
+    return qo, po, g, zo
 
 
 @pytest.mark.parametrize("M", [130, 3000, 50000])
@@ -104,9 +109,9 @@ def _phased(L, q, p, r0, n, sigma, eta, dt, want_p, want_zs, raw=False):
                                                     (0.0, True, False, True), (0.02, True, False, False),
                                                     (0.02, False, False, False)])
 def test_step_column_phases_sum(dev, M, W, eta, want_p, want_zs, raw):
-    """dicp_lddmm_euler_step_cols_f32: a slice's step in column phases (the row split's
-    overlap of the all-gather) = the one-pass slice step (dicp_lddmm_euler_step_zs_f32), fp32
-    summation order only; every rank's slice, incl. the first and last (one remote range)."""
+    """dicp_lddmm_euler_step_phase_f32: a slice's step in two column phases (the row split's
+    overlap of the all-gather: own slice, then the other points, wrapping) = the one-pass slice
+    step (dicp_lddmm_euler_step_zs_f32), fp32 summation order only; every rank's slice."""
     L = _lib()
     q, p, _, _ = _state(M, 3 * M + W, dev)
     per = -(-M // W)
@@ -118,27 +123,42 @@ def test_step_column_phases_sum(dev, M, W, eta, want_p, want_zs, raw):
         with L.coord_mode(raw):
             zs_ref = torch.empty((n, 3), device=dev) if want_zs else None
             qn, pn, g = L.euler_step_rows(q, p, r0, n, 0.1, eta, 0.1, True, want_p=want_p, zs_out=zs_ref)
-        fq, fp, fg, fz = _phased(L, q, p, r0, n, 0.1, eta, 0.1, want_p, want_zs, raw)
+        fq, fp, fg, fz = _phased(L, q, p, r, W, 0.1, eta, 0.1, want_p, want_zs, raw)
         assert rel_err(fq, qn) < 2e-6, (r, rel_err(fq, qn))
         assert rel_err(fg, g) < 2e-5, (r, rel_err(fg, g))
         if want_p:
             assert rel_err(fp, pn) < 2e-6, (r, rel_err(fp, pn))
         if want_zs:
             assert rel_err(fz, zs_ref) < 2e-5, (r, rel_err(fz, zs_ref))
-    # run to run: the same bits
-    again = _phased(L, q, p, 0, per, 0.1, eta, 0.1, want_p, want_zs, raw)
-    first = _phased(L, q, p, 0, per, 0.1, eta, 0.1, want_p, want_zs, raw)
-    assert all(a is None or torch.equal(a, b) for a, b in zip(again, first))
+    # run to run: the same bits; the outputs may be the local slice's own buffers (the shooting
+    # writes the new rows into its send buffer, which phase 0 read)
+    from difficp_amd.core.shooting import split_step_phased
+    first = _phased(L, q, p, W - 1, W, 0.1, eta, 0.1, want_p, want_zs, raw)
+    sp = _split_of(W - 1, W)
+    r0, n, _ = sp.rows(M)
+    ql, pl = q[r0:r0 + n].clone(), p[r0:r0 + n].clone()
+    zo = torch.empty((n, 3), device=dev) if want_zs else None
+    with L.coord_mode(raw):
+        g2 = split_step_phased(sp, q, p, ql, pl, 0.1, eta, 0.1, True, ql, pl if want_p else None, zo)
+    assert torch.equal(ql, first[0]) and torch.equal(g2, first[2])
+    if want_p:
+        assert torch.equal(pl, first[1])
+    if want_zs:
+        assert torch.equal(zo, first[3])
 
 
-def test_step_columns_rejects_overlap(dev):
+def test_step_phase_rejects_bad_calls(dev):
     L = _lib()
     q, p, _, _ = _state(64, 5, dev)
-    with pytest.raises(RuntimeError):
-        L.euler_step_cols(q[:32], p[:32], q, p, 0.1, 0.0, 0.1, q[:32])   # out = rows
-    with pytest.raises(RuntimeError):
-        L.euler_step_cols(q[:32], p[:32], q, p, 0.1, 0.02, 0.1, torch.empty((32, 3), device=dev),
-                          zs_out=torch.empty((32, 3), device=dev))      # zs needs eta = 0
+    ws = L.euler_step_phase_ws(32, 64, 3, dev)
+    with pytest.raises(RuntimeError):   # output inside (q, p)
+        L.euler_step_phase(1, q[:32], p[:32], q, p, 0, 32, 0.1, 0.0, 0.1, q[32:], ws=ws)
+    with pytest.raises(RuntimeError):   # zs needs eta = 0
+        L.euler_step_phase(1, q[:32].clone(), p[:32].clone(), q, p, 0, 32, 0.1, 0.02, 0.1,
+                           torch.empty((32, 3), device=dev), zs_out=torch.empty((32, 3), device=dev), ws=ws)
+    with pytest.raises(RuntimeError):   # all rows: no other points
+        L.euler_step_phase(1, q.clone(), p.clone(), q, p, 0, 64, 0.1, 0.0, 0.1,
+                           torch.empty((64, 3), device=dev), ws=L.euler_step_phase_ws(63, 64, 3, dev))
 
 
 def _free_port():

@@ -63,12 +63,12 @@ def _run(split, mode=None):
     # all-gather of step t in flight during step t+1's local phase) against one-pass steps
     from difficp_amd import _lib
     calls = [0]
-    inner = _lib.euler_step_cols
+    inner = _lib.euler_step_phase
 
     def counted(*a, **k):
         calls[0] += 1
         return inner(*a, **k)
-    _lib.euler_step_cols = counted
+    _lib.euler_step_phase = counted
     q0e, p0e, tgte = q0[:96].clone(), p0[:96].clone(), tgt[:96].clone()
     for ov in (True, False):
         LMe = LDDMMModel(sigma=0.2, D=3, lambd=100.0, version="hybrid", scheme="Euler", nt=5, spec=spec)
@@ -83,7 +83,7 @@ def _run(split, mode=None):
         res[f"ov{int(ov)}_grad"] = pe.grad.clone()
         if ov:
             res["phase_calls"] = torch.tensor(float(calls[0]))
-    _lib.euler_step_cols = inner
+    _lib.euler_step_phase = inner
     # 2. one diff-ICP iteration of a small two-set match (GMM_opt + Reg_opt(nmax=1))
     psr = workloads.build_two_set(120, torch.device("cpu"), seed=2, nt=5)
     if split:
@@ -128,7 +128,7 @@ def test_rowsplit_matches_single_process(world, mode):
     for rank, res in out:
         if mode == "verify":
             assert float(res.pop("verified")) > 0
-        # W | 96: 4 fused steps x (1 local + 1 or 2 remote phases) per shooting
+        # W | 96: 4 fused steps x 2 column phases per shooting
         assert float(res.pop("phase_calls")) >= 4 * 2
         for key in ("q1", "p1", "grad"):   # phased and one-pass steps: summation order only
             a, b = res[f"ov1_{key}"], res[f"ov0_{key}"]
