@@ -3,7 +3,7 @@
 # passes), the SQ/GRBM issue pass, and the driver-form headline (20 steps after 5 warmups)
 set -e
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r04f
+O=gpurun_out/r04z
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread > $O/gpu_tests.log 2>&1
 tail -2 $O/gpu_tests.log

@@ -1,7 +1,7 @@
 # round 4, final build (2/2): the secondary workload lines
 set -e
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r04f
+O=gpurun_out/r04z
 mkdir -p $O
 for w in two_set_50k two_set_200k two_set_50k_exact two_set_100k_2d atlas_c4 atlas_c4_fixed c5; do
   timeout -k 10 400 python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_$w.json 2> $O/bench_$w.err
