@@ -944,7 +944,9 @@ namespace {
 template <class Op>
 int step_phase_op(const char* name, int phase, const Args& a0, const Args& a1, const Scal& sc, int64_t nrows,
                   int64_t M, int64_t coff, const Outs& o, void* ws, size_t wsb, hipStream_t st) {
-  return launch_pk_phase<Op>(name, phase, phase == 0 ? a0 : a1, sc, nrows, nrows, M - nrows, coff, M, o, ws, wsb, st);
+  // phase 0 reads its nrows columns in place (no offset); phase 1 from coff, wrapping at M
+  return launch_pk_phase<Op>(name, phase, phase == 0 ? a0 : a1, sc, nrows, nrows, M - nrows,
+                             phase == 0 ? 0 : coff, phase == 0 ? nrows : M, o, ws, wsb, st);
 }
 
 struct PhaseGo {

@@ -498,6 +498,13 @@ int launch_pk_phase(const char* name, int phase, const Args& a, const Scal& sc, 
   using Base = typename Op::Base;
   if (nrows <= 0) return DICP_OK;
   if (int rc = no_batch(name)) return rc;
+  // the columns read are (coff + j) mod ntot, j < this phase's count: inside [0, ntot)
+  const int64_t nc = phase == 0 ? n0 : n1;
+  if (phase < 0 || phase > 1 || ntot <= 0 || coff < 0 || coff >= ntot || nc > ntot) {
+    set_error("%s: bad column phase (phase %d, coff %lld, ncols %lld, ntot %lld)", name, phase,
+              (long long)coff, (long long)nc, (long long)ntot);
+    return DICP_ERR_INVALID;
+  }
   int S0, S1;
   pk_phase_splits<Op>(nrows, n0, n1, S0, S1);
   const size_t need = pk_phase_ws_bytes<Op>(nrows, n0, n1);
