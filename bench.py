@@ -336,10 +336,10 @@ def _main(out):
                     help="atlas workloads: the local frames' shooting launches in lockstep batches "
                          "(core/batching.py, opt-in), --concurrent-frames groups of them on their own "
                          "HIP streams")
-    ap.add_argument("--batch-share", type=int, default=1,
-                    help="atlas: kernel geometry per frame sized as if alone (1, results bitwise the "
-                         "sequential frame loop's) or for the frame's share of the chip (0 = the "
-                         "frames per batch group / the concurrent frames)")
+    ap.add_argument("--batch-share", type=int, default=0,
+                    help="atlas: kernel geometry per frame sized for the frame's share of the chip "
+                         "(0, default: the concurrent frames / the frames per batch group), as if "
+                         "alone (1), or for 1/n of it (n)")
     ap.add_argument("--lib-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="dicp_set_option before the run (A/B experiments; repeatable)")
     ap.add_argument("--replicas", action="store_true",
@@ -463,12 +463,17 @@ def _main(out):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if prof is not None and concurrent:
-        saved = psr.concurrent_frames
+        # the frames one after another, with the kernel geometry the timed (concurrent)
+        # iterations used (batch_share 0 = the concurrent frames): the same kernels, timed alone
+        saved = psr.concurrent_frames, psr.batch_share
+        nconc = min(psr.concurrent_frames or 4, len(list(psr.frames)))
         psr.concurrent_frames = 1
+        if psr.batch_share == 0 and not getattr(psr, "batch_stats", None):
+            psr.batch_share = nconc
         with prof:
             workloads.psr_iteration(psr)
         torch.cuda.synchronize()
-        psr.concurrent_frames = saved
+        psr.concurrent_frames, psr.batch_share = saved
         prof_iters = 1
 
     if rank == 0:
@@ -516,8 +521,9 @@ def _main(out):
                     "measured_on": (("one extra iteration after the timed region with all local frames "
                                      "in ONE lockstep launch batch (the timed iterations overlap several "
                                      "batches on HIP streams)") if getattr(psr, "batch_stats", None)
-                                    else ("one extra sequential-frame iteration after the timed region "
-                                          "(the timed iterations overlap frames on HIP streams)")) if concurrent
+                                    else ("one extra sequential-frame iteration after the timed region, "
+                                          "with the timed iterations' kernel geometry (they overlap "
+                                          "frames on HIP streams)")) if concurrent
                                    else "the timed iterations",
                     "note": "pair kernels are fp32 VALU/exp-bound (O(N) bytes, O(N^2) work): "
                             "compute roofline, HBM bytes reported as alg_hbm_GBps/traffic; traffic "

@@ -240,10 +240,14 @@ class DiffPSR(MultiPSR):
         self.a0 = [None] * self.K
         self.concurrent_frames = None   # Reg_opt host threads / HIP streams (None = automatic)
         self.batch_frames = None        # Reg_opt lockstep launch batches (opt-in: True)
-        # the frames' kernel geometry when several run at once: 1 = each launch sized as if
-        # alone (results bitwise the sequential loop's), 0 = for its share of the chip (the
-        # frames per batch group, or the concurrent frames), n = for 1/n of the chip
-        self.batch_share = 1
+        # the frames' kernel geometry (library hint "batch_share"): 0 (default) = each launch
+        # sized for its share of the chip -- the concurrent frames (1 when the frames run one
+        # after another) or the frames per batch group -- which picks the 4-row kernels for
+        # 20k frames on 4 streams (csrc/lddmm_sym.hpp DICP_SYM_SHARE4_MIN_PAIRS); 1 = each
+        # launch sized as if alone; n = for 1/n of the chip, in every mode (a sequential run
+        # with n equal to the concurrent frames gives their bits: the geometry, not the
+        # concurrency, decides the fp32 summation order)
+        self.batch_share = 0
         self.initialize_a0()
 
     def initialize_a0(self, **v2p_args):
@@ -322,8 +326,13 @@ class DiffPSR(MultiPSR):
         nconc = min(int(nconc), len(frames))
         if self._batch_frames_ok(len(frames)):
             return self._optimize_frames_batched(frames, max(1, nconc), nmax, tol)
+        from .. import _lib
+        share = int(getattr(self, "batch_share", 0))
         if nconc <= 1 or self.LMi.row_split is not None:
-            return {k: self._optimize_frame(k, nmax, tol) for k in frames}
+            # one frame after another: alone on the chip unless a hint n > 1 is set
+            with _lib.thread_option(share if share > 1 and self.LMi.row_split is None else 1,
+                                    "batch_share"):
+                return {k: self._optimize_frame(k, nmax, tol) for k in frames}
         import threading
         from concurrent.futures import ThreadPoolExecutor
         main = torch.cuda.current_stream()
@@ -337,8 +346,6 @@ class DiffPSR(MultiPSR):
         lock = threading.Lock()
         free = list(streams)
 
-        from .. import _lib
-        share = int(getattr(self, "batch_share", 1))
         share = nconc if share == 0 else max(1, share)     # 0 = the concurrent frames
 
         def work(k):
@@ -396,7 +403,7 @@ class DiffPSR(MultiPSR):
             batchers.append(LaunchBatcher(st))
         owner = {k: batchers[i] for i, g in enumerate(groups) for k in g}
 
-        share = int(getattr(self, "batch_share", 1))
+        share = int(getattr(self, "batch_share", 0))
         share = per if share == 0 else max(1, share)     # 0 = the group size
 
         def work(k):

@@ -37,8 +37,10 @@ class RowSplit:
         because a collective returned different bits on different ranks.  overlap: run each
         forward step in column phases so that the all-gather of the previous step's rows
         overlaps the rank's rows against its own slice (ShootFn, split_step_phased; default
-        from DICP_ROWSPLIT_OVERLAP, on) -- a different fp32 summation order than the one-pass
-        step, the same bits on every rank."""
+        from DICP_ROWSPLIT_OVERLAP = 1 / 0 / auto, auto = from 4 ranks: per step the phases
+        cost +47 us at W = 2, -60 us at W = 4, +17 us at W = 8 against the all-gather they
+        hide, profiles/r04_rowsplit_phases.jsonl) -- a different fp32 summation order than
+        the one-pass step, the same bits on every rank."""
         import os
         self.group = group
         self.rank = dist.get_rank(group)
@@ -48,7 +50,10 @@ class RowSplit:
         self.exact_reduce = bool(int(env("DICP_ROWSPLIT_EXACT", "0"))) if exact_reduce is None \
             else bool(exact_reduce)
         self.verify = bool(int(env("DICP_ROWSPLIT_VERIFY", "0"))) if verify is None else bool(verify)
-        self.overlap = bool(int(env("DICP_ROWSPLIT_OVERLAP", "1"))) if overlap is None else bool(overlap)
+        if overlap is None:   # "auto": from 4 ranks (the measured break-even)
+            ov = env("DICP_ROWSPLIT_OVERLAP", "auto")
+            overlap = self.world >= 4 if ov == "auto" else bool(int(ov))
+        self.overlap = bool(overlap)
         self.verified_calls = 0
 
     def rows(self, M: int):

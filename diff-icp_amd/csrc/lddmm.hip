@@ -333,12 +333,13 @@ bool packed_fwd_alg() { return g_fwd_alg == 2 || g_fwd_alg == 5 || g_fwd_alg == 
 // The symmetric 4-row forward (SymFwdPk4) for this pass?  Whole passes (all rows) in scaled
 // coordinates only.  Automatic rule (fwd_alg 2), measured on MI355X (tools/probes/
 // fwd_sym4_ab.py, profiles/r04_ab_fwd_sym4.jsonl): Euler step with divergence rows 0.95x at
-// 20k, 0.90x at 50k, 1.10x at 100k and 200k -- from 75k points, or, in a launch batch
-// (batch_share > 1), when the batch has >= 2e9 pairs (as the 4-row VJP).
+// 20k, 0.90x at 50k, 1.10x at 100k and 200k -- from 75k points, or, with the geometry hint
+// batch_share > 1 (concurrent / batched frames), when the sharing calls have >= 1e9 pairs
+// (as the 4-row VJP, lddmm_sym.hpp DICP_SYM_SHARE4_MIN_PAIRS).
 bool use_sym_fwd4(int64_t M, bool all, bool raw) {
   if (!all || raw || g_fwd_alg == 6 || !(g_fwd_alg == 2 || g_fwd_alg == 5)) return false;
   if (g_fwd_alg == 5) return true;
-  if (batch_share() > 1) return M >= 8192 && (double)M * (double)M * batch_share() >= 2.0e9;
+  if (batch_share() > 1) return M >= 8192 && (double)M * (double)M * batch_share() >= DICP_SYM_SHARE4_MIN_PAIRS;
   return M >= DICP_SYM_FWD4_MIN_M;
 }
 

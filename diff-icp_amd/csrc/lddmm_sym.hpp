@@ -1099,11 +1099,20 @@ inline int& sym_rp() {
 #ifndef DICP_SYM_ROWS4_MIN_PAIRS
 #define DICP_SYM_ROWS4_MIN_PAIRS 2.0e9
 #endif
+// With a geometry hint batch_share > 1 (a launch shares the chip with the other frames'
+// launches, PSR concurrent frames): the 4-row forms from 1e9 pairs over the sharing calls --
+// the other streams' launches fill the quarter-size grids' tails.  Measured on the 32-frame
+// 20k atlas with 4 concurrent frames (profiles/r04_c4fixed_r4_*.json): 0.379 atlas it/s with
+// the 2-row forms, 0.388 with the 4-row VJP, 0.398 with the 4-row symmetric forward, 0.414
+// with both.
+#ifndef DICP_SYM_SHARE4_MIN_PAIRS
+#define DICP_SYM_SHARE4_MIN_PAIRS 1.0e9
+#endif
 inline bool sym_use_rows4(int64_t M, int nparts) {
   if (sym_rp() == 1) return false;
   if (sym_rp() == 2) return true;
-  if (batch_share() > 1)   // a batch of calls: its total pairs decide (256-point groups kept full)
-    return M >= 8192 && (double)M * (double)M * batch_share() / (double)nparts >= DICP_SYM_ROWS4_MIN_PAIRS;
+  if (batch_share() > 1)   // concurrent / batched calls: their total pairs decide
+    return M >= 8192 && (double)M * (double)M * batch_share() / (double)nparts >= DICP_SYM_SHARE4_MIN_PAIRS;
   return M >= DICP_SYM_ROWS4_MIN_M && (double)M * (double)M / (double)nparts >= DICP_SYM_ROWS4_MIN_PAIRS;
 }
 template <int D, bool GQ, bool B0, bool GT, bool RAW>

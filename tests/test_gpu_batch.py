@@ -97,8 +97,8 @@ def test_atlas_reg_opt_batched_bitwise_sequential(dev, K, N, groups, share):
     """DiffPSR.Reg_opt with the frames in lockstep launch batches == the sequential frame loop
     (PSR.py:528-569) bitwise: momenta, final trajectories and losses of every frame.
     share 0: the batched launches sized for the group (geometry hint batch_share = frames per
-    group, csrc/batch.hpp) == the sequential loop run with the same per-thread hint."""
-    from difficp_amd import _lib, workloads
+    group, csrc/batch.hpp) == the sequential loop run with the same hint."""
+    from difficp_amd import workloads
     per = -(-K // groups)
     res = {}
     for mode in ("seq", "batched"):
@@ -107,14 +107,14 @@ def test_atlas_reg_opt_batched_bitwise_sequential(dev, K, N, groups, share):
         if mode == "seq":
             psr.concurrent_frames = 1
             psr.batch_frames = False
+            psr.batch_share = per if share == 0 else 1   # the batched run's geometry
         else:
             psr.concurrent_frames = groups
             psr.batch_frames = True
             psr.batch_share = share
         psr.GMM_opt(max_iterations=3, tol=1e-3)
         FE0 = psr.FE
-        with _lib.thread_option(per if (share == 0 and mode == "seq") else 1, "batch_share"):
-            psr.Reg_opt(tol=1e-3, nmax=2)
+        psr.Reg_opt(tol=1e-3, nmax=2)
         torch.cuda.synchronize()
         res[mode] = ([a.clone() for a in psr.a0], [s.Q.clone() for s in psr.shoot], list(psr.regloss),
                      psr.FE, FE0, getattr(psr, "batch_stats", None))
