@@ -531,6 +531,17 @@ def _main(out):
                             "MI355X_MICROARCH.md; profiles/pmc_traffic.json; default workload at N=1 only) "
                             "is dominated by the deterministic partial slots (written once, read once "
                             "by the merge), ~2% of HBM bandwidth over the launch"}
+            # whole-iteration view: the algorithmic flops of every pair pass of one iteration
+            # over its wall time (host gaps, E-steps and small kernels included) -- for
+            # concurrent frames the throughput the overlapped streams reach, which the per-launch
+            # timing above (one frame's kernels alone) cannot show
+            it_flops = sum(v["pairs"] * (_lib.flops_per_pair(k, Dw) or 0) for k, v in summ.items()) / prof_iters
+            it_s = elapsed / args.steps
+            roof["aggregate_achieved"] = round(it_flops / it_s / 1e12, 3)
+            roof["aggregate_frac"] = round(it_flops / it_s / 1e12 / FP32_PEAK_TFLOPS, 4)
+            roof["aggregate_note"] = ("algorithmic flops of all pair passes of one iteration "
+                                      + ("(counted on the profiled sequential iteration) " if concurrent else "")
+                                      + "/ the timed iterations' wall time per iteration / peak")
             clk, busy = load_issue(dom) if traffic is not None else (None, None)
             if clk:
                 # the 157.3 TF/s peak assumes the 2.4 GHz peak clock; under this load the chip
