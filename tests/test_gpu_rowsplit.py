@@ -169,37 +169,40 @@ def _free_port():
     return port
 
 
-def _two_set(split):
+def _two_set(split, overlap=None):
     sys.path.insert(0, ROOT)
     from difficp_amd import workloads
     dev = torch.device("cuda:0")
     psr = workloads.build_two_set(3000, dev, seed=4, nt=5)
     if split:
-        psr.LMi.set_row_split()
+        psr.LMi.set_row_split(overlap=overlap)
     workloads.psr_iteration(psr, max_repeat_GMM=3, tol=1e-6)
     return {"FE": float(psr.FE), "a0": psr.a0[0].detach().cpu().clone(),
             "x1": psr.x1[0, 0].detach().cpu().clone()}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = _two_set(True)
+        res = _two_set(True, overlap)
         q.put((rank, res["FE"], res["a0"].numpy(), res["x1"].numpy()))
     finally:
         dist.destroy_process_group()
 
 
-def test_rowsplit_two_set_on_gpu(dev):
+@pytest.mark.parametrize("overlap", [None, True])
+def test_rowsplit_two_set_on_gpu(dev, overlap):
+    """overlap None: the default at W = 2 (one-pass steps); True: the forward steps in the two
+    column phases with the all-gather in flight (async work handles)."""
     import numpy as np
     single = _two_set(False)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=100) for _ in range(2)], key=lambda t: t[0])
@@ -211,6 +214,12 @@ def test_rowsplit_two_set_on_gpu(dev):
         assert np.abs(x1 - single["x1"].numpy()).max() < 1e-3
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])
+
+
+def _async_gather_ok(rs, t):
+    out = torch.empty_like(t)
+    rs.gather_into_async(out, t).wait()    # the current stream waits for the collective
+    return torch.equal(out, t)
 
 
 def _worker_rccl(port, q):
@@ -233,6 +242,7 @@ def _worker_rccl(port, q):
             "sum_ordered": torch.equal(rs.sum_ordered(t), t),
             "all_reduce": torch.equal(rs.all_reduce_(t.clone()), t),
             "gather_into": torch.equal(rs.gather_into(torch.empty_like(t), t), t),
+            "gather_into_async": _async_gather_ok(rs, t),
             "check_identical": rs.check_identical(t) is None and rs.verified_calls == 1,
             "gather_rows": torch.equal(rs.gather_rows([t], 4)[0][0], t),
             "gmm_gather": torch.equal(GMM._gather_rows(t, True)[0], t),
