@@ -2,7 +2,7 @@
 sizes where it runs: automatic vs forced 2 / 4 / 8, adjoint step with divergence rows and the
 gp-only step, alternating in one process (HIP events).
 
-    SIZES=100000,200000 python tools/probes/sym_L_rows4.py
+    SIZES=100000,200000 [REPS=10 ROUNDS=5 LS=0,2,4,8] python tools/probes/sym_L_rows4.py
 """
 import json
 import os
@@ -38,13 +38,16 @@ for M in [int(v) for v in os.environ.get("SIZES", "100000,200000").split(",")]:
     zs = torch.empty_like(q)
     _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs)
     fns = {"adj_zs": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs),
-           "adj_gp": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, want_lq=False, zs=zs)}
-    reps = max(2, int(2e10 / (M * M)))
+           "adj_gp": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, want_lq=False, zs=zs),
+           "adj_b0": lambda: _lib.euler_adjoint_step(q, p, ga, None, gd, 0.1, 0.0, 0.1, zs=zs)}
+    reps = int(os.environ.get("REPS", "0")) or max(2, int(2e10 / (M * M)))
+    rounds = int(os.environ.get("ROUNDS", "3"))
+    Ls = [int(v) for v in os.environ.get("LS", "0,2,4,8").split(",")]
     row = {"M": M}
     for name, fn in fns.items():
         best = {}
-        for _ in range(3):
-            for L in (0, 2, 4, 8):
+        for _ in range(rounds):
+            for L in Ls:
                 _lib.set_option("sym_L", L)
                 best[L] = min(best.get(L, 1e9), timeit(fn, reps))
         _lib.set_option("sym_L", 0)
