@@ -62,7 +62,11 @@ struct SymGeom {
 // pair-subset launch (nparts > 1, row-split over ranks) has 1/nparts of the blocks, so L
 // shrinks until a part still has >= 2048 workgroups (2 x 256 CUs x 4 resident) to fill the
 // chip; smaller L = more (shorter) blocks and more partial slots.
-inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG) {
+// Lsmall: the L below the L = 8 range -- 4, or 2 for the 4-row VJP (256-point groups), whose
+// adjoint steps measured 1.4-3.7% faster with L = 2 than 4 at 70k-100k (the zs / b0 steps;
+// tools/probes/sym_L_rows4.py, profiles/r04_ab_sym_L_rows4_reps.jsonl), equal from 140k where
+// L = 8 applies.
+inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG, int Lsmall = 4) {
   SymGeom g;
   g.M = M;
   g.nG = (int)((M + G - 1) / G);
@@ -71,10 +75,10 @@ inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG) {
   if (L <= 0) {
     // L = 8 where the chip stays full with >= 4096 workgroups (100k points: 9.6k): time
     // within 0.3% of L = 4 (r02_ab_vjp_symL_100k.json) and ~25% fewer partial slots written
-    // and merged; otherwise L = 4, halved until a launch has >= 2048 workgroups (the
+    // and merged; otherwise L = Lsmall, halved until a launch has >= 2048 workgroups (the
     // workgroup targets are this call's share of the chip: batch_share, batch.hpp)
     const double sh = (double)batch_share();
-    L = (double)g.nQ * g.nG / (2.0 * 8 * nparts) >= 4096.0 / sh ? 8 : 4;
+    L = (double)g.nQ * g.nG / (2.0 * 8 * nparts) >= 4096.0 / sh ? 8 : Lsmall;
     while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0 / sh) L /= 2;
   }
   g.L = L;
@@ -817,8 +821,10 @@ struct SymEntry {
 // W = accumulators per point (SymBwd: 2D, SymFwd: 3D with the divergence, else 2D)
 inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
   if (M <= 0) return 0;
-  const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256);  // 128 / 256-point groups
-  const int ns = g.nslot > g4.nslot ? g.nslot : g4.nslot;
+  // 128 / 256-point groups (the 4-row VJP's smaller L: more row slots)
+  const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256), g4v = sym_geom(M, nparts, 256, 2);
+  int ns = g.nslot > g4.nslot ? g.nslot : g4.nslot;
+  ns = g4v.nslot > ns ? g4v.nslot : ns;
   return (size_t)ns * (size_t)M * (size_t)W * sizeof(float);
 }
 
@@ -1189,7 +1195,7 @@ int launch_sym_bwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
   const bool gt = !(zs != nullptr || sc.dev0 == nullptr);  // pair loop with the gam terms
   const float* gd = zs != nullptr ? sc.dev0 : nullptr;
   const bool g4 = pk && sym_use_rows4(M, nparts);   // 256-point groups (fewer slots: the 128 workspace fits)
-  const SymGeom g = sym_geom(M, nparts, g4 ? kSymG4 : kSymG);
+  const SymGeom g = g4 ? sym_geom(M, nparts, kSymG4, 2) : sym_geom(M, nparts, kSymG);
   const size_t need = sym_ws_bytes(M, 2 * D, nparts);
   if (ws == nullptr || wsb < need) {
     set_error("ode_self_bwd(sym): workspace too small (%zu < %zu bytes)", wsb, need);
