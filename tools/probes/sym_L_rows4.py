@@ -2,7 +2,10 @@
 sizes where it runs: automatic vs forced 2 / 4 / 8, adjoint step with divergence rows and the
 gp-only step, alternating in one process (HIP events).
 
-    SIZES=100000,200000 [REPS=10 ROUNDS=5 LS=0,2,4,8] python tools/probes/sym_L_rows4.py
+    SIZES=100000,200000 [REPS=10 ROUNDS=5 LS=0,2,4,8 KIND=vjp|fwd|both] python tools/probes/sym_L_rows4.py
+
+(KIND=fwd: the symmetric 4-row forward's Euler step with divergence rows, which the same
+option steers.)
 """
 import json
 import os
@@ -40,6 +43,10 @@ for M in [int(v) for v in os.environ.get("SIZES", "100000,200000").split(",")]:
     fns = {"adj_zs": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs),
            "adj_gp": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, want_lq=False, zs=zs),
            "adj_b0": lambda: _lib.euler_adjoint_step(q, p, ga, None, gd, 0.1, 0.0, 0.1, zs=zs)}
+    qn, pn, zs2 = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    fwd = {"step_zs": lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, q_out=qn, p_out=pn, zs_out=zs2)}
+    kind = os.environ.get("KIND", "vjp")
+    fns = {"vjp": fns, "fwd": fwd, "both": {**fns, **fwd}}[kind]
     reps = int(os.environ.get("REPS", "0")) or max(2, int(2e10 / (M * M)))
     rounds = int(os.environ.get("ROUNDS", "3"))
     Ls = [int(v) for v in os.environ.get("LS", "0,2,4,8").split(",")]
