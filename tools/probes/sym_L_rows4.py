@@ -5,7 +5,7 @@ gp-only step, alternating in one process (HIP events).
     SIZES=100000,200000 [REPS=10 ROUNDS=5 LS=0,2,4,8 KIND=vjp|fwd|both] python tools/probes/sym_L_rows4.py
 
 (KIND=fwd: the symmetric 4-row forward's Euler step with divergence rows, which the same
-option steers.)
+option steers; SYM_RP=1/2 forces 2 / 4 rows per lane for the VJP.)
 """
 import json
 import os
@@ -18,6 +18,8 @@ from difficp_amd import _lib  # noqa: E402
 
 dev = torch.device("cuda:0")
 st = torch.cuda.current_stream()
+if os.environ.get("SYM_RP"):     # force 2 (1) or 4 (2) rows per lane
+    _lib.set_option("sym_rp", int(os.environ["SYM_RP"]))
 
 
 def timeit(fn, reps):
