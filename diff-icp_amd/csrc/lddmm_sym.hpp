@@ -23,6 +23,8 @@
 //    of group B; each wave's row sums go to slot (Q_A + 1 + k) of its group A; a merge pass
 //    adds the slots of every row in slot order and applies the Outs epilogue.
 #pragma once
+#include <cmath>
+
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
 
@@ -79,6 +81,17 @@ inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG, int Lsmall = 4
     // workgroup targets are this call's share of the chip: batch_share, batch.hpp)
     const double sh = (double)batch_share();
     L = (double)g.nQ * g.nG / (2.0 * 8 * nparts) >= 4096.0 / sh ? 8 : Lsmall;
+    if (L == 2 && Lsmall == 2 && nparts == 1 && batch_share() == 1) {
+      // the 4-row VJP alone on the chip: L = 1 when L = 2's grid ends in a markedly emptier
+      // last round of resident workgroups (4 per CU) -- 50k: 2401 workgroups = 2.34 rounds
+      // against 4802 = 4.69 for L = 1, measured 1.66 vs 1.50 ms (profiles/r04_ab_rows4_L_50k.jsonl)
+      const double cap = 4.0 * device_cus();
+      auto fill = [&](int l) {
+        const double r = (double)g.nQ * g.nG / (2.0 * l) / cap;
+        return r / std::ceil(r);
+      };
+      if (fill(1) > fill(2) + 0.1) L = 1;
+    }
     while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0 / sh) L /= 2;
   }
   g.L = L;
@@ -1088,9 +1101,9 @@ __global__ void sym_bwd_pk_kernel(Args a, Scal sc, int64_t M, int nG, int L, flo
 
 // 4 rows per lane (two float2 row pairs, 256-point groups: lddmm_sym_pk.hpp sym_pk4_body) for
 // the packed eta = 0 VJP.  dicp_set_option "sym_rp" (row pairs per lane): 1 = 2 rows, 2 = 4
-// rows, 0 = automatic -- 4 rows from DICP_SYM_ROWS4_MIN_M points when a launch (a row-split
-// part: 1/nparts of the pairs) still has >= DICP_SYM_ROWS4_MIN_PAIRS pairs; below that the
-// quarter as many workgroups leave a tail.  Measured on MI355X (tools/probes/sym_rp_ab.py,
+// rows, 0 = automatic -- whole passes from DICP_SYM_ROWS4_WHOLE_MIN_M points; row-split parts
+// from DICP_SYM_ROWS4_MIN_M points when the part (1/nparts of the pairs) still has
+// >= DICP_SYM_ROWS4_MIN_PAIRS pairs; below that the quarter as many workgroups leave a tail.  Measured on MI355X (tools/probes/sym_rp_ab.py,
 // profiles/r04_ab_sym_rp.jsonl): adjoint step with divergence rows 0.91x at 50k, 1.05x at
 // 70k, 1.07x at 90k-200k (gp-only step 1.10-1.14x); row-split parts 0.91x at 70k / 8 parts,
 // 1.03-1.15x from ~2e9 pairs per part.
@@ -1104,6 +1117,13 @@ inline int& sym_rp() {
 #endif
 #ifndef DICP_SYM_ROWS4_MIN_PAIRS
 #define DICP_SYM_ROWS4_MIN_PAIRS 2.0e9
+#endif
+// whole passes (one launch over all pairs): with the column-group rule of sym_geom (L = 2, or
+// 1 where L = 2 leaves an emptier last round) 4 rows win from 40k: adjoint step with divergence
+// rows 1.08x at 40k, 1.04x at 46k, 1.00x at 50k (L = 1), 1.08x at 52k, 1.07x at 56k, 1.08x at
+// 64k, 1.10x at 80k (profiles/r04_ab_sym_rp_L2.jsonl, r04_ab_rows4_L_50k.jsonl)
+#ifndef DICP_SYM_ROWS4_WHOLE_MIN_M
+#define DICP_SYM_ROWS4_WHOLE_MIN_M 40000
 #endif
 // With a geometry hint batch_share > 1 (a launch shares the chip with the other frames'
 // launches, PSR concurrent frames): the 4-row forms from 1e9 pairs over the sharing calls --
@@ -1119,6 +1139,7 @@ inline bool sym_use_rows4(int64_t M, int nparts) {
   if (sym_rp() == 2) return true;
   if (batch_share() > 1)   // concurrent / batched calls: their total pairs decide
     return M >= 8192 && (double)M * (double)M * batch_share() / (double)nparts >= DICP_SYM_SHARE4_MIN_PAIRS;
+  if (nparts == 1) return M >= DICP_SYM_ROWS4_WHOLE_MIN_M;
   return M >= DICP_SYM_ROWS4_MIN_M && (double)M * (double)M / (double)nparts >= DICP_SYM_ROWS4_MIN_PAIRS;
 }
 template <int D, bool GQ, bool B0, bool GT, bool RAW>

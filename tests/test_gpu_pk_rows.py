@@ -206,10 +206,11 @@ def test_vjp_four_rows_vs_two_rows(dev, M, D, raw):
 
 
 def test_vjp_rows_automatic_rule(dev):
-    """sym_rp 0 (automatic) picks 4 rows from 64k points (and 2e9 pairs per part) and 2 below: the
-    automatic result equals the forced form bitwise on each side of the threshold."""
+    """sym_rp 0 (automatic) picks 4 rows for whole passes from 40k points and 2 below (row-split
+    parts: from 64k and 2e9 pairs per part): the automatic result equals the forced form
+    bitwise on each side of the threshold (50k: the 4-row form with L = 1)."""
     L = _lib()
-    for M, want in ((20000, 1), (100000, 2)):
+    for M, want in ((20000, 1), (50000, 2), (100000, 2)):
         g = torch.Generator().manual_seed(M)
         qf = torch.rand(M, 3, generator=g).to(dev)
         pf = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
