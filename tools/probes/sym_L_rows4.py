@@ -5,7 +5,8 @@ gp-only step, alternating in one process (HIP events).
     SIZES=100000,200000 [REPS=10 ROUNDS=5 LS=0,2,4,8 KIND=vjp|fwd|both] python tools/probes/sym_L_rows4.py
 
 (KIND=fwd: the symmetric 4-row forward's Euler step with divergence rows, which the same
-option steers; SYM_RP=1/2 forces 2 / 4 rows per lane for the VJP.)
+option steers; SYM_RP=1/2 forces 2 / 4 rows per lane for the VJP; FWD_ALG=5/6 the symmetric
+4-row / the ordered forward.)
 """
 import json
 import os
@@ -20,6 +21,8 @@ dev = torch.device("cuda:0")
 st = torch.cuda.current_stream()
 if os.environ.get("SYM_RP"):     # force 2 (1) or 4 (2) rows per lane
     _lib.set_option("sym_rp", int(os.environ["SYM_RP"]))
+if os.environ.get("FWD_ALG"):    # 5 = symmetric 4-row forward, 6 = ordered
+    _lib.set_option("fwd_alg", int(os.environ["FWD_ALG"]))
 
 
 def timeit(fn, reps):
