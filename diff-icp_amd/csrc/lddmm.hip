@@ -328,12 +328,14 @@ namespace {
 // rows always)
 bool packed_fwd_alg() { return g_fwd_alg == 2 || g_fwd_alg == 5 || g_fwd_alg == 6; }
 #ifndef DICP_SYM_FWD4_MIN_M
-#define DICP_SYM_FWD4_MIN_M 75000
+#define DICP_SYM_FWD4_MIN_M 20000
 #endif
 // The symmetric 4-row forward (SymFwdPk4) for this pass?  Whole passes (all rows) in scaled
-// coordinates only.  Automatic rule (fwd_alg 2), measured on MI355X (tools/probes/
-// fwd_sym4_ab.py, profiles/r04_ab_fwd_sym4.jsonl): Euler step with divergence rows 0.95x at
-// 20k, 0.90x at 50k, 1.10x at 100k and 200k -- from 75k points, or, with the geometry hint
+// coordinates only.  Automatic rule (fwd_alg 2), measured on MI355X: with the column groups
+// of sym_geom's wg_min 4096 rule the Euler step with divergence rows is 1.03x the ordered
+// pass at 20k, 1.10x at 40k, 1.01x at 50k, 1.07x at 60k, 1.10x at 80k-200k
+// (tools/probes/sym_L_rows4.py KIND=fwd, profiles/r04_ab_fwd4_L_small.jsonl; with L = 4 it lost
+// below 75k: r04_ab_fwd_sym4.jsonl) -- from 20k points, or, with the geometry hint
 // batch_share > 1 (concurrent / batched frames), when the sharing calls have >= 1e9 pairs
 // (as the 4-row VJP, lddmm_sym.hpp DICP_SYM_SHARE4_MIN_PAIRS).
 bool use_sym_fwd4(int64_t M, bool all, bool raw) {

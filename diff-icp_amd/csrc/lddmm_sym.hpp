@@ -32,6 +32,7 @@ namespace dicp {
 
 constexpr int kSymG = 128;   // points per group (= rows of one wave)
 constexpr int kSymQ = 4;     // row groups (waves) per workgroup
+constexpr int kSymFwd4WgMin = 4096;   // sym_geom wg_min of the symmetric 4-row forward
 // column groups per workgroup: dicp_set_option "sym_L" forces a value; 0 = automatic
 inline int& sym_L() {
   static int L = 0;
@@ -68,7 +69,10 @@ struct SymGeom {
 // adjoint steps measured 1.4-3.7% faster with L = 2 than 4 at 70k-100k (the zs / b0 steps;
 // tools/probes/sym_L_rows4.py, profiles/r04_ab_sym_L_rows4_reps.jsonl), equal from 140k where
 // L = 8 applies.
-inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG, int Lsmall = 4) {
+// wg_min: the halving below Lsmall stops once a launch has that many workgroups (2048; 4096
+// for the symmetric 4-row forward, whose column groups measured best at L = 1 up to 60k,
+// L = 2 at 80k, L = 4 at 100k -- profiles/r04_ab_fwd4_L_small.jsonl).
+inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG, int Lsmall = 4, int wg_min = 2048) {
   SymGeom g;
   g.M = M;
   g.nG = (int)((M + G - 1) / G);
@@ -92,7 +96,7 @@ inline SymGeom sym_geom(int64_t M, int nparts = 1, int G = kSymG, int Lsmall = 4
       };
       if (fill(1) > fill(2) + 0.1) L = 1;
     }
-    while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < 2048.0 / sh) L /= 2;
+    while (L > 1 && (double)g.nQ * g.nG / (2.0 * L * nparts) < (double)wg_min / sh) L /= 2;
   }
   g.L = L;
   g.Kmax = (g.nG + g.L - 1) / g.L;
@@ -835,9 +839,11 @@ struct SymEntry {
 inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
   if (M <= 0) return 0;
   // 128 / 256-point groups (the 4-row VJP's smaller L: more row slots)
-  const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256), g4v = sym_geom(M, nparts, 256, 2);
+  const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256), g4v = sym_geom(M, nparts, 256, 2),
+                g4f = sym_geom(M, nparts, 256, 4, kSymFwd4WgMin);
   int ns = g.nslot > g4.nslot ? g.nslot : g4.nslot;
   ns = g4v.nslot > ns ? g4v.nslot : ns;
+  ns = g4f.nslot > ns ? g4f.nslot : ns;
   return (size_t)ns * (size_t)M * (size_t)W * sizeof(float);
 }
 
@@ -993,7 +999,7 @@ int launch_sym_fwd4(const Args& a, const Scal& sc, int64_t M, const Outs& o, voi
                     hipStream_t st, bool zs) {
   using S = SymFwd<D, DIV>;
   if (M <= 0) return DICP_OK;
-  const SymGeom g = sym_geom(M, 1, 256);
+  const SymGeom g = sym_geom(M, 1, 256, 4, kSymFwd4WgMin);
   const size_t need = sym_ws_bytes(M, S::W);
   if (ws == nullptr || wsb < need) {
     set_error("ode_self_fwd(sym4): workspace too small (%zu < %zu bytes)", wsb, need);

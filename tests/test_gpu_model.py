@@ -184,18 +184,25 @@ def test_concurrent_frames_bitwise_equal_sequential(dev):
 def test_euler_step_without_momentum_update(dev, M, eta):
     """euler_step(want_p=False) (p_next = NULL at the C-ABI: the Gs' sums skipped) gives
     bitwise the q_next and g of the full step: the mG-less pass keeps the full pass's column
-    splits (packed.hpp OpOdeSelfFwdPk::SplitAs)."""
+    splits (packed.hpp OpOdeSelfFwdPk::SplitAs).  The ordered forward (fwd_alg 6): whole eta = 0
+    passes from 20k points otherwise take the symmetric 4-row pass for the full step, whose
+    fp32 summation order differs."""
     from difficp_amd import _lib as L
     g = torch.Generator().manual_seed(M + 21)
     q = torch.rand(M, 3, generator=g).to(dev)
     p = (0.05 * torch.randn(M, 3, generator=g)).to(dev)
-    for want_div in (False, True):
-        qn, pn, gd = L.euler_step(q, p, 0.1, eta, 0.1, want_div)
-        qn1, none, gd1 = L.euler_step(q, p, 0.1, eta, 0.1, want_div, want_p=False)
-        assert none is None and pn is not None
-        assert torch.equal(qn1, qn)
-        if want_div or eta:
-            assert torch.equal(gd1, gd)
+    old = L.get_option("fwd_alg")
+    L.set_option("fwd_alg", 6)
+    try:
+        for want_div in (False, True):
+            qn, pn, gd = L.euler_step(q, p, 0.1, eta, 0.1, want_div)
+            qn1, none, gd1 = L.euler_step(q, p, 0.1, eta, 0.1, want_div, want_p=False)
+            assert none is None and pn is not None
+            assert torch.equal(qn1, qn)
+            if want_div or eta:
+                assert torch.equal(gd1, gd)
+    finally:
+        L.set_option("fwd_alg", old)
 
 
 @pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])

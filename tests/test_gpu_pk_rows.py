@@ -277,10 +277,11 @@ def test_forward_sym4_vs_ordered(dev, M, D):
 
 
 def test_forward_automatic_rule(dev):
-    """fwd_alg 2 (default) runs the ordered rows below 75k points and the symmetric 4-row pass
-    from 75k on (whole passes): bitwise fwd_alg 6 / fwd_alg 5 on each side."""
+    """fwd_alg 2 (default) runs the ordered rows below 20k points and the symmetric 4-row pass
+    from 20k on (whole passes; L = 1 at 20k-50k, 4 at 100k): bitwise fwd_alg 6 / fwd_alg 5 on
+    each side."""
     L = _lib()
-    for M, want in ((50000, 6), (100000, 5)):
+    for M, want in ((12000, 6), (20000, 5), (50000, 5), (100000, 5)):
         q, p = _case(M, 3, M)
         qf, pf = q.float().to(dev), p.float().to(dev)
         res = {}
