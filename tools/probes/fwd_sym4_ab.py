@@ -1,5 +1,5 @@
 """A/B of the symmetric 4-row forward (fwd_alg 5) against the packed ordered forward
-(fwd_alg 2) on the forms the shooting runs: the Euler step writing the divergence rows
+(fwd_alg 6), and the automatic choice (fwd_alg 2), on the forms the shooting runs: the Euler step writing the divergence rows
 (step_zs, the t >= 1 steps), the first step (ode_self_fwd with zs), the mG-less last step
 (step_nog), alternating in one process, HIP events; agreement of the step outputs.
 
@@ -42,15 +42,15 @@ for M in [int(v) for v in os.environ.get("SIZES", "20000,50000,100000,200000").s
     row = {"M": M}
     for name, fn in fns.items():
         best, outs = {}, {}
-        for alg in (2, 5):
+        for alg in (6, 5, 2):
             _lib.set_option("fwd_alg", alg)
             outs[alg] = [t.clone() for t in fn() if isinstance(t, torch.Tensor)] + [zs.clone()]
         for _ in range(3):
-            for alg in (2, 5):
+            for alg in (6, 5, 2):
                 _lib.set_option("fwd_alg", alg)
                 best[alg] = min(best.get(alg, 1e9), timeit(fn, reps))
         _lib.set_option("fwd_alg", 2)
-        err = max(float((a - b).norm() / max(float(b.norm()), 1e-30)) for a, b in zip(outs[5], outs[2]))
-        row[name] = {"ordered_ms": round(best[2], 4), "sym4_ms": round(best[5], 4),
-                     "speedup": round(best[2] / best[5], 4), "rel_err": err}
+        err = max(float((a - b).norm() / max(float(b.norm()), 1e-30)) for a, b in zip(outs[5], outs[6]))
+        row[name] = {"ordered_ms": round(best[6], 4), "sym4_ms": round(best[5], 4),
+                     "auto_ms": round(best[2], 4), "speedup": round(best[6] / best[5], 4), "rel_err": err}
     print(json.dumps(row), flush=True)
