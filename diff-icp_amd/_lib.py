@@ -142,7 +142,7 @@ USE_ZS = os.environ.get("DICP_ZS", "1") != "0"
 def zs_ok(eta) -> bool:
     """Whether the fused Euler steps can hand divergence rows from the forward to the VJP
     (eta = 0 with a packed forward -- fwd_alg 2, the default: ordered rows or, for whole passes
-    from 75k points, symmetric 4-row; 5: symmetric 4-row; 6: ordered rows -- and the packed
+    from 20k points, symmetric 4-row; 5: symmetric 4-row; 6: ordered rows -- and the packed
     symmetric VJP)."""
     return USE_ZS and eta == 0 and get_option("fwd_alg") in (2, 5, 6) and get_option("bwd_alg") == 3
 

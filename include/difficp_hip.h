@@ -366,8 +366,9 @@ int dicp_supports_dim(int D);
 /* Tuning / A-B knobs (process-wide unless stated; results of every setting agree to fp32
  * summation order):
  *   "fwd_alg"      eta = 0 ODE forward: 0 ordered rows, 1 symmetric pair-once, 2 packed-FP32
- *                  (default: ordered packed rows, and for whole passes from 75k points -- or a
- *                  launch batch of >= 2e9 pairs -- the symmetric pass of 5), 3 channel
+ *                  (default: ordered packed rows, and for whole passes from 20k points -- or,
+ *                  under a "batch_share" hint, >= 1e9 pairs over the sharing calls -- the
+ *                  symmetric pass of 5; its mG-less form stays ordered), 3 channel
  *                  contraction on the matrix cores (opt-in; fp32 error bounded by the rows'
  *                  spread: pass a spatial row_order), 4 symmetric pair-once with packed-FP32
  *                  rows, 5 symmetric pair-once with 4 packed rows per lane and packed column
@@ -383,8 +384,9 @@ int dicp_supports_dim(int D);
  *                  forward and the packed external-point / KRed passes from 32k rows and 8k
  *                  columns, else 1), 1 or 2 forced
  *   "sym_rp"       packed symmetric eta = 0 VJP: row pairs per lane, 0 automatic (2, i.e. 4 rows
- *                  in 256-point groups, from 64k points when a launch or row-split part has
- *                  >= 2e9 pairs; else 1), 1 or 2 forced
+ *                  in 256-point groups, for whole passes from 40k points, for row-split parts
+ *                  from 64k points with >= 2e9 pairs per part, under a "batch_share" hint from
+ *                  1e9 pairs over the sharing calls; else 1), 1 or 2 forced
  *   "red_alg"      KBase / KRedScal / KRed / GradKRed and the external-point forward: 0 never
  *                  the centred expansion, 1 automatic by size (default), 2 always
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
