@@ -195,7 +195,7 @@ def cpu_baseline(pair_counts, M_work, D=3):
     return base
 
 
-def kernel_sum_probe(dev, M, reps=5):
+def kernel_sum_probe(dev, M, reps=5, same=True):
     """The north_star's "100k x 100k 3D Gaussian kernel sum": KRed (kernel.py:138,
     X_i = sum_j K(x_i - y_j) b_j) at M x M on this GPU, HIP events on the launch stream, best of
     `reps`.  Reported beside the compute roofline because the north_star quotes this sum
@@ -206,13 +206,14 @@ def kernel_sum_probe(dev, M, reps=5):
     g = torch.Generator(device="cpu").manual_seed(1)
     x = torch.rand(M, 3, generator=g).to(dev)
     b = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
+    y = x if same else torch.rand(M, 3, generator=g).to(dev)
     st = torch.cuda.current_stream(dev)
-    _lib.gauss_red(_lib.KRED, x, x, 0.1, b=b)
+    _lib.gauss_red(_lib.KRED, x, y, 0.1, b=b)
     best = None
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        _lib.gauss_red(_lib.KRED, x, x, 0.1, b=b)
+        _lib.gauss_red(_lib.KRED, x, y, 0.1, b=b)
         e1.record(st)
         e1.synchronize()
         ms = e0.elapsed_time(e1)
@@ -226,7 +227,8 @@ def kernel_sum_probe(dev, M, reps=5):
             "per pair, 4 rows per thread packed in pairs, prep pass included in the time)"
             if _lib.get_option("red_alg") and M >= 32768 and float(M) * M >= 2.5e9
             else "packed scaled-coordinate kernel (ext_pk.hpp)")
-    return {"op": "KRed (kernel.py:138) x = y, D = 3, sigma 0.1", "M": M, "ms": round(best, 4),
+    return {"op": f"KRed (kernel.py:138) {'x = y' if same else 'x != y (two independent clouds)'}, D = 3, sigma 0.1",
+            "M": M, "ms": round(best, 4),
             "path": path, "Tpair_per_s": round(pairs / s / 1e12, 3),
             "tflops": round(pairs * fl / s / 1e12, 2), "frac_fp32_peak": round(pairs * fl / s / 1e12 / FP32_PEAK_TFLOPS, 4),
             "compute_bound_ms": round(bound_s * 1e3, 4),
@@ -442,8 +444,10 @@ def _main(out):
                   (psr.concurrent_frames is None or psr.concurrent_frames > 1))
     prof = _lib.KernelProfile() if not args.no_profile else None
     prof_iters = args.steps
+    from difficp_amd.tools import runstats
     barrier()
     torch.cuda.synchronize()
+    rs0 = runstats.snapshot()
     t0 = time.perf_counter()
     if prof is not None and not concurrent:
         with prof:
@@ -455,13 +459,25 @@ def _main(out):
             workloads.psr_iteration(psr)
             log(f"[rank {rank}] step {i} FE={psr.FE:.6g}")
     torch.cuda.synchronize()
+    t_done = time.perf_counter() - t0       # this rank's own work (before waiting for the others)
+    rs1 = runstats.snapshot()
     barrier()
     elapsed = time.perf_counter() - t0
+    # per-rank diagnostics of the timed region (a first multi-GPU line that misses its target
+    # must say why: uneven work, closures, time inside the collectives)
+    mine = {"rank": rank, "work_s": round(t_done, 4), "frames": len(list(getattr(psr, "frames", [0]))),
+            **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in runstats.delta(rs0, rs1).items()}}
+    if prof is not None and not concurrent:
+        mine["kernel_busy_s"] = round(sum(v["ms"] for v in prof.summary().values()) * 1e-3, 4)
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
     if prof is not None and concurrent:
         # the frames one after another, with the kernel geometry the timed (concurrent)
         # iterations used (batch_share 0 = the concurrent frames): the same kernels, timed alone
@@ -548,17 +564,23 @@ def _main(out):
                 # runs at the DVFS clock GRBM_GUI_ACTIVE reports (profiles/pmc_issue.json)
                 roof["pmc_eff_clock_GHz"] = round(clk, 3)
                 roof["pmc_valu_issue_busy"] = round(busy, 3) if busy else None
-                roof["frac_at_eff_clock"] = round(achieved / (FP32_PEAK_TFLOPS * clk / 2.4), 4)
+                # the EXECUTED flops (hot-loop instruction count, exec_flops_per_pair) against
+                # the peak at that clock: the algorithmic count prices work the pair-once
+                # kernels do not execute, so its ratio to the clock-scaled peak can exceed 1
+                if efpp and fpp:
+                    roof["frac_executed_at_eff_clock"] = round(
+                        achieved * efpp / fpp / (FP32_PEAK_TFLOPS * clk / 2.4), 4)
         base = None
         if not args.no_cpu_baseline and world == 1 and pair_counts:
             try:
                 base = cpu_baseline(pair_counts, min(wl["N"], 50000), D=wl.get("D", 3))
             except Exception as e:  # baseline is informative; never fail the bench on it
                 base = {"error": repr(e)}
-        ksum = None
+        ksum = ksum_xy = None
         if world == 1 and wl.get("N") == 100000 and wl.get("D", 3) == 3:
             try:
                 ksum = kernel_sum_probe(dev, wl["N"])
+                ksum_xy = kernel_sum_probe(dev, wl["N"], same=False)
             except Exception as e:  # informative; never fail the bench on it
                 ksum = {"error": repr(e)}
         tot_ms = sum(v["ms"] for v in summ.values())
@@ -566,6 +588,19 @@ def _main(out):
                      if tot_ms > 0 else None)
         if getattr(psr, "batch_stats", None):
             cfg["batch_stats_last_reg_opt"] = psr.batch_stats
+        if rehearse:
+            cfg["parallelism"] = (cfg["parallelism"].replace("RCCL", "gloo")
+                                  + " -- REHEARSAL: every rank on cuda:0 over gloo, not RCCL")
+        works = [r["work_s"] for r in ranks]
+        per_rank = {"ranks": ranks,
+                    "work_s_max_over_min": round(max(works) / max(min(works), 1e-9), 4),
+                    "closures_max_over_min": (round(max(r["closures"] for r in ranks)
+                                                    / max(min(r["closures"] for r in ranks), 1), 4)),
+                    "note": "per rank over the timed steps: work_s = time to its own last kernel "
+                            "(before the closing barrier), closures = L-BFGS loss evaluations, "
+                            "em_steps, collectives (count) and collective_s (host wall time inside "
+                            "the blocking ones: the exchange plus waiting for the slowest rank), "
+                            "kernel_busy_s = summed kernel time (timed iterations only)"}
         line = {
             "metric": METRIC, "value": round(value, 5), "unit": "PSR iterations/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -574,6 +609,8 @@ def _main(out):
             "config": cfg, "roofline": roof, "cpu_baseline": base,
             "kernel_sum_hbm_GBps": kern_gbps,
             "kernel_sum_100k": ksum,
+            "kernel_sum_100k_xy": ksum_xy,
+            "per_rank": per_rank,
             "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                             "Gpairs": round(v["pairs"] / 1e9, 3)} for k, v in summ.items()},
         }

@@ -28,6 +28,7 @@ from torch.nn.functional import log_softmax, softmax
 
 from .. import _lib
 from ..tools.point_sets import intrinsic_scale
+from ..tools import runstats
 from ..tools.spec import defspec
 
 _LOG2E = 1.4426950408889634
@@ -50,7 +51,8 @@ def _gather_rows(t, comm):
     import torch.distributed as dist
     W = dist.get_world_size(_group(comm))
     out = [torch.empty_like(t) for _ in range(W)]
-    dist.all_gather(out, t.contiguous(), group=_group(comm))
+    with runstats.collective():
+        dist.all_gather(out, t.contiguous(), group=_group(comm))
     return torch.stack(out, 0)
 
 
@@ -337,6 +339,7 @@ class GaussianMixtureUnif(torch.nn.Module):
             return torch.empty(X.shape, **defspec), torch.tensor(0.0), torch.tensor(0.0), 0
         Y, Cfe, FE, last_FE = None, None, None, None
         for i in range(max_iterations):
+            runstats.add("em_steps")
             Y, Cfe, FE = self.EM_step(X)
             if last_FE is not None and tol is not None and abs(FE - last_FE) < tol * abs(last_FE):
                 return Y, Cfe, FE, i + 1

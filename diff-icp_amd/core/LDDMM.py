@@ -257,7 +257,8 @@ class LDDMMModel:
             with _lib.coord_mode(raw):
                 complete_p1(shoot.Q, shoot.P, self.Kernel.sigma, float(self.eta),
                             bool(self.withlogdet), int(self.nt),
-                            order=order_l if split is not None else order, split=split)
+                            order=order_l if split is not None else order, split=split,
+                            C=shoot.C)
             shoot.p1_missing = False
             shoot.q0_key = None
         return shoot

@@ -23,6 +23,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..tools import runstats
+
 
 class RowSplit:
     """Rank / world of a torch.distributed process group (RCCL over xGMI on the GPU box,
@@ -66,10 +68,11 @@ class RowSplit:
     def all_gather(self, local: torch.Tensor) -> torch.Tensor:
         """(W * n,) concatenation of every rank's (n,) buffer, in rank order."""
         out = torch.empty(self.world * local.numel(), device=local.device, dtype=local.dtype)
-        if self._gather_base:
-            dist.all_gather_into_tensor(out, local, group=self.group)
-        else:
-            dist.all_gather(list(out.chunk(self.world)), local, group=self.group)
+        with runstats.collective():
+            if self._gather_base:
+                dist.all_gather_into_tensor(out, local, group=self.group)
+            else:
+                dist.all_gather(list(out.chunk(self.world)), local, group=self.group)
         return out
 
     def gather_into(self, out: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
@@ -79,10 +82,11 @@ class RowSplit:
         flat = out.view(-1)
         if flat.numel() != self.world * local.numel():
             raise ValueError("gather_into: out must hold W x local elements")
-        if self._gather_base:
-            dist.all_gather_into_tensor(flat, local.reshape(-1), group=self.group)
-        else:
-            dist.all_gather(list(flat.chunk(self.world)), local.reshape(-1), group=self.group)
+        with runstats.collective():
+            if self._gather_base:
+                dist.all_gather_into_tensor(flat, local.reshape(-1), group=self.group)
+            else:
+                dist.all_gather(list(flat.chunk(self.world)), local.reshape(-1), group=self.group)
         return out
 
     def gather_into_async(self, out: torch.Tensor, local: torch.Tensor):
@@ -92,6 +96,7 @@ class RowSplit:
         flat = out.view(-1)
         if flat.numel() != self.world * local.numel():
             raise ValueError("gather_into_async: out must hold W x local elements")
+        runstats.add("collectives")
         if self._gather_base:
             return dist.all_gather_into_tensor(flat, local.reshape(-1), group=self.group, async_op=True)
         return dist.all_gather(list(flat.chunk(self.world)), local.reshape(-1), group=self.group,
@@ -114,7 +119,8 @@ class RowSplit:
         if self.exact_reduce:
             t.copy_(self.sum_ordered(t))
         else:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            with runstats.collective():
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         if self.verify:
             self.check_identical(t)
         return t

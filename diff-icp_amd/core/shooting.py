@@ -293,10 +293,21 @@ def split_step_phased(split, Qt, Pt, q_loc, p_loc, sigma, eta, dt, want_div, q_o
     return g_out
 
 
-def complete_p1(Q, P, sigma, eta, want_div, nt, order=None, split=None):
+def last_cost_step(C, Gd, nt, dt):
+    """C[nt] = C[nt-1] + dt sum_i g_i(nt-1) of a fused Euler shooting: the last step's
+    increment as its own reduction (of row nt-1 of the (nt, M) divergence rows Gd), so a
+    completion (complete_p1) that re-runs the last step forms it with the same bits."""
+    inc = Gd[nt - 1:nt].sum(1, keepdim=True).mul_(dt)
+    torch.add(C[nt - 1], inc[0], out=C[nt])
+
+
+def complete_p1(Q, P, sigma, eta, want_div, nt, order=None, split=None, C=None):
     """Form P[nt] of a trajectory shot with need_p1=False: the last Euler step again, by the
     same fused pass a full shooting uses (bitwise the P[nt] it would have produced; row split:
-    each rank's slice, one all-gather)."""
+    each rank's slice, one all-gather).  Single device: Q[nt] and (with C) the cost C[nt] are
+    rewritten from that pass too -- the mG-less pass of the need_p1=False step may run another
+    kernel (the ordered rows where a full pass takes the symmetric 4-row forward, other column
+    splits), so the completed trajectory is bitwise a fresh full shooting's."""
     with torch.no_grad():
         if split is not None:
             M = Q.shape[1]
@@ -314,9 +325,18 @@ def complete_p1(Q, P, sigma, eta, want_div, nt, order=None, split=None):
             (pn,), _ = split.gather_rows([pn_l], M)
             P[nt].copy_(pn)
             return
-        scratch = torch.empty_like(Q[nt])
-        _lib.euler_step(Q[nt - 1], P[nt - 1], sigma, eta, 1.0 / nt, want_div, q_out=scratch,
-                        p_out=P[nt], order=order)
+        M, D = Q.shape[1], Q.shape[2]
+        # the full step exactly as ShootFn's fused loop issues it: divergence rows into row
+        # nt-1 of an (nt, M) buffer (same alignment as the forward's Gd), zs rows when the
+        # forward keeps them (the zs variant is another kernel)
+        use_zs = bool(want_div) and nt >= 2 and _lib.zs_ok(eta)
+        Gd = torch.empty((nt, M), device=Q.device, dtype=Q.dtype) if want_div else None
+        zs = torch.empty((M, D), device=Q.device, dtype=Q.dtype) if use_zs else None
+        _lib.euler_step(Q[nt - 1], P[nt - 1], sigma, eta, 1.0 / nt, want_div, q_out=Q[nt],
+                        p_out=P[nt], g_out=Gd[nt - 1] if want_div else None, order=order,
+                        zs_out=zs)
+        if C is not None and want_div:
+            last_cost_step(C, Gd, nt, 1.0 / nt)
 
 
 class ShootFn(torch.autograd.Function):
@@ -570,10 +590,14 @@ class ShootFn(torch.autograd.Function):
                 C[2:].copy_(C[1].expand(nt - 1, 1))
         if fused_from is not None:
             # cost of the fused steps: C[t+1] = C[t] + dt sum_i g_i(t), one reduction + scan
+            # over the steps before the last, the last step's increment on its own
+            # (last_cost_step: complete_p1 re-forms it from the full pass bit for bit)
             if want_div:
-                inc = Gd[fused_from:].sum(1, keepdim=True).mul_(dt)
-                torch.cumsum(inc, 0, out=C[fused_from + 1:])
-                C[fused_from + 1:].add_(C[fused_from])
+                if fused_from < nt - 1:
+                    inc = Gd[fused_from:nt - 1].sum(1, keepdim=True).mul_(dt)
+                    torch.cumsum(inc, 0, out=C[fused_from + 1:nt])
+                    C[fused_from + 1:nt].add_(C[fused_from])
+                last_cost_step(C, Gd, nt, dt)
             else:
                 C[fused_from + 1:].copy_(C[fused_from].expand(nt - fused_from, 1))
         ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x = \

@@ -4,9 +4,10 @@
 //      :296 NDsigma2 with the OLD mu, :303 Y, :312-314 Cfe terms)
 //   M  (rows c, cols n): log sum_n gamma_nc and the gamma-weighted mean of x  (GMM.py:287, :293)
 //   T  (rows n, cols c): targets / free-energy sums with OLD gamma, NEW mu, w  (GMM.py:303-314)
-// LSE passes use the exact row maximum (first sweep, no exp) and then one exp2 per pair
-// (second sweep), all in the log2 domain; column chunks (split mode) carry (max, sum, acc)
-// partials merged with max-rescaling in chunk order -> deterministic, no atomics.
+// LSE passes make one exp2 sweep per pair, shifted by the maximum of the chunk's first column
+// tile (re-referenced on a much larger logit), all in the log2 domain; column chunks (split
+// mode) carry (shift, sum, acc) partials merged with max-rescaling in a fixed order ->
+// deterministic, no atomics.
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
 
@@ -15,11 +16,21 @@ using namespace dicp;
 namespace {
 
 constexpr int kRG = 2;  // rows per thread
+// more column-chunk partials per row than this: the one-wave-per-row merge
+constexpr int kWaveMergeMinSplits = 64;
 
 // ---------------------------------------------------------------------------------------
 // LSE row-reduction skeleton: part[(s*M + i)*(2+NACC) + ...] = {m, l, acc...} with
-// m = max_j t_ij (log2 domain), l = sum_j 2^(t_ij - m), acc = Op::accum weighted sums.
+// m = the chunk's shift (log2 domain), l = sum_j 2^(t_ij - m), acc = Op::accum weighted sums.
+// One exp2 sweep: the shift m is the exact maximum of the chunk's FIRST tile of columns (one
+// logit-only pass over <= 256 columns), and a later logit above m + kLseSlack (rare: a
+// component much closer than any of the first tile's) re-references the row's sums to it.
+// Terms up to 2^kLseSlack above the shift are summed as they are (no overflow: l stays below
+// 2^(kLseSlack + 30) for 10^9 columns).  Round 4 swept all columns twice (exact maximum, then
+// the exps): the logit, 8 of the E-step's ~25 VALU per pair, was paid twice.
 // ---------------------------------------------------------------------------------------
+constexpr float kLseSlack = 64.f;
+
 template <class Op, int R>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
                                                             int64_t M, int64_t N, int64_t chunk,
@@ -41,13 +52,14 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   int64_t j1 = j0 + chunk;
   if (j1 > N) j1 = N;
 
-  // sweep 1: exact row maximum of the logits over this chunk
+  // the shift: exact maximum of the logits over the chunk's first tile
   float m[R];
+  bool none[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) m[r] = -__builtin_huge_valf();
-  for (int64_t jt = j0; jt < j1; jt += kTile) {
-    const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
-    if (tid < cnt) Op::load_col(args, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+  if (j0 < j1) {
+    const int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
+    if (tid < cnt) Op::load_col(args, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
     __syncthreads();
 #pragma unroll 2
     for (int t = 0; t < cnt; ++t) {
@@ -58,23 +70,28 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
         m[r] = fmaxf(m[r], Op::logit(sc, row[r], rec, aux));
       }
     }
-    __syncthreads();
   }
-  // guard: an all -inf chunk contributes nothing (stored max stays -inf, merge skips it)
-  float ms[R];
+  // an all -inf first tile (dead components only): shift 0, as the exact-maximum form did;
+  // a chunk with no finite logit at all stores -inf (the merge skips it)
 #pragma unroll
-  for (int r = 0; r < R; ++r) ms[r] = (m[r] == -__builtin_huge_valf()) ? 0.f : m[r];
+  for (int r = 0; r < R; ++r) {
+    none[r] = m[r] == -__builtin_huge_valf();
+    if (none[r]) m[r] = 0.f;
+  }
 
-  // sweep 2: one exp2 per pair
   float tot[R][NACC + 1];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int k = 0; k <= NACC; ++k) tot[r][k] = 0.f;
+  bool first = true;   // the first tile is already in LDS
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
-    if (tid < cnt) Op::load_col(args, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
-    __syncthreads();
+    if (!first) {
+      if (tid < cnt) Op::load_col(args, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+      __syncthreads();
+    }
+    first = false;
     float acc[R][NACC + 1];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -86,7 +103,24 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         float aux;
-        const float tm = Op::logit(sc, row[r], rec, aux) - ms[r];
+        const float lg = Op::logit(sc, row[r], rec, aux);
+        float tm = lg - m[r];
+        if (tm > kLseSlack) {   // re-reference this row's sums to the new shift lg
+          const float f = fast_exp2(-tm);
+#pragma unroll
+          for (int k = 0; k <= NACC; ++k) {
+            float a = acc[r][k], b = tot[r][k];
+            if (Op::kShifted >= 0 && k == Op::kShifted + 1) {   // sum e (t - m): t - m' = (t - m) - tm
+              a = fmaf(-tm, acc[r][0], a);
+              b = fmaf(-tm, tot[r][0], b);
+            }
+            acc[r][k] = f * a;
+            tot[r][k] = f * b;
+          }
+          m[r] = lg;
+          none[r] = false;
+          tm = 0.f;
+        }
         const float e = fast_exp2(tm);
         acc[r][0] += e;
         Op::accum(sc, row[r], rec, tm, aux, e, acc[r] + 1);
@@ -103,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
     const int64_t i = ibase + (int64_t)r * kBlock;
     if (i >= M) continue;
     float* dst = part + ((int64_t)blockIdx.y * M + i) * W;
-    dst[0] = m[r];
+    dst[0] = none[r] ? -__builtin_huge_valf() : m[r];
 #pragma unroll
     for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[r][k];
   }
@@ -136,6 +170,72 @@ __global__ __launch_bounds__(kBlock) void lse_finalize_kernel(const float* __res
     }
   }
   Op::finalize(sc, i, mx, l, acc, outs);
+}
+
+// Many chunk partials per row (the M-step: C = 256-512 component rows against 10^5-10^6
+// points, so ~10^3 column chunks fill the chip): one wave per row, each lane merging a strided
+// share of the chunks, then a fixed xor tree across the lanes.  (The one-thread-per-row merge
+// above reads the S partials of a row one after the other: at S ~ 1250 that latency chain,
+// not the pair pass, was the M-step's time.)  Deterministic: fixed shares, fixed tree.
+template <int NACC, int kShifted>
+struct LsePart {
+  float m, l, a[NACC > 0 ? NACC : 1];
+  __device__ void clear() {
+    m = -__builtin_huge_valf();
+    l = 0.f;
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) a[k] = 0.f;
+  }
+  // this <- this (+) (m2, l2, a2), both referenced to their own maxima
+  __device__ void merge(float m2, float l2, const float* a2) {
+    if (m2 == -__builtin_huge_valf()) return;
+    if (m == -__builtin_huge_valf()) {
+      m = m2;
+      l = l2;
+#pragma unroll
+      for (int k = 0; k < NACC; ++k) a[k] = a2[k];
+      return;
+    }
+    const float mn = fmaxf(m, m2);
+    const float f1 = fast_exp2(m - mn), f2 = fast_exp2(m2 - mn);
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) {
+      float x1 = a[k], x2 = a2[k];
+      if (k == kShifted) {  // re-reference sum e (t - m_s) to the merged maximum
+        x1 = fmaf(m - mn, l, x1);
+        x2 = fmaf(m2 - mn, l2, x2);
+      }
+      a[k] = fmaf(f1, x1, f2 * x2);
+    }
+    l = fmaf(f1, l, f2 * l2);
+    m = mn;
+  }
+};
+
+template <class Op>
+__global__ __launch_bounds__(kBlock) void lse_finalize_wave_kernel(const float* __restrict__ part,
+                                                                   int64_t M, int S, Scal sc,
+                                                                   Outs outs) {
+  constexpr int NACC = Op::NACC;
+  constexpr int W = 2 + NACC;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (i >= M) return;  // whole wave leaves together
+  LsePart<NACC, Op::kShifted> acc;
+  acc.clear();
+  for (int s = lane; s < S; s += 64) {
+    const float* p = part + ((int64_t)s * M + i) * W;
+    acc.merge(p[0], p[1], p + 2);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    float a2[NACC > 0 ? NACC : 1];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) a2[k] = __shfl_xor(acc.a[k], off, 64);
+    const float m2 = __shfl_xor(acc.m, off, 64), l2 = __shfl_xor(acc.l, off, 64);
+    acc.merge(m2, l2, a2);
+  }
+  if (lane == 0) Op::finalize(sc, i, acc.m, acc.l, acc.a, outs);
 }
 
 // ---- E-step op ------------------------------------------------------------------------
@@ -303,8 +403,13 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
       a, sc, M, N, chunk, part);
   int rc = check_launch(name);
   if (rc) return rc;
-  const int64_t nb = (M + kBlock - 1) / kBlock;
-  lse_finalize_kernel<Op><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(part, M, S, sc, fin);
+  if (S > kWaveMergeMinSplits) {
+    const int64_t nw = (M + kBlock / 64 - 1) / (kBlock / 64);
+    lse_finalize_wave_kernel<Op><<<dim3((unsigned)nw), dim3(kBlock), 0, st>>>(part, M, S, sc, fin);
+  } else {
+    const int64_t nb = (M + kBlock - 1) / kBlock;
+    lse_finalize_kernel<Op><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(part, M, S, sc, fin);
+  }
   return check_launch(name);
 }
 

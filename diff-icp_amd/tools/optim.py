@@ -9,6 +9,7 @@ import math
 
 import torch
 
+from . import runstats
 from .lbfgs import CompactLBFGS
 
 
@@ -38,6 +39,7 @@ def LBFGS_optimization(p0, lossfunc, nmax=10, tol=1e-3, errthresh=1e8, generator
     optimizer.on_loss = lambda Ld: record(Ld)
 
     def closure():
+        runstats.add("closures")
         optimizer.zero_grad()
         if lossgrad is not None:
             L, grads = lossgrad(*p)

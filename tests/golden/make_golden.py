@@ -433,6 +433,109 @@ def chui_case():
     print("chui", os.path.getsize(os.path.join(HERE, "chui_ex3.npz")), "bytes")
 
 
+def multi_inputs(case):
+    """Inputs of the multi-structure traces (diffICP_full.py:37-97 style): K = 3 frames x S = 3
+    structures, each structure a noisy sample of its own curve of C centres, warped per frame
+    by a smooth field, one structure of one frame EMPTY (the case diffICP_full.py:94-97 leaves
+    commented out).  Seeded, float64; also used by tests/multi_case.py (via the stored arrays)."""
+    import torch
+    f64 = torch.float64
+    D = 2 if case == "m2d" else 3
+    g = torch.Generator().manual_seed(41 if D == 2 else 43)
+    t = torch.linspace(0, 2 * np.pi, 13, dtype=f64)[:-1]
+    curves = [torch.stack((0.5 + 0.4 * (t / 7) * t.cos(), 0.5 + 0.3 * t.sin()), 1),
+              torch.stack((1 + 0.4 * t.cos(), 0.5 + 0.4 * t.sin()), 1),
+              torch.stack((0.8 + 0.1 * (t - np.pi), -0.06 * (t - np.pi)), 1)]
+    if D == 3:
+        curves = [torch.cat((c, (0.2 * s + 0.1 * torch.sin(t + s))[:, None]), 1) for s, c in enumerate(curves)]
+    sig = [0.025, 0.04, 0.06]
+    empty = (1, 2) if D == 2 else (2, 0)
+    x = []
+    for k in range(3):
+        fr = []
+        amp = 0.02 * (1 + k)
+        for s in range(3):
+            if (k, s) == empty:
+                fr.append(torch.empty(0, D, dtype=f64))
+                continue
+            n = int(torch.randint(25, 40, (1,), generator=g))
+            lab = torch.randint(0, 12, (n,), generator=g)
+            pts = curves[s][lab] + sig[s] * torch.randn(n, D, generator=g, dtype=f64)
+            perm = [(d + 1) % D for d in range(D)]
+            fr.append((pts + amp * torch.sin(2 * np.pi * pts[:, perm])).contiguous())
+        x.append(fr)
+    return x
+
+
+def multi_case():
+    """Multi-structure diff-ICP traces (MultiPSR with S > 1: one GMM per structure, targets
+    concatenated per frame across structures, per-structure sigma in the quadratic loss,
+    PSR.py:197-271, 498-516, 521-569), float64, torch path, dense support, 2 iterations of
+    GMM_opt(10, tol 1e-3) + Reg_opt(nmax=1, tol 1e-3):
+      m2d: 2D, hybrid LDDMM sigma 0.2 lambda 5e2 (diffICP_full.py:131-134), ONE GMM (C = 12,
+           mu / sigma / w optimised) copied per structure, reinitialize_GMM (seed 5);
+      m3d: 3D, classic LDDMM sigma 0.25 lambda 1e2, a LIST of GMMs with C = 6 / 10 / 8:
+           structure 1 with sigma fixed, structure 2 with the outlier component.
+    The randn draws of reinitialize_GMM are recorded (mu_init / sigma_init per structure)."""
+    import torch
+    K, L, G, P = import_reference()
+    f64 = torch.float64
+    spec64 = {"device": "cpu", "dtype": f64}
+    out = {}
+    for case in ("m2d", "m3d"):
+        x = multi_inputs(case)
+        D = x[0][0].shape[1] if x[0][0].shape[0] else x[0][1].shape[1]
+        if case == "m2d":
+            GMMi = G.GaussianMixtureUnif(torch.zeros(12, D, dtype=f64), computversion="torch", spec=spec64)
+            GMMi.to_optimize = {"mu": True, "sigma": True, "w": True, "eta0": False}
+            LM = L.LDDMMModel(sigma=0.2, D=D, lambd=5e2, version="hybrid", scheme="Euler", nt=10,
+                              computversion="torch", spec=spec64)
+        else:
+            GMMi = []
+            for s, C in enumerate((6, 10, 8)):
+                gm = G.GaussianMixtureUnif(torch.zeros(C, D, dtype=f64), use_outliers=(s == 2),
+                                           computversion="torch", spec=spec64)
+                gm.to_optimize = {"mu": True, "sigma": s != 1, "w": True, "eta0": True}
+                if s == 1:
+                    gm.sigma = 0.05
+                GMMi.append(gm)
+            LM = L.LDDMMModel(sigma=0.25, D=D, lambd=1e2, version="classic", scheme="Euler", nt=10,
+                              computversion="torch", spec=spec64)
+        PS = P.DiffPSR(x, GMMi, LM, dataspec=spec64, compspec=spec64)
+        PS.printstuff = False
+        torch.manual_seed(5)
+        PS.reinitialize_GMM()
+        for k in range(3):
+            for s in range(3):
+                out[f"{case}/x0_{k}_{s}"] = x[k][s].numpy()
+        for s in range(3):
+            out[f"{case}/mu_init_{s}"] = PS.GMMi[s].mu.numpy()
+            out[f"{case}/sigma_init_{s}"] = np.array(float(PS.GMMi[s].sigma))
+        out[f"{case}/FE_init"] = np.array(float(PS.FE))
+        for it in range(2):
+            PS.GMM_opt(max_iterations=10, tol=1e-3)
+            out[f"{case}/it{it}/FE_gmm"] = np.array(float(PS.FE))
+            for s in range(3):
+                gm = PS.GMMi[s]
+                out[f"{case}/it{it}/mu_{s}"] = gm.mu.numpy()
+                out[f"{case}/it{it}/w_{s}"] = gm.w.numpy()
+                out[f"{case}/it{it}/sigma_{s}"] = np.array(float(gm.sigma))
+                out[f"{case}/it{it}/Cfe_{s}"] = np.array(float(PS.Cfe[s]))
+                if gm.outliers:
+                    out[f"{case}/it{it}/eta0_{s}"] = np.array(float(gm.outliers["eta0"]))
+            PS.Reg_opt(tol=1e-3, nmax=1)
+            out[f"{case}/it{it}/FE_reg"] = np.array(float(PS.FE))
+            out[f"{case}/it{it}/quadloss"] = np.array(PS.quadloss, dtype=np.float64)
+            out[f"{case}/it{it}/regloss"] = np.array([float(r) for r in PS.regloss])
+            for k in range(3):
+                out[f"{case}/it{it}/a0_{k}"] = PS.a0[k].detach().numpy()
+                for s in range(3):
+                    out[f"{case}/it{it}/x1_{k}_{s}"] = PS.x1[k, s].detach().numpy()
+            print("multi", case, "it", it, float(PS.FE), [float(g.sigma) for g in PS.GMMi])
+    np.savez_compressed(os.path.join(HERE, "multi.npz"), **out)
+    print("multi", os.path.getsize(os.path.join(HERE, "multi.npz")), "bytes")
+
+
 if __name__ == "__main__":
     only = sys.argv[2] if sys.argv[1:2] == ["--only"] else None
     if only is None:
@@ -447,3 +550,5 @@ if __name__ == "__main__":
         chui_case()
     if only in (None, "red_large"):
         reductions_large()
+    if only in (None, "multi"):
+        multi_case()

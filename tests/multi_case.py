@@ -1,0 +1,106 @@
+"""Multi-structure diff-ICP traces (tests/golden/multi.npz, make_golden.multi_case) replayed
+through the product API: K = 3 frames x S = 3 structures with one empty structure, one GMM
+per structure, targets concatenated per frame across structures and the per-structure sigma
+in the quadratic loss (/root/reference/diffICP/core/PSR.py:197-271, 498-516, 521-569)."""
+import os
+
+import numpy as np
+import torch
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "multi.npz")
+CASES = ("m2d", "m3d")
+
+
+def build(spec, case, z):
+    """The DiffPSR of make_golden.multi_case, with reinitialize_GMM's draws injected."""
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    T = lambda k: torch.from_numpy(np.asarray(z[k])).to(dtype=spec["dtype"], device=spec["device"])
+    x = [[T(f"{case}/x0_{k}_{s}") for s in range(3)] for k in range(3)]
+    D = x[0][1].shape[1]
+    if case == "m2d":
+        GMMi = GaussianMixtureUnif(torch.zeros(12, D), spec=spec)
+        GMMi.to_optimize = {"mu": True, "sigma": True, "w": True, "eta0": False}
+        LM = LDDMMModel(sigma=0.2, D=D, lambd=5e2, version="hybrid", scheme="Euler", nt=10, spec=spec)
+    else:
+        GMMi = []
+        for s, C in enumerate((6, 10, 8)):
+            gm = GaussianMixtureUnif(torch.zeros(C, D), use_outliers=(s == 2), spec=spec)
+            gm.to_optimize = {"mu": True, "sigma": s != 1, "w": True, "eta0": True}
+            if s == 1:
+                gm.sigma = 0.05
+            GMMi.append(gm)
+        LM = LDDMMModel(sigma=0.25, D=D, lambd=1e2, version="classic", scheme="Euler", nt=10, spec=spec)
+    PS = DiffPSR(x, GMMi, LM, dataspec=spec, compspec=spec)
+    PS.printstuff = False
+    for s in range(3):
+        PS.GMMi[s].mu = T(f"{case}/mu_init_{s}")
+        PS.GMMi[s].sigma = float(z[f"{case}/sigma_init_{s}"])
+    PS.update_GMM_targets()
+    return PS
+
+
+def run_multi(spec, case, iters=2, check=None):
+    """check(stage, it, PS, z) after init ("init"), each GMM_opt ("gmm") and Reg_opt ("reg")."""
+    z = np.load(GOLD)
+    PS = build(spec, case, z)
+    check("init", -1, PS, z)
+    for it in range(iters):
+        PS.GMM_opt(max_iterations=10, tol=1e-3)
+        check("gmm", it, PS, z)
+        PS.Reg_opt(tol=1e-3, nmax=1)
+        check("reg", it, PS, z)
+    return PS
+
+
+def deviations(PS, z, case, stage, it):
+    """Relative deviations of PS from the golden trace at (stage, it): a dict of named
+    scalars (free energy; per-structure mu / w / sigma / eta0 after GMM_opt; per (frame,
+    structure) x1 and per-frame a0 after Reg_opt)."""
+    from conftest import rel_err
+    out = {}
+    fe = float(z[f"{case}/it{it}/FE_{stage}"])
+    out["fe"] = abs(PS.FE - fe) / abs(fe)
+    if stage == "gmm":
+        for s in range(3):
+            g = PS.GMMi[s]
+            t = lambda n: torch.from_numpy(z[f"{case}/it{it}/{n}_{s}"])
+            out[f"mu{s}"] = rel_err(g.mu.detach().cpu().double(), t("mu"))
+            out[f"w{s}"] = float((g.w.detach().cpu().double() - t("w")).abs().max())
+            out[f"sigma{s}"] = abs(g.sigma - float(z[f"{case}/it{it}/sigma_{s}"])) / float(z[f"{case}/it{it}/sigma_{s}"])
+            out[f"Cfe{s}"] = abs(float(PS.Cfe[s]) - float(z[f"{case}/it{it}/Cfe_{s}"])) / abs(float(z[f"{case}/it{it}/Cfe_{s}"]))
+            if g.outliers:
+                out[f"eta0{s}"] = abs(float(g.outliers["eta0"]) - float(z[f"{case}/it{it}/eta0_{s}"]))
+    else:
+        for k in range(3):
+            out[f"a0{k}"] = rel_err(PS.a0[k].detach().cpu().double(), torch.from_numpy(z[f"{case}/it{it}/a0_{k}"]))
+            for s in range(3):
+                ref = torch.from_numpy(z[f"{case}/it{it}/x1_{k}_{s}"])
+                got = PS.x1[k, s].detach().cpu().double()
+                assert got.shape == ref.shape, (k, s, got.shape, ref.shape)
+                out[f"x1_{k}{s}"] = rel_err(got, ref) if ref.numel() else 0.0
+        q = np.asarray(z[f"{case}/it{it}/quadloss"])
+        out["quadloss"] = float(np.abs(np.asarray(PS.quadloss, dtype=np.float64) - q).max() / np.abs(q).max())
+    return out
+
+
+def group(name):
+    """'mu2' -> 'mu', 'x1_01' -> 'x1', 'a00' -> 'a0', 'eta02' -> 'eta0'."""
+    for g in ("x1", "a0", "eta0", "quadloss", "fe", "Cfe", "sigma", "mu", "w"):
+        if name.startswith(g):
+            return g
+    raise KeyError(name)
+
+
+# Worst float32 deviation of the oracle-backed host logic from the float64 trace over the 2
+# iterations, per quantity group (measured by test_host_logic.py::
+# test_multi_structure_fp32_oracle_deviation, rounded up by ~10%; eta0 is absolute, the
+# others relative).  L-BFGS with a strong-Wolfe line search amplifies fp32 rounding into a0
+# (SURVEY 7(c)); the GPU test allows max(1e-4, 2 x these).
+FP32_DEV = {
+    "m2d": {"fe": 1.0e-5, "mu": 3.5e-5, "w": 3.1e-4, "sigma": 4.0e-5, "Cfe": 1.7e-5,
+            "a0": 5.1e-3, "x1": 2.2e-4, "quadloss": 4.6e-4},
+    "m3d": {"fe": 2.2e-4, "mu": 3.9e-4, "w": 4.5e-3, "sigma": 7.7e-4, "Cfe": 4.2e-4,
+            "eta0": 3.4e-2, "a0": 3.9e-3, "x1": 7.7e-4, "quadloss": 1.3e-3},
+}

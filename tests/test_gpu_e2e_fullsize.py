@@ -24,15 +24,15 @@ pytestmark = pytest.mark.gpu
 SIG, LAM, NT = 0.1, 1e3, 10
 
 
-def _case(M, dev):
+def _case(M, dev, amp=2e-6):
     from difficp_amd import workloads
     _, xB = workloads.two_set_points(M, seed=3)
     q0 = xB.double().to(dev)
     g = torch.Generator().manual_seed(M)
     ph = torch.rand(3, generator=g, dtype=torch.float64).to(dev)
-    # a smooth momentum field (coherent over a kernel width, as L-BFGS iterates are), sized so
-    # the displacement is ~0.1 sigma on this dense cloud (~1.5k points per sigma-ball)
-    p0 = 2e-6 * torch.sin(2 * math.pi * (q0[:, [1, 2, 0]] + ph))
+    # a smooth momentum field (coherent over a kernel width, as L-BFGS iterates are); the
+    # default amplitude gives a ~0.1 sigma displacement at 100k (~1.5k points per sigma-ball)
+    p0 = amp * torch.sin(2 * math.pi * (q0[:, [1, 2, 0]] + ph))
     y = q0 + 0.01 * torch.sin(2 * math.pi * q0[:, [2, 0, 1]])
     return q0, p0, y
 
@@ -41,16 +41,40 @@ def _tol(r64, r32):
     return max(1e-5, 2 * rel_err(r32, r64))
 
 
+# (M, version, displacement): "small" = the fixed amplitude 2e-6 (~0.1 sigma at 100k, less at
+# smaller M); a number = max |q1 - q0| / sigma the momentum is scaled to (a realistic L-BFGS
+# iterate of the bench, whose synthetic warp is 0.3 sigma).  "logdet" is the exact
+# ICP_two_set model (gradcomponent=True, eta = 1/lambda: ICP_two_set.py:203-207,
+# LDDMM.py:34, 198-203) through the default symmetric eta != 0 VJP.
+CASES = [(20000, "hybrid", "small"), (50000, "hybrid", "small"), (100000, "hybrid", "small"),
+         (20000, "hybrid", 0.5), (50000, "hybrid", 0.5),
+         (20000, "logdet", "small"), (50000, "logdet", "small"), (20000, "logdet", 0.5),
+         (50000, "logdet", 0.5)]
+
+
+def _amplitude(M, disp, dev):
+    """Momentum amplitude giving a max displacement of disp sigma (one fp64 forward probe:
+    the displacement of a 10-step Euler shooting is linear in the amplitude to first order,
+    and one rescale lands within a few % of the target)."""
+    if disp == "small":
+        return 2e-6
+    q0, p0, _ = _case(M, dev, 1e-6)
+    v, _, _ = F.ode_full(q0, p0, SIG, 0.0, True)
+    return 1e-6 * disp * SIG / float(v.norm(dim=1).max())
+
+
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("M", [20000, 50000, 100000])
-def test_shoot_and_gradient_fullsize(dev, M):
+@pytest.mark.parametrize("M,version,disp", CASES, ids=[f"{m}-{v}-{d}" for m, v, d in CASES])
+def test_shoot_and_gradient_fullsize(dev, M, version, disp):
     from difficp_amd.core.LDDMM import LDDMMModel
-    q0, p0, y = _case(M, dev)
-    kw = dict(rows=2048, chunk=8192)
+    q0, p0, y = _case(M, dev, _amplitude(M, disp, dev))
+    eta = 1.0 / LAM if version == "logdet" else 0.0
+    kw = dict(rows=2048, chunk=8192, eta=eta)
     r64 = F.shoot_loss_grad_p0(q0, p0, SIG, NT, LAM, y, **kw)
     r32 = F.shoot_loss_grad_p0(q0.float(), p0.float(), SIG, NT, LAM, y.float(), **kw)
-    LM = LDDMMModel(sigma=SIG, D=3, lambd=LAM, version="hybrid", scheme="Euler", nt=NT,
+    LM = LDDMMModel(sigma=SIG, D=3, lambd=LAM, version=version, scheme="Euler", nt=NT,
                     spec={"device": dev, "dtype": torch.float32})
+    assert LM.eta == eta
     LM.shoot_cache = None
     p = p0.float().contiguous().requires_grad_(True)
     sh = LM.Shoot(q0.float().contiguous(), p, need_p1=False)
@@ -66,6 +90,7 @@ def test_shoot_and_gradient_fullsize(dev, M):
         a64 = a64.detach().reshape(h.shape).cpu()
         a32 = a32.detach().reshape(h.shape).cpu()
         report[n] = (rel_err(h.cpu(), a64), _tol(a64, a32))
-    print("e2e", M, {k: (f"{e:.2e}", f"{t:.2e}") for k, (e, t) in report.items()})
+    disp_sig = float((r64[0].reshape(q0.shape) - q0).norm(dim=1).max()) / SIG
+    print("e2e", M, version, f"disp {disp_sig:.3f} sigma", {k: (f"{e:.2e}", f"{t:.2e}") for k, (e, t) in report.items()})
     for n, (e, t) in report.items():
         assert e <= t, (n, e, t, report)

@@ -1,0 +1,55 @@
+"""EM passes on inputs that exercise the single-sweep LSE's re-referencing (csrc/gmm.hip
+lse_rowred_kernel): the shift of a column chunk is the maximum of its FIRST tile (256
+columns), so rows whose nearby columns all come later must re-reference their sums.
+
+  * E-step (rows = points, columns = components): the first 256 components sit far from the
+    points of one cluster (~2^-1000 of the near ones);
+  * M-step (rows = components, columns = points): the first points are far from the
+    components of the other cluster;
+  * the wave-per-row merge of many column chunks (the M-step at the atlas shape).
+
+Criterion: err vs the float64 oracle (oracle/torch_ref.py em_step, pinned by the
+reference's EM goldens) <= max(2e-5, 2 x the float32 oracle's own deviation)."""
+import pytest
+import torch
+
+from conftest import rel_err
+from oracle import torch_ref as R
+
+pytestmark = pytest.mark.gpu
+
+OPT = {"mu": True, "w": True, "sigma": True, "eta0": False}
+
+
+def _two_clusters(N, C, far, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.cat([torch.tensor([far, far, far]) + 0.05 * torch.randn(N // 2, 3, generator=g),
+                   0.05 * torch.randn(N - N // 2, 3, generator=g)])
+    mu = torch.cat([torch.tensor([far, far, far]) + 0.05 * torch.randn(C // 2, 3, generator=g),
+                    0.05 * torch.randn(C - C // 2, 3, generator=g)])
+    # E-step: the first 256 components are the far cluster's; M-step: the first N/2 points
+    return X.to(dev), mu.to(dev)
+
+
+@pytest.mark.parametrize("N,C,far,sigma", [(4000, 600, 3.0, 0.05), (3000, 520, 1.0, 0.2),
+                                           (200000, 512, 2.0, 0.03)])
+def test_em_rescaled_shift(dev, N, C, far, sigma):
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    X, mu0 = _two_clusters(N, C, far, dev)
+    GM = GaussianMixtureUnif(mu0, sigma=sigma, spec={"device": dev, "dtype": torch.float32})
+    GM.to_optimize = dict(OPT)
+    st64 = dict(mu=mu0.double(), w=torch.zeros(C, dtype=torch.float64, device=dev), sigma=sigma)
+    st32 = dict(mu=mu0.clone(), w=torch.zeros(C, device=dev), sigma=sigma)
+    for it in range(2):
+        Y, Cfe, FE = GM.EM_step(X)
+        Y64, Cfe64, FE64, n64 = R.em_step(X.double(), st64["mu"], st64["w"], st64["sigma"], OPT)
+        Y32, Cfe32, FE32, n32 = R.em_step(X, st32["mu"], st32["w"], st32["sigma"], OPT)
+        tol = lambda a32, a64: max(2e-5, 2 * rel_err(a32, a64))
+        assert rel_err(Y, Y64) < tol(Y32, Y64), (it, rel_err(Y, Y64))
+        assert rel_err(GM.mu, n64["mu"]) < tol(n32["mu"], n64["mu"]), it
+        assert rel_err(GM.w, n64["w"]) < tol(n32["w"], n64["w"]), (it, rel_err(GM.w, n64["w"]))
+        assert abs(GM.sigma - n64["sigma"]) < max(1e-5, 2 * abs(n32["sigma"] - n64["sigma"]) / n64["sigma"]) * n64["sigma"]
+        for a, a64, a32 in ((float(FE), float(FE64), float(FE32)), (float(Cfe), float(Cfe64), float(Cfe32))):
+            assert abs(a - a64) <= max(2e-5, 2 * abs(a32 - a64) / abs(a64)) * abs(a64), (it, a, a64, a32)
+        st64, st32 = n64, n32
+        assert torch.isfinite(GM.w).all() and torch.isfinite(Y).all()

@@ -205,28 +205,33 @@ def test_euler_step_without_momentum_update(dev, M, eta):
         L.set_option("fwd_alg", old)
 
 
-@pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])
-def test_optimize_final_shoot_complete(dev, version):
+@pytest.mark.parametrize("version,M,D", [("classic", 1000, 2), ("hybrid", 1000, 2), ("logdet", 1000, 2),
+                                         ("hybrid", 25000, 3), ("classic", 25000, 3)])
+def test_optimize_final_shoot_complete(dev, version, M, D):
     """LDDMMModel.Optimize's loss closures shoot with need_p1=False (the final momenta are
     never read by the loss); the shoot it returns is completed and equals, bitwise, a fresh
-    full shooting at the returned p0 (trajectory, cost and final momenta)."""
+    full shooting at the returned p0 (trajectory, cost and final momenta), and so do the
+    returned trajl / datal (LDDMM.py:390-398).  From 20k points a full pass takes the symmetric
+    4-row forward while the closures' mG-less last step keeps the ordered rows:
+    the completion re-forms Q[nt] and C[nt] from the full pass."""
     from difficp_amd.core.LDDMM import LDDMMModel
     g = torch.Generator().manual_seed(5)
-    M = 1000    # (the logdet cost is unbounded below on this toy cloud: kept small, lambda 1e3)
-    q0 = torch.rand(M, 2, generator=g).to(dev)
-    p0 = torch.zeros(M, 2, device=dev)
-    tgt = (torch.rand(M, 2, generator=g) * 0.1).to(dev) + q0
-    LM = LDDMMModel(sigma=0.1, D=2, lambd=1e3, version=version, scheme="Euler", nt=6,
+    # (the logdet cost is unbounded below on this toy cloud: kept small, lambda 1e3)
+    q0 = torch.rand(M, D, generator=g).to(dev)
+    p0 = torch.zeros(M, D, device=dev)
+    tgt = (torch.rand(M, D, generator=g) * 0.1).to(dev) + q0
+    LM = LDDMMModel(sigma=0.1, D=D, lambd=1e3, version=version, scheme="Euler", nt=6,
                     spec={"device": dev, "dtype": torch.float32})
     sh0 = LM.Shoot(q0, p0, need_p1=False)
     assert sh0.p1_missing and torch.isnan(sh0.P[-1]).all()
-    p, shoot, trajl, datal, nsteps, change = LM.Optimize(
-        lambda q: ((q - tgt) ** 2).sum(), q0, p0, nmax=4)
+    loss = lambda q: ((q - tgt) ** 2).sum()
+    p, shoot, trajl, datal, nsteps, change = LM.Optimize(loss, q0, p0, nmax=4 if M < 5000 else 2)
     assert not getattr(shoot, "p1_missing", False)
     LM.shoot_cache = None
     ref = LM.Shoot(q0, p)
     assert torch.equal(shoot.Q, ref.Q) and torch.equal(shoot.P, ref.P)
     assert torch.equal(shoot.C, ref.C)
+    assert trajl == LM.trajloss(ref).item() and datal == loss(ref[-1][0]).item()
 
 
 @pytest.mark.gpu

@@ -518,3 +518,65 @@ def test_shoot_loss_grad_bitwise_autograd(fake, version):
     a, b = res["autograd"], res["manual"]
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
     assert a[3:] == b[3:]
+
+
+@pytest.mark.parametrize("case", ["m2d", "m3d"])
+def test_multi_structure_trace_host_logic_fp64(fake, case):
+    """Multi-structure diff-ICP (S = 3 structures incl. one empty, one GMM per structure --
+    a shared copy in m2d, a list with a fixed sigma and an outlier component in m3d;
+    PSR.py:197-271, 498-516, 521-569) replayed in float64 with oracle-backed kernels against
+    the reference's float64 trace (tests/golden/multi.npz), 2 iterations."""
+    import multi_case
+    spec = {"device": "cpu", "dtype": torch.float64}
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            assert abs(PS.FE - float(z[f"{case}/FE_init"])) < 1e-9 * abs(float(z[f"{case}/FE_init"]))
+            return
+        dev = multi_case.deviations(PS, z, case, stage, it)
+        worst = max(dev.values())
+        assert worst < 1e-6, (stage, it, dev)
+    multi_case.run_multi(spec, case, iters=2, check=check)
+
+
+def test_multi_structure_reinitialize_gmm_draws(fake):
+    """reinitialize_GMM (PSR.py:143-167) draws one randn(C, D) per structure in structure
+    order from the global generator: seeded as make_golden.multi_case, the float64 host
+    logic reproduces the reference's drawn centroids and sigmas exactly."""
+    import numpy as np
+    import multi_case
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    from difficp_amd.core.LDDMM import LDDMMModel
+    from difficp_amd.core.PSR import DiffPSR
+    z = np.load(multi_case.GOLD)
+    spec = {"device": "cpu", "dtype": torch.float64}
+    x = [[torch.from_numpy(z[f"m2d/x0_{k}_{s}"]) for s in range(3)] for k in range(3)]
+    GM = GaussianMixtureUnif(torch.zeros(12, 2, dtype=torch.float64), spec=spec)
+    GM.to_optimize = {"mu": True, "sigma": True, "w": True, "eta0": False}
+    LM = LDDMMModel(sigma=0.2, D=2, lambd=5e2, version="hybrid", scheme="Euler", nt=10, spec=spec)
+    PS = DiffPSR(x, GM, LM, dataspec=spec, compspec=spec)
+    PS.printstuff = False
+    torch.manual_seed(5)
+    PS.reinitialize_GMM()
+    for s in range(3):
+        assert torch.allclose(PS.GMMi[s].mu, torch.from_numpy(z[f"m2d/mu_init_{s}"]), rtol=0, atol=1e-14)
+        assert abs(PS.GMMi[s].sigma - float(z[f"m2d/sigma_init_{s}"])) < 1e-14
+    assert abs(PS.FE - float(z["m2d/FE_init"])) < 1e-9 * abs(float(z["m2d/FE_init"]))
+
+
+@pytest.mark.parametrize("case", ["m2d", "m3d"])
+def test_multi_structure_fp32_oracle_deviation(fake, case):
+    """The float32 deviation of the oracle-backed host logic from the float64 multi-structure
+    trace; test_gpu_multi.py takes 2 x this (the SURVEY 8c criterion) per quantity."""
+    import multi_case
+    worst = {}
+
+    def check(stage, it, PS, z):
+        if stage == "init":
+            return
+        for k, v in multi_case.deviations(PS, z, case, stage, it).items():
+            worst[k] = max(worst.get(k, 0.0), v)
+    multi_case.run_multi({"device": "cpu", "dtype": torch.float32}, case, iters=2, check=check)
+    print(case, {k: f"{v:.3g}" for k, v in worst.items()})
+    for k, v in worst.items():
+        assert v <= multi_case.FP32_DEV[case][multi_case.group(k)], (k, v)
