@@ -465,7 +465,7 @@ def _main(out):
     elapsed = time.perf_counter() - t0
     # per-rank diagnostics of the timed region (a first multi-GPU line that misses its target
     # must say why: uneven work, closures, time inside the collectives)
-    mine = {"rank": rank, "work_s": round(t_done, 4), "frames": len(list(getattr(psr, "frames", [0]))),
+    mine = {"rank": rank, "FE": psr.FE, "work_s": round(t_done, 4), "frames": len(list(getattr(psr, "frames", [0]))),
             **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in runstats.delta(rs0, rs1).items()}}
     if prof is not None and not concurrent:
         mine["kernel_busy_s"] = round(sum(v["ms"] for v in prof.summary().values()) * 1e-3, 4)
@@ -592,7 +592,7 @@ def _main(out):
             cfg["parallelism"] = (cfg["parallelism"].replace("RCCL", "gloo")
                                   + " -- REHEARSAL: every rank on cuda:0 over gloo, not RCCL")
         works = [r["work_s"] for r in ranks]
-        per_rank = {"ranks": ranks,
+        per_rank = {"ranks": ranks, "FE_identical_on_all_ranks": len({r["FE"] for r in ranks}) == 1,
                     "work_s_max_over_min": round(max(works) / max(min(works), 1e-9), 4),
                     "closures_max_over_min": (round(max(r["closures"] for r in ranks)
                                                     / max(min(r["closures"] for r in ranks), 1), 4)),

@@ -2,6 +2,7 @@
 // Morton codes, stable rocPRIM radix sort, one wave per 64-column sub-tile building the
 // records) and the main row pass with the usual deterministic split-column merge.
 #include "centred.hpp"
+#include "sym_cx.hpp"
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -175,6 +176,70 @@ int launch_cx(const char* name, const float* x, int64_t M, Args a, int64_t N, do
   return DICP_OK;
 }
 
+int& sym_red() {
+  static int v = 1;
+  return v;
+}
+
+namespace {
+
+template <int D, int OPK>
+size_t scx_ws(int64_t M) {
+  if (M <= 0) return 0;
+  const SymGeom g = sym_geom(M, 1, kScG, 4, kSymFwd4WgMin);
+  return cx_layout(M, 3, (int64_t)g.nslot * M * scx_w<D, OPK>).total;
+}
+
+// Pair-once centred sum (sym_cx.hpp) of rows = columns = x (M, D); f: the column fields
+// (KRedScal: d (M,), KRed: b (M, D), KBase: none)
+template <int D, int OPK>
+int launch_scx(const char* name, const float* x, int64_t M, const float* f, double sigma,
+               const Outs& fin, void* ws, size_t wsb, hipStream_t st) {
+  if (M <= 0) return DICP_OK;
+  constexpr int W = scx_w<D, OPK>;
+  const SymGeom g = sym_geom(M, 1, kScG, 4, kSymFwd4WgMin);
+  const CxLayout L = cx_layout(M, 3, (int64_t)g.nslot * M * W);
+  if (ws == nullptr || wsb < L.total) {
+    set_error("%s: workspace too small (%zu < %zu bytes)", name, wsb, L.total);
+    return DICP_ERR_WORKSPACE;
+  }
+  char* base = reinterpret_cast<char*>(ws);
+  float* box = reinterpret_cast<float*>(base + L.box);
+  uint32_t* k0 = reinterpret_cast<uint32_t*>(base + L.keys0);
+  uint32_t* k1 = reinterpret_cast<uint32_t*>(base + L.keys1);
+  int32_t* v0 = reinterpret_cast<int32_t*>(base + L.vals0);
+  int32_t* v1 = reinterpret_cast<int32_t*>(base + L.vals1);
+  float4* recs = reinterpret_cast<float4*>(base + L.recs);
+  float4* meta = reinterpret_cast<float4*>(base + L.meta);
+  float* slab = reinterpret_cast<float*>(base + L.slabs);
+  const double alpha = std::sqrt(1.4426950408889634 / (2.0 * sigma * sigma));
+  float rho = cx_rho_x100() / 100.f;
+  if (rho > kCxRhoCap) rho = kCxRhoCap;
+  int64_t nparts = (M + 1023) / 1024;
+  if (nparts > kBoxBlocks) nparts = kBoxBlocks;
+  cx_bbox_kernel<D><<<(unsigned)nparts, 256, 0, st>>>(x, M, box);
+  int rc = check_launch(name);
+  if (rc) return rc;
+  cx_codes_kernel<D><<<(unsigned)((M + 255) / 256), 256, 0, st>>>(x, M, box, (int)nparts, k0, v0);
+  if ((rc = check_launch(name))) return rc;
+  size_t tb = sort_temp_bytes(M);
+  if (rocprim::radix_sort_pairs(base + L.sort, tb, k0, k1, v0, v1, (unsigned int)M, 0, 30, st) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("%s: rocprim radix sort failed", name);
+    return DICP_ERR_HIP;
+  }
+  scx_group_kernel<D, OPK><<<(unsigned)g.nG, 256, 0, st>>>(x, f, M, (float)alpha, rho * rho, v1, recs, meta);
+  if ((rc = check_launch(name))) return rc;
+  const int64_t stride = M * W;
+  scx_kernel<D, OPK><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
+      recs, meta, M, g.nG, g.L, (float)alpha, slab, stride);
+  if ((rc = check_launch(name))) return rc;
+  scx_merge_kernel<W><<<(unsigned)((M + 255) / 256), 256, 0, st>>>(slab, stride, M, g.nG, g.L, v1, fin);
+  return check_launch(name);
+}
+
+}  // namespace
+
 #ifndef DICP_CX_R
 #define DICP_CX_R 4
 #endif
@@ -185,6 +250,13 @@ int cx_gauss_red_d(int op, const float* x, int64_t M, const float* y, int64_t N,
                    double sigma, float* out, void* ws, size_t wsb, hipStream_t st) {
   const Args a = {nullptr, nullptr, nullptr, nullptr, y, b, nullptr, nullptr, 0.f};
   const Outs o = make_outs(out);
+  if (scx_eligible(op, x, M, y, N)) {   // rows = columns: the pair-once form (sym_cx.hpp)
+    switch (op) {
+      case DICP_KBASE: return launch_scx<D, 0>("KBase(sym cx)", x, M, nullptr, sigma, o, ws, wsb, st);
+      case DICP_KREDSCAL: return launch_scx<D, 1>("KRedScal(sym cx)", x, M, b, sigma, o, ws, wsb, st);
+      default: return launch_scx<D, 2>("KRed(sym cx)", x, M, b, sigma, o, ws, wsb, st);
+    }
+  }
   switch (op) {
     case DICP_KBASE: return launch_cx<CxKBase<D>, D, kCxR>("KBase(cx)", x, M, a, N, sigma, 0.0, o, ws, wsb, st);
     case DICP_KREDSCAL: return launch_cx<CxKRedScal<D>, D, kCxR>("KRedScal(cx)", x, M, a, N, sigma, 0.0, o, ws, wsb, st);
@@ -192,6 +264,14 @@ int cx_gauss_red_d(int op, const float* x, int64_t M, const float* y, int64_t N,
     case DICP_GRADK: return launch_cx<CxGradK<D>, D, kCxR>("GradKRed(cx)", x, M, a, N, sigma, 0.0, o, ws, wsb, st);
     default: set_error("cx_gauss_red: op %d has no centred form", op); return DICP_ERR_UNSUPPORTED;
   }
+}
+
+// the pair-once form: x is y (same buffer and size), an op with a symmetric pair term, sym_red
+// 1 (automatic: the centred form's size rule, cx_eligible) or 2 (always)
+bool scx_eligible(int op, const float* x, int64_t M, const float* y, int64_t N) {
+  if (sym_red() == 0 || x != y || M != N || M <= 0) return false;
+  if (op != DICP_KBASE && op != DICP_KREDSCAL && op != DICP_KRED) return false;
+  return sym_red() == 2 || red_alg() == 2 || (red_alg() == 1 && cx_eligible(M, N));
 }
 
 bool cx_has_op(int op) {
@@ -229,6 +309,9 @@ size_t cx_ws_d(int64_t M, int64_t N) {
   for (size_t v : {cx_ws<CxKBase<D>, D, kCxR>(M, N), cx_ws<CxKRedScal<D>, D, kCxR>(M, N),
                    cx_ws<CxKRed<D>, D, kCxR>(M, N), cx_ws<CxGradK<D>, D, kCxR>(M, N)})
     m = v > m ? v : m;
+  if (M == N) {   // rows may be the columns: the pair-once form
+    for (size_t v : {scx_ws<D, 0>(M), scx_ws<D, 1>(M), scx_ws<D, 2>(M)}) m = v > m ? v : m;
+  }
   return m;
 }
 

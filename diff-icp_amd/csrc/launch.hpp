@@ -206,9 +206,12 @@ int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, in
 // skeleton), 1 = automatic (large enough passes), 2 = always; cx_rho_x100: sub-tile radius (in
 // scaled units x 100) up to which the expanded exponent is used.
 int& red_alg();
+// pair-once centred sums when the rows are the columns (sym_cx.hpp): 0 off, 1 auto, 2 always
+int& sym_red();
 int& cx_rho_x100();
 // rows M, columns N; ext: the external-point forward (its non-centred kernel is the packed one)
 bool cx_eligible(int64_t M, int64_t N, bool ext = false);
+bool scx_eligible(int op, const float* x, int64_t M, const float* y, int64_t N);
 bool cx_has_op(int op);
 int cx_gauss_red(int op, const float* x, int64_t M, const float* y, int64_t N, int D, const float* b,
                  double sigma, float* out, void* ws, size_t wsb, hipStream_t st);

@@ -220,6 +220,16 @@ extern "C" int dicp_set_option(const char* name, int value) {
     cx_rho_x100() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "sym_fwd_rows")) {
+    if (value != 0 && value != 4 && value != 8) return DICP_ERR_INVALID;
+    sym_fwd_rows() = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "sym_red")) {
+    if (value < 0 || value > 2) return DICP_ERR_INVALID;
+    sym_red() = value;
+    return DICP_OK;
+  }
   if (value != 1 && value != 2 && value != 4) return DICP_ERR_INVALID;
   if (!strcmp(name, "r_fwd")) { g_r_fwd = value; return DICP_OK; }
   if (!strcmp(name, "r_bwd")) { g_r_bwd = value; return DICP_OK; }
@@ -244,6 +254,8 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "bwd_alg")) { *value = g_bwd_alg; return DICP_OK; }
   if (!strcmp(name, "red_alg")) { *value = red_alg(); return DICP_OK; }
   if (!strcmp(name, "cx_rho_x100")) { *value = cx_rho_x100(); return DICP_OK; }
+  if (!strcmp(name, "sym_red")) { *value = sym_red(); return DICP_OK; }
+  if (!strcmp(name, "sym_fwd_rows")) { *value = sym_fwd_rows(); return DICP_OK; }
   if (!strcmp(name, "ext_alg")) { *value = g_ext_alg; return DICP_OK; }
   if (!strcmp(name, "coord_raw")) { *value = tl_coord_raw; return DICP_OK; }
   if (!strcmp(name, "r_fwd")) { *value = r_fwd(); return DICP_OK; }
@@ -270,7 +282,7 @@ extern "C" int dicp_gauss_red_f32(int op, const float* x, int64_t M, const float
     set_error("dicp_gauss_red_f32: op %d needs b%s", op, needc ? " and c" : "");
     return DICP_ERR_INVALID;
   }
-  if (cx_has_op(op) && (D == 2 || D == 3) && cx_eligible(M, N))
+  if (cx_has_op(op) && (D == 2 || D == 3) && (cx_eligible(M, N) || scx_eligible(op, x, M, y, N)))
     return cx_gauss_red(op, x, M, y, N, D, b, sigma, out, ws, ws_bytes, st);
   if (op == DICP_KRED && g_ext_alg == 1 && (D == 2 || D == 3) && N > 0) {
     // KRed = the external-point forward's velocity sum: the packed scaled-coordinate kernel
@@ -345,6 +357,19 @@ bool use_sym_fwd4(int64_t M, bool all, bool raw) {
   return M >= DICP_SYM_FWD4_MIN_M;
 }
 
+// 8 rows per lane for the symmetric forward (SymFwdPk8, 512-point groups): from
+// DICP_SYM_FWD8_MIN_M points when the pass runs alone on the chip (batch_share 1, not inside a
+// lockstep batch); sym_fwd_rows 4 / 8 forces (tools/probes/fwd8_ab.py)
+#ifndef DICP_SYM_FWD8_MIN_M
+#define DICP_SYM_FWD8_MIN_M 60000
+#endif
+bool use_sym_fwd8(int64_t M) {
+  if (batching()) return false;
+  if (sym_fwd_rows() == 8) return true;
+  if (sym_fwd_rows() == 4) return false;
+  return batch_share() <= 1 && M >= DICP_SYM_FWD8_MIN_M;
+}
+
 // rows [row0, row0 + nrows) of the pass against all M columns (row-split over ranks);
 // nrows < 0: all rows.  Output pointers in `o` address the row slice.
 // order: optional nrows int32 row indices (a permutation of the slice's rows) that groups
@@ -374,7 +399,8 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     // (the mG-less last step keeps the ordered pass without the Gs' sums: 2.49 against 3.27 ms
     // for the symmetric pass, which forms them anyway, at 100k)
     if (o.ptr[1] != nullptr && use_sym_fwd4(M, all, raw))
-      return launch_sym_fwd4<D, true>(a, sc, M, oz, ws, wsb, st, true);
+      return use_sym_fwd8(M) ? launch_sym_fwd8<D, true>(a, sc, M, oz, ws, wsb, st, true)
+                             : launch_sym_fwd4<D, true>(a, sc, M, oz, ws, wsb, st, true);
     if (o.ptr[1] == nullptr)
       return launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
                                                                            M, oz, ws, wsb, st);
@@ -400,9 +426,13 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     return o.ptr[2] != nullptr
                ? launch_mfma_fwd<D, true>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order)
                : launch_mfma_fwd<D, false>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order);
-  if (use_sym_fwd4(M, all, raw))   // symmetric pair-once, 4 rows per lane
+  if (use_sym_fwd4(M, all, raw)) {  // symmetric pair-once, 4 (or 8) rows per lane
+    if (use_sym_fwd8(M))
+      return o.ptr[2] != nullptr ? launch_sym_fwd8<D, true>(a, sc, M, o, ws, wsb, st, false)
+                                 : launch_sym_fwd8<D, false>(a, sc, M, o, ws, wsb, st, false);
     return o.ptr[2] != nullptr ? launch_sym_fwd4<D, true>(a, sc, M, o, ws, wsb, st, false)
                                : launch_sym_fwd4<D, false>(a, sc, M, o, ws, wsb, st, false);
+  }
   if (g_fwd_alg == 2 || g_fwd_alg == 4 || g_fwd_alg == 5 || g_fwd_alg == 6)
     return o.ptr[2] != nullptr
                ? launch_fwd_pk<OpOdeSelfFwdPk<D, true>, OpOdeSelfFwdPk<D, true, false, true, false, true>>(raw, "ode_self_fwd(pk)", a, sc, nrows, M, o, ws, wsb, st)
@@ -1121,7 +1151,7 @@ size_t dicp_lddmm_ws(int kind, int64_t M, int64_t N, int D) {
                     D == 2 ? rowred_pk_ws_bytes<OpExtFwdPk<2, false, false>>(M, N)
                            : rowred_pk_ws_bytes<OpExtFwdPk<3, false, false>>(M, N)};
       for (size_t v : c) m = v > m ? v : m;
-      if (cx_eligible(M, N)) {
+      if (cx_eligible(M, N) || (M == N && sym_red() == 2)) {   // (sym_red 2: x = y forced)
         const size_t v = cx_red_ws(M, N, D);
         m = v > m ? v : m;
       }

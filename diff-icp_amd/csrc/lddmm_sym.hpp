@@ -33,6 +33,13 @@ namespace dicp {
 constexpr int kSymG = 128;   // points per group (= rows of one wave)
 constexpr int kSymQ = 4;     // row groups (waves) per workgroup
 constexpr int kSymFwd4WgMin = 4096;   // sym_geom wg_min of the symmetric 4-row forward
+constexpr int kSymFwd8WgMin = 2048;   // ... and of the 8-row forward (512-point groups)
+// rows per lane of the symmetric forward: dicp_set_option "sym_fwd_rows" 4 or 8 forces, 0 =
+// automatic (8 from DICP_SYM_FWD8_MIN_M points)
+inline int& sym_fwd_rows() {
+  static int v = 0;
+  return v;
+}
 // column groups per workgroup: dicp_set_option "sym_L" forces a value; 0 = automatic
 inline int& sym_L() {
   static int L = 0;
@@ -838,12 +845,15 @@ struct SymEntry {
 // W = accumulators per point (SymBwd: 2D, SymFwd: 3D with the divergence, else 2D)
 inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
   if (M <= 0) return 0;
-  // 128 / 256-point groups (the 4-row VJP's smaller L: more row slots)
+  // 128 / 256-point groups (the 4-row VJP's smaller L: more row slots), 512-point groups (the
+  // 8-row forward)
   const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256), g4v = sym_geom(M, nparts, 256, 2),
-                g4f = sym_geom(M, nparts, 256, 4, kSymFwd4WgMin);
+                g4f = sym_geom(M, nparts, 256, 4, kSymFwd4WgMin),
+                g8f = sym_geom(M, nparts, 512, 4, kSymFwd8WgMin);
   int ns = g.nslot > g4.nslot ? g.nslot : g4.nslot;
   ns = g4v.nslot > ns ? g4v.nslot : ns;
   ns = g4f.nslot > ns ? g4f.nslot : ns;
+  ns = g8f.nslot > ns ? g8f.nslot : ns;
   return (size_t)ns * (size_t)M * (size_t)W * sizeof(float);
 }
 
@@ -920,14 +930,14 @@ int launch_sym_fwd(const Args& a, const Scal& sc, int64_t M, const Outs& o, void
 // Merge: one thread per row sums its slots in slot order (8 loads in flight, the additions
 // sequential) and applies the epilogue to v = V, mG = sa Gs, g = -sa p.Z and either h = p.V / 2
 // or (ZS) the divergence rows zs = Z' / alpha (original units, as OpOdeSelfFwdZs) in the h slot.
-template <int D, bool DIV, bool ZS>
+template <int D, bool DIV, bool ZS, int G = 256>
 __device__ __forceinline__ void sym_fwd4_merge_body(const float* __restrict__ slab, int64_t slot_stride,
                                                     int64_t M, int nG, int L, const float* __restrict__ p,
                                                     float sa, float ia, const Outs& o, unsigned bx) {
   constexpr int W = SymFwd<D, DIV>::W;
   const int64_t i = (int64_t)bx * 256 + threadIdx.x;
   if (i >= M) return;
-  const int ns = sym_nslots((int)(i / 256), nG, L);
+  const int ns = sym_nslots((int)(i / G), nG, L);
   float t[W];
   const float* src = slab + i * W;
 #pragma unroll
@@ -961,11 +971,11 @@ __device__ __forceinline__ void sym_fwd4_merge_body(const float* __restrict__ sl
   if (o.ptr[2]) o.ptr[2][i] = epilogue(o, 2, i, DIV ? -sa * pz : 0.f);
   if (!ZS && o.ptr[3]) o.ptr[3][i] = epilogue(o, 3, i, 0.5f * pv);
 }
-template <int D, bool DIV, bool ZS>
+template <int D, bool DIV, bool ZS, int G = 256>
 __global__ __launch_bounds__(256) void sym_fwd4_merge_kernel(const float* __restrict__ slab, int64_t slot_stride,
                                                              int64_t M, int nG, int L, const float* __restrict__ p,
                                                              float sa, float ia, Outs o) {
-  sym_fwd4_merge_body<D, DIV, ZS>(slab, slot_stride, M, nG, L, p, sa, ia, o, blockIdx.x);
+  sym_fwd4_merge_body<D, DIV, ZS, G>(slab, slot_stride, M, nG, L, p, sa, ia, o, blockIdx.x);
 }
 struct SymFwdMergeEntry {
   const float* slab;

@@ -968,6 +968,222 @@ struct SymFwdPk4 {
   }
 };
 
+// ---- the symmetric eta = 0 forward with 8 rows per lane (fwd_alg 2 from DICP_SYM_FWD8_MIN_M
+// points; dicp_set_option "sym_fwd_rows" 4 / 8 forces) -- 512-point groups: a lane holds rows
+// r * 64 + l (r = 0..7) of its group as four float2 row pairs, so each column's record, its LDS
+// reads, and the column side's one scalar add + DPP rotation per accumulator serve 8 rows
+// instead of 4 (~19% of the 4-row loop's issue went to that column side).  Per
+// step: 76 v_pk (row side) + 36 v_pk + 9 adds + 9 DPP (column side) + 8 exp for 16 ordered
+// pair-equivalents, against 2 x (56 v_pk + 9 + 9 + 4 exp) for the 4-row form.  Own body (the
+// 4-row sym_pk4_body also runs the tuned VJP, whose schedule must not move); slots and merge
+// as the 4-row form with G = 512.
+constexpr int kSymG8 = 512;
+template <int D, bool DIV>
+struct SymFwdPk8 {
+  using P4 = SymFwdPk4<D, DIV>;
+  using S = typename P4::S;
+  static constexpr int W = S::W;
+  using Row2 = typename P4::Row2;
+  using Sh = typename P4::Sh;
+  __device__ static void pair_sym8(const Row2* r, const float* rec, f2 (*acc)[W], float* ct) {
+    f2 cv[2 * D];
+    P4::colvec(rec, cv);
+    Sh t[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      P4::shared(r[h], cv, t[h]);
+      P4::row_side(t[h], cv, acc[h]);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      // column j's side over the 8 rows, chained over the 4 row pairs; (i, j) -> (j, i) flips z
+      f2 cV = t[0].K * r[0].p[d], cG = t[0].Kpp * t[0].z[d];
+#pragma unroll
+      for (int h = 1; h < 4; ++h) {
+        cV = pk_fma(t[h].K, r[h].p[d], cV);
+        cG = pk_fma(t[h].Kpp, t[h].z[d], cG);
+      }
+      ct[d] = cV.x + cV.y;
+      ct[D + d] = -(cG.x + cG.y);
+      if (DIV) {
+        f2 cZ = t[0].K * t[0].z[d];
+#pragma unroll
+        for (int h = 1; h < 4; ++h) cZ = pk_fma(t[h].K, t[h].z[d], cZ);
+        ct[2 * D + d] = -(cZ.x + cZ.y);
+      }
+    }
+  }
+  __device__ static void pair_row(const Row2& r, const float* rec, f2* acc) {
+    P4::pair_row(typename P4::Prm{}, r, rec, acc);
+  }
+};
+
+template <int D, bool DIV>
+__global__ __launch_bounds__(256) void sym_fwd_pk8_kernel(Args a, Scal sc, int64_t M, int nG, int L,
+                                                          float* __restrict__ slab, int64_t slot_stride) {
+  using P = SymFwdPk8<D, DIV>;
+  using P4 = SymFwdPk4<D, DIV>;
+  using S = typename P::S;
+  using LY = rec_layout<P4>;
+  constexpr int G = kSymG8;
+  constexpr int CW = S::CW, NP = LY::kPlanes, W = P::W;
+  __shared__ float4 planes[2][NP][G];
+  __shared__ float colacc[kSymQ][64][W];    // one 64-column quarter of a group at a time
+
+  const int Q = (int)blockIdx.y, kc = (int)blockIdx.x;
+  const int B0 = kSymQ * Q + kc * L;
+  if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
+  const int B1 = min(B0 + L, nG);
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int A = kSymQ * Q + wv;
+
+  typename P::Row2 row[4];
+  int64_t ri[8];
+  bool rv[8];
+  {
+    typename S::Row r8[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      ri[r] = (int64_t)A * G + r * 64 + l;
+      rv[r] = A < nG && ri[r] < M;
+      S::load_row(a, sc, rv[r] ? ri[r] : 0, rv[r], r8[r]);
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) P4::pack(r8[2 * h], r8[2 * h + 1], row[h]);
+  }
+  f2 racc[4][W];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int k = 0; k < W; ++k) racc[h][k] = splat(0.f);
+
+  auto stage = [&](int B, int buf) {
+#pragma unroll
+    for (int u = 0; u < G / 256; ++u) {
+      const int c = u * 256 + tid;
+      const int64_t j = (int64_t)B * G + c;
+      float rec[4 * CW], ph[4 * NP];
+      S::load_col(a, sc, j < M ? j : 0, j < M, rec);
+#pragma unroll
+      for (int k = 0; k < 4 * NP; ++k) ph[k] = 0.f;
+#pragma unroll
+      for (int i = 0; i < S::kUsed; ++i) ph[LY::slot(i)] = rec[i];
+      if constexpr (LY::kDupW) {
+#pragma unroll
+        for (int m = 0; m < NP; ++m) ph[4 * m + 3] = ph[4 * m + 2];
+      }
+#pragma unroll
+      for (int m = 0; m < NP; ++m)
+        planes[buf][m][c] = make_float4(ph[4 * m], ph[4 * m + 1], ph[4 * m + 2], ph[4 * m + 3]);
+    }
+  };
+  int buf = 0;
+  auto ldrec = [&](int col, float* rec) {
+    float ph[4 * NP];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      const float4 v = planes[buf][m][col];
+      ph[4 * m] = v.x, ph[4 * m + 1] = v.y, ph[4 * m + 2] = v.z, ph[4 * m + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * CW; ++i) rec[i] = i < S::kUsed ? ph[LY::slot(i)] : 0.f;
+#pragma unroll
+    for (int m = 0; m < NP; ++m) rec[4 * CW + m] = LY::kDupW ? ph[4 * m + 3] : 0.f;
+  };
+  stage(B0, 0);
+  __syncthreads();
+  for (int B = B0; B < B1; ++B) {
+    if (B + 1 < B1) stage(B + 1, buf ^ 1);
+    const bool sym = A < B;          // wave-uniform
+    const bool diag = A == B;
+#pragma unroll 1
+    for (int h = 0; h < G / 64; ++h) {   // 64-column quarters of the group
+      {
+        float cacc[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+        if (sym) {
+#pragma unroll 1
+          for (int k2 = 0; k2 < 64; ++k2) {
+            const int col = h * 64 + ((l + k2) & 63);
+            float rec[4 * CW + NP];
+            ldrec(col, rec);
+            float ct[W];
+            P::pair_sym8(row, rec, racc, ct);
+#pragma unroll
+            for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
+          }
+#pragma unroll
+          for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+        } else if (diag) {
+#pragma unroll 1
+          for (int k2 = 0; k2 < 64; ++k2) {
+            const int col = h * 64 + ((l + k2) & 63);
+            float rec[4 * CW + NP];
+            ldrec(col, rec);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) P::pair_row(row[r], rec, racc[r]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) colacc[wv][l][k] = cacc[k];
+      }
+      __syncthreads();
+      {
+        // the quarter's 64 column sums of the 4 waves, added in wave order (contiguous stores)
+        const int64_t j0 = (int64_t)B * G + h * 64;
+        float* dst = slab + (int64_t)Q * slot_stride + j0 * W;
+        for (int e = tid; e < 64 * W; e += 256) {
+          const int c = e / W, k = e - c * W;
+          if (j0 + c < M) dst[e] = ((colacc[0][c][k] + colacc[1][c][k]) + colacc[2][c][k]) + colacc[3][c][k];
+        }
+      }
+      __syncthreads();
+    }
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    if (!rv[r]) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+    const f2* ra = racc[r >> 1];
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = (r & 1) == 0 ? ra[k].x : ra[k].y;
+  }
+}
+
+// zs: the divergence rows out through the h slot (o.ptr[3], M x D), DIV required; the
+// launcher of the 4-row form's contract (launch_sym_fwd4)
+template <int D, bool DIV>
+int launch_sym_fwd8(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                    hipStream_t st, bool zs) {
+  using S = SymFwd<D, DIV>;
+  if (M <= 0) return DICP_OK;
+  if (int rc = no_batch("ode_self_fwd(sym8)")) return rc;
+  const SymGeom g = sym_geom(M, 1, kSymG8, 4, kSymFwd8WgMin);
+  const size_t need = sym_ws_bytes(M, S::W);
+  if (ws == nullptr || wsb < need) {
+    set_error("ode_self_fwd(sym8): workspace too small (%zu < %zu bytes)", wsb, need);
+    return DICP_ERR_WORKSPACE;
+  }
+  if (o.ptr[0] == nullptr || (zs && (!DIV || o.ptr[3] == nullptr))) {
+    set_error("ode_self_fwd(sym8): v is required, zs needs the divergence sums");
+    return DICP_ERR_INVALID;
+  }
+  float* slab = reinterpret_cast<float*>(ws);
+  const int64_t stride = M * S::W;
+  const dim3 grid((unsigned)g.Kmax, (unsigned)g.nQ), mg((unsigned)((M + 255) / 256));
+  const float ia = 1.f / a.scale;
+  sym_fwd_pk8_kernel<D, DIV><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride);
+  int rc = check_launch("ode_self_fwd(sym8)");
+  if (rc) return rc;
+  if (zs)
+    sym_fwd4_merge_kernel<D, DIV, true, kSymG8><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
+  else
+    sym_fwd4_merge_kernel<D, DIV, false, kSymG8><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
+  return check_launch("ode_self_fwd(sym8 merge)");
+}
+
 template <int D, bool DIV>
 __global__ __launch_bounds__(256) void sym_fwd_pk4_kernel(Args a, Scal sc, int64_t M, int nG, int L,
                                                           float* __restrict__ slab, int64_t slot_stride) {

@@ -1,0 +1,367 @@
+// Pair-once (symmetric) centred Gaussian-kernel sums for x = y: KBase, KRedScal, KRed
+// (kernel.py:131/:135/:138, torch :178-187) when the rows and columns are the SAME point set
+// -- the north_star's "100k x 100k 3D Gaussian kernel sum" as LDDMMModel.v(q, q, p) and the
+// Hamiltonian evaluate it (LDDMM.py:114, :151).
+//
+// K_ij = K_ji, so every unordered pair is evaluated once and its two contributions go to row
+// i (K f_j) and to row j (K f_i): one exp per unordered pair instead of two.  The points are
+// Morton-sorted (the prep of centred.hip: bounding box, 30-bit codes, stable radix sort) and
+// grouped in groups of 256 consecutive sorted points; group g has a centre c_g (mid-range) and
+// a radius.  For a pair of groups (A rows, B columns) both sides are expressed relative to
+// c_B in scaled units (X = alpha (x - c_B), Y = alpha (y - c_B), alpha = sqrt(log2 e / 2 sigma^2)):
+//     K = exp2(-|X - Y|^2) = F_i * exp2(2 X.Y - |Y|^2 - m),   F_i = exp2(m - |X|^2)
+// as centred.hpp's expansion (m = 16, the same range argument and |X| clamp), so a pair costs
+// 3 FMA for its exponent; the row factor F_i multiplies the row's partial sum over group B
+// once (row side) and is folded into the row's fields, F_i f_i, once per group pair (column
+// side).  Per step a lane pairs its 4 rows (two float2 row pairs) with one column:
+//     6 v_pk (exponents) + 4 v_exp + 6 v_pk (row sums) + 6 v_pk + 3 add + 3 DPP (column sums)
+// for 8 ordered pairs, against 12 v_pk + 8 v_exp for the ordered centred kernel (cx_kernel, 4
+// rows); the column sums ride the wave_rol:1 rotation of the symmetric forward / VJP
+// (lddmm_sym.hpp), so no reduction tree is needed.  Groups whose radius exceeds rho_max
+// (cx_rho_x100) are paired in the difference form on the raw coordinates (as cx_kernel's wide
+// sub-tiles).
+//
+// Work decomposition, slots and merge as the symmetric 4-row kernels (lddmm_sym_pk.hpp
+// sym_pk4_body): a workgroup = 4 waves = row groups A = 4Q + w of quad Q against the column
+// groups B of chunk kc; A < B both sides, A == B the ordered pairs (row side, self pair
+// included), A > B nothing (done by wave B).  Column sums of the 4 waves are added in LDS in
+// wave order into slot Q of group B, row sums go to slot Q + 1 + kc; the merge adds a row's
+// slots in slot order and scatters it back to the caller's order.  Deterministic, no atomics.
+#pragma once
+#include "centred.hpp"
+#include "lddmm_sym.hpp"
+#include "packed.hpp"
+
+namespace dicp {
+
+constexpr int kScG = 256;   // points per group: one wave of 64 lanes x 4 rows
+// record (3 float4): [2Y0, 2Y1, c, c] [2Y2 | fields (D = 3) or fields (D = 2)] [raw y | 0]
+template <int D> constexpr int scx_f = D == 3 ? 5 : 4;     // first field
+constexpr int kScRaw = 8;                                  // raw coordinates
+// fields per op: 0 KBase (1: the constant 1), 1 KRedScal (1: d_j), 2 KRed (D: b_j)
+template <int D, int OPK> constexpr int scx_w = OPK == 2 ? D : 1;
+
+// one workgroup per group of 256 sorted points: centre, compactness and the records
+template <int D, int OPK>
+__global__ __launch_bounds__(256) void scx_group_kernel(const float* __restrict__ x, const float* __restrict__ f,
+                                                        int64_t N, float alpha, float rho2max,
+                                                        const int32_t* __restrict__ order,
+                                                        float4* __restrict__ recs, float4* __restrict__ gmeta) {
+  constexpr int W = scx_w<D, OPK>;
+  __shared__ float red[2 * D + 1][4];
+  __shared__ float cen[D + 1];
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int64_t s = (int64_t)blockIdx.x * kScG + tid;
+  const bool valid = s < N;
+  const int64_t o = valid ? order[s] : 0;
+  float y[D], lo[D], hi[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    y[d] = x[o * D + d];
+    lo[d] = valid ? y[d] : __builtin_huge_valf();
+    hi[d] = valid ? y[d] : -__builtin_huge_valf();
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    for (int off = 32; off > 0; off >>= 1) {
+      lo[d] = fminf(lo[d], __shfl_xor(lo[d], off, 64));
+      hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off, 64));
+    }
+  if (l == 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      red[d][wv] = lo[d];
+      red[D + d][wv] = hi[d];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      float a = red[d][0], b = red[D + d][0];
+      for (int w = 1; w < 4; ++w) {
+        a = fminf(a, red[d][w]);
+        b = fmaxf(b, red[D + d][w]);
+      }
+      cen[d] = 0.5f * (a + b);   // raw centre of the group (mid-range)
+    }
+  }
+  __syncthreads();
+  float Yc[D], r2 = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    Yc[d] = alpha * (y[d] - cen[d]);
+    r2 = fmaf(Yc[d], Yc[d], r2);
+  }
+  float rmax = valid ? r2 : 0.f;
+  for (int off = 32; off > 0; off >>= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, off, 64));
+  if (l == 0) red[0][wv] = rmax;
+  __syncthreads();
+  if (tid == 0) {
+    float m = red[0][0];
+    for (int w = 1; w < 4; ++w) m = fmaxf(m, red[0][w]);
+    float mt[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < D; ++d) mt[d] = cen[d];
+    mt[3] = m <= rho2max ? 1.f : 0.f;
+    gmeta[blockIdx.x] = make_float4(mt[0], mt[1], mt[2], mt[3]);
+  }
+  if (!valid) return;
+  float rec[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) rec[k] = 0.f;
+  rec[0] = 2.f * Yc[0];
+  rec[1] = 2.f * Yc[1];
+  if (D == 3) rec[4] = 2.f * Yc[2];
+  rec[2] = rec[3] = -r2 - kCxShift;
+#pragma unroll
+  for (int k = 0; k < W; ++k) rec[scx_f<D> + k] = OPK == 0 ? 1.f : f[o * W + k];
+#pragma unroll
+  for (int d = 0; d < D; ++d) rec[kScRaw + d] = y[d];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) recs[s * 3 + k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
+}
+
+// the pair-once kernel.  grid (Kmax, nQ): blockIdx.y = quad Q, blockIdx.x = column chunk kc
+template <int D, int OPK>
+__global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ recs, const float4* __restrict__ gmeta,
+                                                  int64_t M, int nG, int L, float alpha,
+                                                  float* __restrict__ slab, int64_t slot_stride) {
+  constexpr int W = scx_w<D, OPK>;
+  constexpr int F0 = scx_f<D>;
+  __shared__ float4 planes[2][3][kScG];
+  __shared__ float colacc[kSymQ][kScG][W];
+  const int Q = (int)blockIdx.y, kc = (int)blockIdx.x;
+  const int B0 = kSymQ * Q + kc * L;
+  if (B0 >= nG) return;   // uniform for the whole workgroup, before any barrier
+  const int B1 = min(B0 + L, nG);
+  const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+  const int A = kSymQ * Q + wv;
+
+  // the lane's 4 rows (r * 64 + l of group A) as two float2 pairs: raw coordinates, fields.
+  // Rows past the end (or of a group past nG) take a real point's coordinates with zero
+  // fields: they add nothing to any column and their own sums are not written.
+  f2 xr[2][D], fr[2][W];
+  int64_t ri[4];
+  bool rv[4];
+  {
+    float xs[4][D], fs[4][W];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ri[r] = (int64_t)A * kScG + r * 64 + l;
+      rv[r] = A < nG && ri[r] < M;
+      const int64_t src = rv[r] ? ri[r] : M - 1;
+      const float* rc = reinterpret_cast<const float*>(recs + src * 3);
+#pragma unroll
+      for (int d = 0; d < D; ++d) xs[r][d] = rc[kScRaw + d];
+#pragma unroll
+      for (int k = 0; k < W; ++k) fs[r][k] = rv[r] ? rc[F0 + k] : 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) xr[h][d] = f2{xs[2 * h][d], xs[2 * h + 1][d]};
+#pragma unroll
+      for (int k = 0; k < W; ++k) fr[h][k] = f2{fs[2 * h][k], fs[2 * h + 1][k]};
+    }
+  }
+  f2 racc[2][W];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < W; ++k) racc[h][k] = splat(0.f);
+
+  auto stage = [&](int B, int buf) {
+    const int64_t j = (int64_t)B * kScG + tid;
+    if (j < M) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) planes[buf][k][tid] = recs[j * 3 + k];
+    } else {   // padding column: K = 0 against every row, zero fields
+      planes[buf][0][tid] = make_float4(0.f, 0.f, -1.0e30f, -1.0e30f);
+      planes[buf][1][tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+      planes[buf][2][tid] = make_float4(kFar, kFar, kFar, 0.f);
+    }
+  };
+  int buf = 0;
+  stage(B0, 0);
+  __syncthreads();
+  for (int B = B0; B < B1; ++B) {
+    if (B + 1 < B1) stage(B + 1, buf ^ 1);
+    const bool sym = A < B;    // wave-uniform
+    const bool diag = A == B;
+    const float4 mB = gmeta[B];
+    const bool compact = mB.w != 0.f;
+    const float cB[3] = {mB.x, mB.y, mB.z};
+    // row side relative to c_B: X, the row factor F = exp2(m - |X|^2) (clamped as cx_kernel)
+    f2 X[2][D], F[2], bF[2][W], rp[2][W];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f2 a2 = splat(0.f);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        X[h][d] = (xr[h][d] - splat(cB[d])) * splat(alpha);
+        a2 = pk_fma(X[h][d], X[h][d], a2);
+      }
+      F[h] = f2{fast_exp2(kCxShift - a2.x), fast_exp2(kCxShift - a2.y)};
+      const f2 cl = f2{a2.x > kCxClamp * kCxClamp ? kCxClamp * __builtin_amdgcn_rsqf(a2.x) : 1.f,
+                       a2.y > kCxClamp * kCxClamp ? kCxClamp * __builtin_amdgcn_rsqf(a2.y) : 1.f};
+#pragma unroll
+      for (int d = 0; d < D; ++d) X[h][d] = X[h][d] * cl;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        bF[h][k] = compact ? F[h] * fr[h][k] : fr[h][k];
+        rp[h][k] = splat(0.f);
+      }
+    }
+#pragma unroll 1
+    for (int qq = 0; qq < kScG / 64; ++qq) {
+      float cacc[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+      if (sym && compact) {
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = qq * 64 + ((l + k2) & 63);
+          const float4 p0 = planes[buf][0][col], p1 = planes[buf][1][col];
+          const float rec[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+          const float y2[3] = {rec[0], rec[1], rec[4]};
+          f2 K[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f2 e = f2{rec[2], rec[3]};
+#pragma unroll
+            for (int d = 0; d < D; ++d) e = pk_fma(X[h][d], splat(y2[d]), e);
+            K[h] = f2{fast_exp2(e.x), fast_exp2(e.y)};
+#pragma unroll
+            for (int k = 0; k < W; ++k) rp[h][k] = pk_fma(K[h], splat(rec[F0 + k]), rp[h][k]);
+          }
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            const f2 c = pk_fma(K[1], bF[1][k], K[0] * bF[0][k]);
+            cacc[k] = rol1(cacc[k]) + (c.x + c.y);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+      } else if (sym) {   // wide column group: difference form on the raw coordinates
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = qq * 64 + ((l + k2) & 63);
+          const float4 p1 = planes[buf][1][col], p2 = planes[buf][2][col];
+          const float rec[8] = {p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
+          f2 K[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f2 e = splat(0.f);
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+              const f2 z = (xr[h][d] - splat(rec[4 + d])) * splat(alpha);
+              e = pk_fma(z, z, e);
+            }
+            K[h] = f2{fast_exp2(-e.x), fast_exp2(-e.y)};
+#pragma unroll
+            for (int k = 0; k < W; ++k) rp[h][k] = pk_fma(K[h], splat(rec[F0 - 4 + k]), rp[h][k]);
+          }
+#pragma unroll
+          for (int k = 0; k < W; ++k) {
+            const f2 c = pk_fma(K[1], bF[1][k], K[0] * bF[0][k]);
+            cacc[k] = rol1(cacc[k]) + (c.x + c.y);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]);
+      } else if (diag) {  // ordered pairs of the group with itself, row side only
+#pragma unroll 2
+        for (int k2 = 0; k2 < 64; ++k2) {
+          const int col = qq * 64 + k2;
+          const float4 p0 = planes[buf][0][col], p1 = planes[buf][1][col], p2 = planes[buf][2][col];
+          const float rec[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
+          const float y2[3] = {rec[0], rec[1], rec[4]};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f2 K;
+            if (compact) {
+              f2 e = f2{rec[2], rec[3]};
+#pragma unroll
+              for (int d = 0; d < D; ++d) e = pk_fma(X[h][d], splat(y2[d]), e);
+              K = f2{fast_exp2(e.x), fast_exp2(e.y)};
+            } else {
+              f2 e = splat(0.f);
+#pragma unroll
+              for (int d = 0; d < D; ++d) {
+                const f2 z = (xr[h][d] - splat(rec[kScRaw + d])) * splat(alpha);
+                e = pk_fma(z, z, e);
+              }
+              K = f2{fast_exp2(-e.x), fast_exp2(-e.y)};
+            }
+#pragma unroll
+            for (int k = 0; k < W; ++k) rp[h][k] = pk_fma(K, splat(rec[F0 + k]), rp[h][k]);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) colacc[wv][qq * 64 + l][k] = cacc[k];
+    }
+    // fold the row partials of group B into the row totals (compact: times F)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < W; ++k) racc[h][k] = compact ? pk_fma(F[h], rp[h][k], racc[h][k]) : racc[h][k] + rp[h][k];
+    __syncthreads();
+    {
+      const int64_t j = (int64_t)B * kScG + tid;
+      if (j < M) {
+        float* dst = slab + (int64_t)Q * slot_stride + j * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+          dst[k] = ((colacc[0][tid][k] + colacc[1][tid][k]) + colacc[2][tid][k]) + colacc[3][tid][k];
+      }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (!rv[r]) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+    const f2* ra = racc[r >> 1];
+#pragma unroll
+    for (int k = 0; k < W; ++k) dst[k] = (r & 1) == 0 ? ra[k].x : ra[k].y;
+  }
+}
+
+// merge: one thread per sorted point sums its slots in slot order and writes the result to
+// the point's original row (order[s]) through the Outs epilogue of output 0
+template <int W>
+__global__ __launch_bounds__(256) void scx_merge_kernel(const float* __restrict__ slab, int64_t slot_stride,
+                                                        int64_t M, int nG, int L, const int32_t* __restrict__ order,
+                                                        Outs o) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= M) return;
+  const int ns = sym_nslots((int)(s / kScG), nG, L);
+  float t[W];
+  const float* src = slab + s * W;
+#pragma unroll
+  for (int k = 0; k < W; ++k) t[k] = src[k];
+  int u = 1;
+  for (; u + 4 <= ns; u += 4) {
+    float v[4][W];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < W; ++k) v[c][k] = src[(int64_t)(u + c) * slot_stride + k];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < W; ++k) t[k] += v[c][k];
+  }
+  for (; u < ns; ++u) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) t[k] += src[(int64_t)u * slot_stride + k];
+  }
+  const int64_t i = order[s];
+#pragma unroll
+  for (int k = 0; k < W; ++k) o.ptr[0][i * W + k] = epilogue(o, 0, i * W + k, t[k]);
+}
+
+}  // namespace dicp

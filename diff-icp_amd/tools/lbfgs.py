@@ -41,10 +41,14 @@ import numpy as np
 import torch
 
 # the host-scalar line search reaches torch's decisions through NEP 50 promotion (a numpy
-# float32 scalar combined with a Python float stays float32), which numpy 1.x does not do
-if int(np.__version__.split(".")[0]) < 2:
-    raise ImportError(f"difficp_amd.tools.lbfgs needs numpy >= 2 (NEP 50 scalar promotion), "
-                      f"found {np.__version__}")
+# float32 scalar combined with a Python float stays float32), which numpy 1.x does not do --
+# checked when an optimizer is built (not at import: the rest of the package does not need it)
+_NUMPY_NEP50 = int(np.__version__.split(".")[0]) >= 2
+
+
+def _require_nep50():
+    if not _NUMPY_NEP50:
+        raise ImportError(f"CompactLBFGS needs numpy >= 2 (NEP 50 scalar promotion), found {np.__version__}")
 
 
 def _rowdots(A, v):
@@ -56,6 +60,10 @@ def _rowdots(A, v):
 
 class CompactLBFGS(torch.optim.LBFGS):
     """Drop-in for torch.optim.LBFGS (same constructor and step semantics)."""
+
+    def __init__(self, *args, **kwargs):
+        _require_nep50()
+        super().__init__(*args, **kwargs)
 
     # ------------------------------------------------------------------------------
     def _hist_init(self, n, like):

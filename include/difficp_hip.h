@@ -426,7 +426,9 @@ int dicp_num_splits(int kind, int64_t M, int64_t N);
  * instantiation and stage (blockIdx.z = the call, up to 12 calls per launch).  Each call
  * computes bitwise what it computes alone (same geometry, same order of summation).  Returns
  * DICP_ERR_UNSUPPORTED, and issues nothing, if a recorded call took a path whose kernels have
- * no batched form -- the batchable paths are the packed eta = 0 forward passes (fwd_alg 2,
+ * no batched form (checked before the first launch); returns DICP_ERR_HIP if a batched launch
+ * fails, in which case earlier stages may already have been issued and the outputs and
+ * workspaces of every call of the batch are undefined -- the batchable paths are the packed eta = 0 forward passes (fwd_alg 2,
  * with or without the divergence rows) and the packed symmetric eta = 0 VJPs (bwd_alg 3: full,
  * zero mG cotangent, gp only, 2 or 4 rows per lane, scaled or raw coordinates) with their
  * merges.  dicp_batch_abort: discard an open batch.  One open batch per host thread. */

@@ -536,6 +536,57 @@ def multi_case():
     print("multi", os.path.getsize(os.path.join(HERE, "multi.npz")), "bytes")
 
 
+def psr_std_support_cases():
+    """DiffPSR_std with a non-dense support (PSR_standard.py:445-505 set_support_scheme "decim"
+    / "grid", rho 1) and with / without template weights (:159-166): 3 frames of 200 2D points
+    around a 120-point ellipse template, classic LDDMM sigma 0.2 lambda 2, data kernel 0.1,
+    noise 0.05; energies after init and after 2 x (Reg_opt(nmax=2, tol 1e-4) +
+    Template_opt(nmax=2, tol 1e-4)).  The inputs are drawn in float32 exactly as
+    tests/test_gpu_support.py::test_psr_std_support_schemes draws them; the reference runs in
+    float64.  Also records whether the reference itself warns of an energy increase (its
+    PSR_standard.py:311-315 check)."""
+    import warnings as W
+    import torch
+    K, L, G, P = import_reference()
+    import diffICP.core.PSR_standard as PS
+    f64 = torch.float64
+    spec64 = {"device": "cpu", "dtype": f64}
+    out = {}
+    for scheme in ("decim", "grid"):
+        for weights in (False, True):
+            g = torch.Generator().manual_seed(13)
+            t = torch.linspace(0, 2 * np.pi, 121)[:-1]
+            y0 = torch.stack([0.5 + 0.3 * torch.cos(t), 0.5 + 0.2 * torch.sin(t)], 1)
+            xs = []
+            for k in range(3):
+                tk = torch.rand(200, generator=g) * 2 * np.pi
+                xs.append(torch.stack([0.5 + (0.3 + 0.03 * k) * torch.cos(tk), 0.5 + (0.2 - 0.02 * k) * torch.sin(tk)], 1)
+                          + 0.01 * torch.randn(200, 2, generator=g))
+            key = f"{scheme}_w{int(weights)}"
+            DK = K.GaussKernel(0.1, 2, computversion="torch", spec=spec64)
+            LM = L.LDDMMModel(sigma=0.2, D=2, lambd=2.0, version="classic", scheme="Euler", nt=10,
+                              computversion="torch", spec=spec64)
+            with W.catch_warnings(record=True) as caught:
+                W.simplefilter("always")
+                PSR = PS.DiffPSR_std([[xk.to(f64)] for xk in xs], y0.to(f64), 0.05, LM, DK,
+                                     template_weights=weights, dataspec=spec64, compspec=spec64)
+                PSR.printstuff = False
+                PSR.set_support_scheme(scheme, rho=1.0)
+                Es = [float(PSR.E)]
+                for _ in range(2):
+                    PSR.Reg_opt(nmax=2, tol=1e-4)
+                    Es.append(float(PSR.E))
+                    PSR.Template_opt(nmax=2, tol=1e-4)
+                    Es.append(float(PSR.E))
+            incr = sum("increase in optimization energy" in str(c.message) for c in caught)
+            out[f"{key}/E"] = np.array(Es)
+            out[f"{key}/n_increase_warnings"] = np.array(incr)
+            out[f"{key}/nq0"] = np.array(PSR.q0.shape[0] if hasattr(PSR.q0, "shape") else PSR.q0[0].shape[0])
+            print("psr_std_support", key, Es, "increase warnings:", incr)
+    np.savez_compressed(os.path.join(HERE, "psr_std_support.npz"), **out)
+    print("psr_std_support", os.path.getsize(os.path.join(HERE, "psr_std_support.npz")), "bytes")
+
+
 if __name__ == "__main__":
     only = sys.argv[2] if sys.argv[1:2] == ["--only"] else None
     if only is None:
@@ -552,3 +603,5 @@ if __name__ == "__main__":
         reductions_large()
     if only in (None, "multi"):
         multi_case()
+    if only in (None, "psr_std_support"):
+        psr_std_support_cases()

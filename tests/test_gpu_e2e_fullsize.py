@@ -69,6 +69,17 @@ def test_shoot_and_gradient_fullsize(dev, M, version, disp):
     from difficp_amd.core.LDDMM import LDDMMModel
     q0, p0, y = _case(M, dev, _amplitude(M, disp, dev))
     eta = 1.0 / LAM if version == "logdet" else 0.0
+    if version == "logdet":
+        # as ICP_two_set starts it (PSR.py:406-413 initialize_a0, the ridge form PSR.py:402 --
+        # the only one that scales, device CG): a0 with zero initial speed, v(q0, a0) =
+        # K a0 - eta GradKRed(q0, q0) ~ 0, around which the momentum field is perturbed.  (From
+        # p0 = the small field alone the gradcomponent drift -eta GradKRed of these dense
+        # clusters blows the 10-step Euler shooting up, in float64 as in float32.)
+        LM0 = LDDMMModel(sigma=SIG, D=3, lambd=LAM, version="logdet", scheme="Euler", nt=NT,
+                         spec={"device": dev, "dtype": torch.float32})
+        q32 = q0.float().contiguous()
+        a0 = LM0.v2p(q32, torch.zeros_like(q32), version="ridge_keops", alpha=1e-3)
+        p0 = p0 + a0.double()
     kw = dict(rows=2048, chunk=8192, eta=eta)
     r64 = F.shoot_loss_grad_p0(q0, p0, SIG, NT, LAM, y, **kw)
     r32 = F.shoot_loss_grad_p0(q0.float(), p0.float(), SIG, NT, LAM, y.float(), **kw)

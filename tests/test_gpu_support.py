@@ -82,7 +82,19 @@ def test_psr_std_support_schemes(dev, scheme, weights):
         Es.append(P.E)
         P.Template_opt(nmax=2, tol=1e-4)
         Es.append(P.E)
-    assert Es[-1] < Es[0]
     assert all(np.isfinite(Es))
     if weights:
         assert P.w0[0].shape == (120,)
+    # against the reference's float64 trace of the same inputs (tests/golden/psr_std_support.npz)
+    import std_support_case as C
+    ref = C.reference(scheme, weights)
+    assert abs(Es[0] - ref[0]) <= 1e-5 * abs(ref[0]), (Es[0], ref[0])
+    if scheme == "grid":
+        tol = max(1e-3, 2 * C.FP32_DEV[(scheme, weights)])
+        for a, b in zip(Es, ref):
+            assert abs(a - b) <= tol * abs(b), (Es, ref)
+    else:
+        # the decim traces are not float32-reproducible (test_host_logic.py::
+        # test_psr_std_support_fp32_oracle_deviation); the reference itself decreases the
+        # energy overall -- and raises its own increase warning once without weights
+        assert Es[-1] < Es[0] and ref[-1] < ref[0]
