@@ -223,10 +223,16 @@ def kernel_sum_probe(dev, M, reps=5, same=True):
     fl = _lib.FLOPS_PER_PAIR.get("gauss_red", 15)
     # the compute bound of the sum is max(flops / P_fp32, exps / P_exp)
     bound_s = max(pairs * fl / (FP32_PEAK_TFLOPS * 1e12), pairs * 1.0 / (EXP_PEAK_TPS * 1e12))
-    path = ("centred expansion (csrc/centred.hpp: Morton-sorted 64-column sub-tiles, 6 FMA + 1 exp "
-            "per pair, 4 rows per thread packed in pairs, prep pass included in the time)"
-            if _lib.get_option("red_alg") and M >= 32768 and float(M) * M >= 2.5e9
-            else "packed scaled-coordinate kernel (ext_pk.hpp)")
+    centred = _lib.get_option("red_alg") and M >= 32768 and float(M) * M >= 2.5e9
+    if centred and same and _lib.get_option("sym_red"):
+        path = ("pair-once centred sum (csrc/sym_cx.hpp: Morton-sorted 256-point groups, each unordered "
+                "pair once -- 3 FMA exponent + 1 exp, row and column sides, 4 rows per lane; prep pass "
+                "and merge included in the time)")
+    elif centred:
+        path = ("centred expansion (csrc/centred.hpp: Morton-sorted 64-column sub-tiles, 6 FMA + 1 exp "
+                "per pair, 4 rows per thread packed in pairs, prep pass included in the time)")
+    else:
+        path = "packed scaled-coordinate kernel (ext_pk.hpp)"
     return {"op": f"KRed (kernel.py:138) {'x = y' if same else 'x != y (two independent clouds)'}, D = 3, sigma 0.1",
             "M": M, "ms": round(best, 4),
             "path": path, "Tpair_per_s": round(pairs / s / 1e12, 3),

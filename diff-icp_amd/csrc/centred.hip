@@ -180,14 +180,35 @@ int& sym_red() {
   static int v = 1;
   return v;
 }
+int& sym_red_rows() {
+  static int v = 0;
+  return v;
+}
 
 namespace {
+
+// rows per lane of the pair-once sums: sym_red_rows 4 / 8 forces, 0 = automatic (8 from
+// DICP_SCX8_MIN_M points)
+#ifndef DICP_SCX8_MIN_M
+#define DICP_SCX8_MIN_M 60000
+#endif
+bool scx_rows8(int64_t M) {
+  if (sym_red_rows() == 4) return false;
+  if (sym_red_rows() == 8) return true;
+  return M >= DICP_SCX8_MIN_M;
+}
+constexpr int kScxWgMin = 4096;   // sym_geom wg_min (>= 4096 workgroups before halving L stops)
+
+inline SymGeom scx_geom(int64_t M, bool rows8) {
+  return sym_geom(M, 1, rows8 ? 2 * kScG : kScG, 4, kScxWgMin);
+}
 
 template <int D, int OPK>
 size_t scx_ws(int64_t M) {
   if (M <= 0) return 0;
-  const SymGeom g = sym_geom(M, 1, kScG, 4, kSymFwd4WgMin);
-  return cx_layout(M, 3, (int64_t)g.nslot * M * scx_w<D, OPK>).total;
+  const SymGeom g4 = scx_geom(M, false), g8 = scx_geom(M, true);
+  const int ns = g4.nslot > g8.nslot ? g4.nslot : g8.nslot;
+  return cx_layout(M, 3, (int64_t)ns * M * scx_w<D, OPK>).total;
 }
 
 // Pair-once centred sum (sym_cx.hpp) of rows = columns = x (M, D); f: the column fields
@@ -197,7 +218,8 @@ int launch_scx(const char* name, const float* x, int64_t M, const float* f, doub
                const Outs& fin, void* ws, size_t wsb, hipStream_t st) {
   if (M <= 0) return DICP_OK;
   constexpr int W = scx_w<D, OPK>;
-  const SymGeom g = sym_geom(M, 1, kScG, 4, kSymFwd4WgMin);
+  const bool rows8 = scx_rows8(M);
+  const SymGeom g = scx_geom(M, rows8);
   const CxLayout L = cx_layout(M, 3, (int64_t)g.nslot * M * W);
   if (ws == nullptr || wsb < L.total) {
     set_error("%s: workspace too small (%zu < %zu bytes)", name, wsb, L.total);
@@ -228,13 +250,21 @@ int launch_scx(const char* name, const float* x, int64_t M, const float* f, doub
     set_error("%s: rocprim radix sort failed", name);
     return DICP_ERR_HIP;
   }
+  const int64_t stride = M * W;
+  const dim3 grid((unsigned)g.Kmax, (unsigned)g.nQ), mg((unsigned)((M + 255) / 256));
+  if (rows8) {
+    scx_group_kernel<D, OPK, 2 * kScG><<<(unsigned)g.nG, 256, 0, st>>>(x, f, M, (float)alpha, rho * rho, v1, recs, meta);
+    if ((rc = check_launch(name))) return rc;
+    scx_kernel<D, OPK, 4><<<grid, dim3(256), 0, st>>>(recs, meta, M, g.nG, g.L, (float)alpha, slab, stride);
+    if ((rc = check_launch(name))) return rc;
+    scx_merge_kernel<W, 2 * kScG><<<mg, 256, 0, st>>>(slab, stride, M, g.nG, g.L, v1, fin);
+    return check_launch(name);
+  }
   scx_group_kernel<D, OPK><<<(unsigned)g.nG, 256, 0, st>>>(x, f, M, (float)alpha, rho * rho, v1, recs, meta);
   if ((rc = check_launch(name))) return rc;
-  const int64_t stride = M * W;
-  scx_kernel<D, OPK><<<dim3((unsigned)g.Kmax, (unsigned)g.nQ), dim3(256), 0, st>>>(
-      recs, meta, M, g.nG, g.L, (float)alpha, slab, stride);
+  scx_kernel<D, OPK, 2><<<grid, dim3(256), 0, st>>>(recs, meta, M, g.nG, g.L, (float)alpha, slab, stride);
   if ((rc = check_launch(name))) return rc;
-  scx_merge_kernel<W><<<(unsigned)((M + 255) / 256), 256, 0, st>>>(slab, stride, M, g.nG, g.L, v1, fin);
+  scx_merge_kernel<W><<<mg, 256, 0, st>>>(slab, stride, M, g.nG, g.L, v1, fin);
   return check_launch(name);
 }
 

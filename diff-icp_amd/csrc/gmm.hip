@@ -22,14 +22,18 @@ constexpr int kWaveMergeMinSplits = 64;
 // ---------------------------------------------------------------------------------------
 // LSE row-reduction skeleton: part[(s*M + i)*(2+NACC) + ...] = {m, l, acc...} with
 // m = the chunk's shift (log2 domain), l = sum_j 2^(t_ij - m), acc = Op::accum weighted sums.
-// One exp2 sweep: the shift m is the exact maximum of the chunk's FIRST tile of columns (one
-// logit-only pass over <= 256 columns), and a later logit above m + kLseSlack (rare: a
-// component much closer than any of the first tile's) re-references the row's sums to it.
+// One exp2 sweep: the shift m is the exact maximum over the chunk's first kLseShiftCols
+// columns (a logit-only pass), and a later logit above m + kLseSlack (rare: a component much
+// closer than any of those) re-references the row's sums to it.
 // Terms up to 2^kLseSlack above the shift are summed as they are (no overflow: l stays below
 // 2^(kLseSlack + 30) for 10^9 columns).  Round 4 swept all columns twice (exact maximum, then
 // the exps): the logit, 8 of the E-step's ~25 VALU per pair, was paid twice.
 // ---------------------------------------------------------------------------------------
 constexpr float kLseSlack = 64.f;
+// columns of the chunk's first tile whose logits set the shift (the exact maximum over them):
+// 64 of the <= 256 staged -- a 1/28 logit overhead at the 100k two-set E-step's ~1800-column
+// chunks instead of 1/7; a row whose nearest components come later is re-referenced once
+constexpr int kLseShiftCols = 64;
 
 template <class Op, int R>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
@@ -52,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   int64_t j1 = j0 + chunk;
   if (j1 > N) j1 = N;
 
-  // the shift: exact maximum of the logits over the chunk's first tile
+  // the shift: exact maximum of the logits over the chunk's first kLseShiftCols columns
   float m[R];
   bool none[R];
 #pragma unroll
@@ -61,8 +65,9 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
     const int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
     if (tid < cnt) Op::load_col(args, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
     __syncthreads();
+    const int ns = cnt < kLseShiftCols ? cnt : kLseShiftCols;
 #pragma unroll 2
-    for (int t = 0; t < cnt; ++t) {
+    for (int t = 0; t < ns; ++t) {
       const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
 #pragma unroll
       for (int r = 0; r < R; ++r) {

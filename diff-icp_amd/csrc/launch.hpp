@@ -208,6 +208,7 @@ int launch_rowred(const char* name, const Args& a, const Scal& sc, int64_t M, in
 int& red_alg();
 // pair-once centred sums when the rows are the columns (sym_cx.hpp): 0 off, 1 auto, 2 always
 int& sym_red();
+int& sym_red_rows();   // rows per lane of the pair-once sums: 0 auto, 4, 8
 int& cx_rho_x100();
 // rows M, columns N; ext: the external-point forward (its non-centred kernel is the packed one)
 bool cx_eligible(int64_t M, int64_t N, bool ext = false);

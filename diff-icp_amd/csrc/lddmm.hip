@@ -230,6 +230,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     sym_red() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "sym_red_rows")) {
+    if (value != 0 && value != 4 && value != 8) return DICP_ERR_INVALID;
+    sym_red_rows() = value;
+    return DICP_OK;
+  }
   if (value != 1 && value != 2 && value != 4) return DICP_ERR_INVALID;
   if (!strcmp(name, "r_fwd")) { g_r_fwd = value; return DICP_OK; }
   if (!strcmp(name, "r_bwd")) { g_r_bwd = value; return DICP_OK; }
@@ -255,6 +260,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "red_alg")) { *value = red_alg(); return DICP_OK; }
   if (!strcmp(name, "cx_rho_x100")) { *value = cx_rho_x100(); return DICP_OK; }
   if (!strcmp(name, "sym_red")) { *value = sym_red(); return DICP_OK; }
+  if (!strcmp(name, "sym_red_rows")) { *value = sym_red_rows(); return DICP_OK; }
   if (!strcmp(name, "sym_fwd_rows")) { *value = sym_fwd_rows(); return DICP_OK; }
   if (!strcmp(name, "ext_alg")) { *value = g_ext_alg; return DICP_OK; }
   if (!strcmp(name, "coord_raw")) { *value = tl_coord_raw; return DICP_OK; }

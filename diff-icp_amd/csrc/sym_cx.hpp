@@ -41,25 +41,39 @@ constexpr int kScRaw = 8;                                  // raw coordinates
 // fields per op: 0 KBase (1: the constant 1), 1 KRedScal (1: d_j), 2 KRed (D: b_j)
 template <int D, int OPK> constexpr int scx_w = OPK == 2 ? D : 1;
 
-// one workgroup per group of 256 sorted points: centre, compactness and the records
-template <int D, int OPK>
+// one workgroup per group of G sorted points (G / 256 per thread): centre, compactness and
+// the records
+template <int D, int OPK, int G = kScG>
 __global__ __launch_bounds__(256) void scx_group_kernel(const float* __restrict__ x, const float* __restrict__ f,
                                                         int64_t N, float alpha, float rho2max,
                                                         const int32_t* __restrict__ order,
                                                         float4* __restrict__ recs, float4* __restrict__ gmeta) {
   constexpr int W = scx_w<D, OPK>;
+  constexpr int U = G / 256;
   __shared__ float red[2 * D + 1][4];
   __shared__ float cen[D + 1];
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-  const int64_t s = (int64_t)blockIdx.x * kScG + tid;
-  const bool valid = s < N;
-  const int64_t o = valid ? order[s] : 0;
-  float y[D], lo[D], hi[D];
+  float y[U][D], lo[D], hi[D];
+  int64_t o[U];
+  bool valid[U];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    y[d] = x[o * D + d];
-    lo[d] = valid ? y[d] : __builtin_huge_valf();
-    hi[d] = valid ? y[d] : -__builtin_huge_valf();
+    lo[d] = __builtin_huge_valf();
+    hi[d] = -__builtin_huge_valf();
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t s = (int64_t)blockIdx.x * G + u * 256 + tid;
+    valid[u] = s < N;
+    o[u] = valid[u] ? order[s] : 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      y[u][d] = x[o[u] * D + d];
+      if (valid[u]) {
+        lo[d] = fminf(lo[d], y[u][d]);
+        hi[d] = fmaxf(hi[d], y[u][d]);
+      }
+    }
   }
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -87,13 +101,17 @@ __global__ __launch_bounds__(256) void scx_group_kernel(const float* __restrict_
     }
   }
   __syncthreads();
-  float Yc[D], r2 = 0.f;
+  float Yc[U][D], r2[U], rmax = 0.f;
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    Yc[d] = alpha * (y[d] - cen[d]);
-    r2 = fmaf(Yc[d], Yc[d], r2);
+  for (int u = 0; u < U; ++u) {
+    r2[u] = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      Yc[u][d] = alpha * (y[u][d] - cen[d]);
+      r2[u] = fmaf(Yc[u][d], Yc[u][d], r2[u]);
+    }
+    if (valid[u]) rmax = fmaxf(rmax, r2[u]);
   }
-  float rmax = valid ? r2 : 0.f;
   for (int off = 32; off > 0; off >>= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, off, 64));
   if (l == 0) red[0][wv] = rmax;
   __syncthreads();
@@ -106,31 +124,39 @@ __global__ __launch_bounds__(256) void scx_group_kernel(const float* __restrict_
     mt[3] = m <= rho2max ? 1.f : 0.f;
     gmeta[blockIdx.x] = make_float4(mt[0], mt[1], mt[2], mt[3]);
   }
-  if (!valid) return;
-  float rec[12];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) rec[k] = 0.f;
-  rec[0] = 2.f * Yc[0];
-  rec[1] = 2.f * Yc[1];
-  if (D == 3) rec[4] = 2.f * Yc[2];
-  rec[2] = rec[3] = -r2 - kCxShift;
+  for (int u = 0; u < U; ++u) {
+    if (!valid[u]) continue;
+    const int64_t s = (int64_t)blockIdx.x * G + u * 256 + tid;
+    float rec[12];
 #pragma unroll
-  for (int k = 0; k < W; ++k) rec[scx_f<D> + k] = OPK == 0 ? 1.f : f[o * W + k];
+    for (int k = 0; k < 12; ++k) rec[k] = 0.f;
+    rec[0] = 2.f * Yc[u][0];
+    rec[1] = 2.f * Yc[u][1];
+    if (D == 3) rec[4] = 2.f * Yc[u][2];
+    rec[2] = rec[3] = -r2[u] - kCxShift;
 #pragma unroll
-  for (int d = 0; d < D; ++d) rec[kScRaw + d] = y[d];
+    for (int k = 0; k < W; ++k) rec[scx_f<D> + k] = OPK == 0 ? 1.f : f[o[u] * W + k];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) recs[s * 3 + k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
+    for (int d = 0; d < D; ++d) rec[kScRaw + d] = y[u][d];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) recs[s * 3 + k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
+  }
 }
 
-// the pair-once kernel.  grid (Kmax, nQ): blockIdx.y = quad Q, blockIdx.x = column chunk kc
-template <int D, int OPK>
+// the pair-once kernel.  grid (Kmax, nQ): blockIdx.y = quad Q, blockIdx.x = column chunk kc.
+// RP row pairs per lane: 2 (4 rows, groups of 256) or 4 (8 rows, groups of 512 -- the column
+// side's adds, DPP rotations and LDS addressing then serve 8 rows).
+template <int D, int OPK, int RP = 2>
 __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ recs, const float4* __restrict__ gmeta,
                                                   int64_t M, int nG, int L, float alpha,
                                                   float* __restrict__ slab, int64_t slot_stride) {
   constexpr int W = scx_w<D, OPK>;
   constexpr int F0 = scx_f<D>;
-  __shared__ float4 planes[2][3][kScG];
-  __shared__ float colacc[kSymQ][kScG][W];
+  constexpr int NR = 2 * RP;         // rows per lane
+  constexpr int G = 64 * NR;         // points per group
+  __shared__ float4 planes[2][3][G];
+  __shared__ float colacc[kSymQ][64][W];   // one 64-column quarter at a time
   const int Q = (int)blockIdx.y, kc = (int)blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
   if (B0 >= nG) return;   // uniform for the whole workgroup, before any barrier
@@ -138,17 +164,17 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int A = kSymQ * Q + wv;
 
-  // the lane's 4 rows (r * 64 + l of group A) as two float2 pairs: raw coordinates, fields.
-  // Rows past the end (or of a group past nG) take a real point's coordinates with zero
-  // fields: they add nothing to any column and their own sums are not written.
-  f2 xr[2][D], fr[2][W];
-  int64_t ri[4];
-  bool rv[4];
+  // the lane's rows (r * 64 + l of group A) as float2 pairs: raw coordinates, fields.  Rows
+  // past the end (or of a group past nG) take a real point's coordinates with zero fields:
+  // they add nothing to any column and their own sums are not written.
+  f2 xr[RP][D], fr[RP][W];
+  int64_t ri[NR];
+  bool rv[NR];
   {
-    float xs[4][D], fs[4][W];
+    float xs[NR][D], fs[NR][W];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      ri[r] = (int64_t)A * kScG + r * 64 + l;
+    for (int r = 0; r < NR; ++r) {
+      ri[r] = (int64_t)A * G + r * 64 + l;
       rv[r] = A < nG && ri[r] < M;
       const int64_t src = rv[r] ? ri[r] : M - 1;
       const float* rc = reinterpret_cast<const float*>(recs + src * 3);
@@ -158,28 +184,32 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
       for (int k = 0; k < W; ++k) fs[r][k] = rv[r] ? rc[F0 + k] : 0.f;
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < RP; ++h) {
 #pragma unroll
       for (int d = 0; d < D; ++d) xr[h][d] = f2{xs[2 * h][d], xs[2 * h + 1][d]};
 #pragma unroll
       for (int k = 0; k < W; ++k) fr[h][k] = f2{fs[2 * h][k], fs[2 * h + 1][k]};
     }
   }
-  f2 racc[2][W];
+  f2 racc[RP][W];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < RP; ++h)
 #pragma unroll
     for (int k = 0; k < W; ++k) racc[h][k] = splat(0.f);
 
   auto stage = [&](int B, int buf) {
-    const int64_t j = (int64_t)B * kScG + tid;
-    if (j < M) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) planes[buf][k][tid] = recs[j * 3 + k];
-    } else {   // padding column: K = 0 against every row, zero fields
-      planes[buf][0][tid] = make_float4(0.f, 0.f, -1.0e30f, -1.0e30f);
-      planes[buf][1][tid] = make_float4(0.f, 0.f, 0.f, 0.f);
-      planes[buf][2][tid] = make_float4(kFar, kFar, kFar, 0.f);
+    for (int u = 0; u < G / 256; ++u) {
+      const int c = u * 256 + tid;
+      const int64_t j = (int64_t)B * G + c;
+      if (j < M) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) planes[buf][k][c] = recs[j * 3 + k];
+      } else {   // padding column: K = 0 against every row, zero fields
+        planes[buf][0][c] = make_float4(0.f, 0.f, -1.0e30f, -1.0e30f);
+        planes[buf][1][c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        planes[buf][2][c] = make_float4(kFar, kFar, kFar, 0.f);
+      }
     }
   };
   int buf = 0;
@@ -193,9 +223,9 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
     const bool compact = mB.w != 0.f;
     const float cB[3] = {mB.x, mB.y, mB.z};
     // row side relative to c_B: X, the row factor F = exp2(m - |X|^2) (clamped as cx_kernel)
-    f2 X[2][D], F[2], bF[2][W], rp[2][W];
+    f2 X[RP][D], F[RP], bF[RP][W], rp[RP][W];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < RP; ++h) {
       f2 a2 = splat(0.f);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
@@ -214,7 +244,7 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
       }
     }
 #pragma unroll 1
-    for (int qq = 0; qq < kScG / 64; ++qq) {
+    for (int qq = 0; qq < G / 64; ++qq) {
       float cacc[W];
 #pragma unroll
       for (int k = 0; k < W; ++k) cacc[k] = 0.f;
@@ -225,9 +255,9 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
           const float4 p0 = planes[buf][0][col], p1 = planes[buf][1][col];
           const float rec[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
           const float y2[3] = {rec[0], rec[1], rec[4]};
-          f2 K[2];
+          f2 K[RP];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < RP; ++h) {
             f2 e = f2{rec[2], rec[3]};
 #pragma unroll
             for (int d = 0; d < D; ++d) e = pk_fma(X[h][d], splat(y2[d]), e);
@@ -237,7 +267,9 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
           }
 #pragma unroll
           for (int k = 0; k < W; ++k) {
-            const f2 c = pk_fma(K[1], bF[1][k], K[0] * bF[0][k]);
+            f2 c = K[0] * bF[0][k];
+#pragma unroll
+            for (int h = 1; h < RP; ++h) c = pk_fma(K[h], bF[h][k], c);
             cacc[k] = rol1(cacc[k]) + (c.x + c.y);
           }
         }
@@ -249,9 +281,9 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
           const int col = qq * 64 + ((l + k2) & 63);
           const float4 p1 = planes[buf][1][col], p2 = planes[buf][2][col];
           const float rec[8] = {p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
-          f2 K[2];
+          f2 K[RP];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < RP; ++h) {
             f2 e = splat(0.f);
 #pragma unroll
             for (int d = 0; d < D; ++d) {
@@ -264,7 +296,9 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
           }
 #pragma unroll
           for (int k = 0; k < W; ++k) {
-            const f2 c = pk_fma(K[1], bF[1][k], K[0] * bF[0][k]);
+            f2 c = K[0] * bF[0][k];
+#pragma unroll
+            for (int h = 1; h < RP; ++h) c = pk_fma(K[h], bF[h][k], c);
             cacc[k] = rol1(cacc[k]) + (c.x + c.y);
           }
         }
@@ -278,7 +312,7 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
           const float rec[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
           const float y2[3] = {rec[0], rec[1], rec[4]};
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < RP; ++h) {
             f2 K;
             if (compact) {
               f2 e = f2{rec[2], rec[3]};
@@ -300,28 +334,28 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
         }
       }
 #pragma unroll
-      for (int k = 0; k < W; ++k) colacc[wv][qq * 64 + l][k] = cacc[k];
+      for (int k = 0; k < W; ++k) colacc[wv][l][k] = cacc[k];
+      __syncthreads();
+      {
+        // the quarter's 64 column sums of the 4 waves, added in wave order (contiguous stores)
+        const int64_t j0 = (int64_t)B * G + qq * 64;
+        float* dst = slab + (int64_t)Q * slot_stride + j0 * W;
+        for (int e = tid; e < 64 * W; e += 256) {
+          const int c = e / W, k = e - c * W;
+          if (j0 + c < M) dst[e] = ((colacc[0][c][k] + colacc[1][c][k]) + colacc[2][c][k]) + colacc[3][c][k];
+        }
+      }
+      __syncthreads();
     }
     // fold the row partials of group B into the row totals (compact: times F)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < RP; ++h)
 #pragma unroll
       for (int k = 0; k < W; ++k) racc[h][k] = compact ? pk_fma(F[h], rp[h][k], racc[h][k]) : racc[h][k] + rp[h][k];
-    __syncthreads();
-    {
-      const int64_t j = (int64_t)B * kScG + tid;
-      if (j < M) {
-        float* dst = slab + (int64_t)Q * slot_stride + j * W;
-#pragma unroll
-        for (int k = 0; k < W; ++k)
-          dst[k] = ((colacc[0][tid][k] + colacc[1][tid][k]) + colacc[2][tid][k]) + colacc[3][tid][k];
-      }
-    }
-    __syncthreads();
     buf ^= 1;
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < NR; ++r) {
     if (!rv[r]) continue;
     float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
     const f2* ra = racc[r >> 1];
@@ -332,13 +366,13 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
 
 // merge: one thread per sorted point sums its slots in slot order and writes the result to
 // the point's original row (order[s]) through the Outs epilogue of output 0
-template <int W>
+template <int W, int G = kScG>
 __global__ __launch_bounds__(256) void scx_merge_kernel(const float* __restrict__ slab, int64_t slot_stride,
                                                         int64_t M, int nG, int L, const int32_t* __restrict__ order,
                                                         Outs o) {
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (s >= M) return;
-  const int ns = sym_nslots((int)(s / kScG), nG, L);
+  const int ns = sym_nslots((int)(s / G), nG, L);
   float t[W];
   const float* src = slab + s * W;
 #pragma unroll

@@ -38,6 +38,11 @@ def test_multi_structure_trace_gpu(dev, case):
         # Reg_opt inherits its amplified fp32 rounding: the single-structure traces' 2e-3
         floor = 1e-4 if (stage == "gmm" and it == 0) else 2e-3
         for k, v in dev_.items():
+            if multi_case.group(k) == "eta0" and it > 0:
+                # the outlier log-odds after the first Reg_opt: absolute, 0.1 (the float32
+                # oracle's own 0.031, a GPU run 0.069 -- downstream of the L-BFGS step)
+                assert v <= 0.1, (stage, it, k, v)
+                continue
             if multi_case.group(k) in ("a0", "quadloss"):
                 # printed, not asserted: the momenta are weakly determined along the kernel's
                 # small eigen-directions and a frame's quadratic loss is a small difference

@@ -4,7 +4,8 @@ KRedScal, KRed; kernel.py:131-138 / :178-187 with the rows equal to the columns,
 LDDMMModel.v(q, q, p) and the Hamiltonian call KRed, LDDMM.py:114, :151).
 
 Parity against the float64 oracle (1e-5 norm-wise) with the path forced on
-(sym_red 2) at ragged sizes (1 point, a partial group, group boundaries, a partial quad),
+(sym_red 2), with 4 and 8 rows per lane (sym_red_rows; 256- / 512-point groups), at ragged
+sizes (1 point, a partial group, group boundaries, a partial quad),
 compact and wide clouds (every group in the difference form) and clouds far from the origin;
 against the ordered centred kernel; bitwise run-to-run determinism; the automatic rule takes
 it for the north_star's 100k x 100k sum only when the rows are the columns."""
@@ -37,12 +38,13 @@ def _ops(L, x, b, d, s):
             "KRed": L.gauss_red(L.KRED, x, x, s, b=b)}
 
 
+@pytest.mark.parametrize("rows", [4, 8])
 @pytest.mark.parametrize("D", [2, 3])
 @pytest.mark.parametrize("M,sig,ext,off", [(1, 0.1, 1.0, 0.0), (77, 0.1, 1.0, 0.0), (256, 0.2, 1.0, 0.0),
                                            (257, 0.05, 1.0, 0.0), (1023, 0.1, 1.0, 0.0), (1025, 0.1, 1.0, 0.0),
                                            (5000, 0.05, 1.0, 0.0), (4097, 0.1, 40.0, 0.0),
                                            (6000, 0.1, 3.0, 100.0), (9000, 1.0, 1.0, 0.0)])
-def test_sym_reductions_match_oracle(dev, D, M, sig, ext, off):
+def test_sym_reductions_match_oracle(dev, D, M, sig, ext, off, rows):
     from difficp_amd import _lib as L
     g = torch.Generator().manual_seed(M * 3 + D)
     r32 = lambda t: t.float().double()      # the float64 reference sees the float32 inputs
@@ -52,7 +54,7 @@ def test_sym_reductions_match_oracle(dev, D, M, sig, ext, off):
     f = lambda t: t.float().to(dev).contiguous()
     ref = {"KBase": R.KBase(x, x, sig), "KRedScal": R.KRedScal(x, x, d, sig), "KRed": R.KRed(x, x, b, sig)}
     xd, bd, dd = f(x), f(b), f(d)
-    with opts(sym_red=2):
+    with opts(sym_red=2, sym_red_rows=rows):
         sy = _ops(L, xd, bd, dd, sig)
         sy2 = _ops(L, xd, bd, dd, sig)
     with opts(sym_red=0, red_alg=2):
@@ -63,8 +65,9 @@ def test_sym_reductions_match_oracle(dev, D, M, sig, ext, off):
         assert rel_err(sy[k].cpu(), cx[k].cpu()) < 1e-5, k
 
 
+@pytest.mark.parametrize("rows", [4, 8])
 @pytest.mark.parametrize("rho", [0, 150, 400])
-def test_sym_wide_and_compact_groups_agree(dev, rho):
+def test_sym_wide_and_compact_groups_agree(dev, rho, rows):
     """rho_max 0 (every group pair in the difference form), the default 1.5, the cap 4: all
     within the criterion on a 3D cloud ~30 sigma wide."""
     from difficp_amd import _lib as L
@@ -74,7 +77,7 @@ def test_sym_wide_and_compact_groups_agree(dev, rho):
     b = torch.randn(M, 3, generator=g, dtype=torch.float64)
     ref = R.KRed(x.float().double(), x.float().double(), b.float().double(), sig)
     f = lambda t: t.float().to(dev).contiguous()
-    with opts(sym_red=2, cx_rho_x100=rho):
+    with opts(sym_red=2, cx_rho_x100=rho, sym_red_rows=rows):
         out = L.gauss_red(L.KRED, f(x), f(x), sig, b=f(b))
     assert rel_err(out.cpu(), ref) < 1e-5, (rho, rel_err(out.cpu(), ref))
 

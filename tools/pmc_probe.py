@@ -34,6 +34,13 @@ def main():
         _lib.set_option("fwd_alg", 2)
         torch.cuda.synchronize()
         return
+    if os.environ.get("PMC_OPS") == "ksum":   # the kernel sum x = y (pair-once) and x != y (ordered)
+        y = torch.rand(M, 3, device=dev)
+        for _ in range(5):
+            _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)
+            _lib.gauss_red(_lib.KRED, q, y, 0.1, b=p)
+        torch.cuda.synchronize()
+        return
     if os.environ.get("PMC_OPS") == "kred":   # the north_star's kernel sum alone (centred path)
         for _ in range(5):
             _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)

@@ -15,7 +15,8 @@ import json
 import os
 import sys
 
-NAMES = {"sym_fwd_pk_kernel": "ode_self_fwd_sym", "sym_fwd_kernel": "ode_self_fwd_sym",
+NAMES = {"sym_fwd_pk8_kernel": "ode_self_fwd_sym8", "scx_kernel": "sym_centred_reduction",
+         "scx_merge": "sym_centred_merge", "sym_fwd_pk_kernel": "ode_self_fwd_sym", "sym_fwd_kernel": "ode_self_fwd_sym",
          "sym_fwd_pk4_kernel": "ode_self_fwd_sym4", "sym_fwd4_merge": "sym_fwd_merge",
          "sym_bwd_pk4_kernel": "ode_self_bwd", "sym_bwd_pk_kernel": "ode_self_bwd", "sym_bwd_kernel": "ode_self_bwd", "sym_merge_kernel": "sym_merge",
          "OpOdeSelfBwd": "ode_self_bwd_ordered", "OpOdeSelfFwd": "ode_self_fwd",

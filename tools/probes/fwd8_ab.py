@@ -15,7 +15,7 @@ from difficp_amd import _lib  # noqa: E402
 
 dev = torch.device("cuda:0")
 st = torch.cuda.current_stream()
-Ms = [int(a) for a in sys.argv[1:]] or [20000, 40000, 60000, 80000, 100000, 200000]
+Ms = [int(a) for a in sys.argv[1:]] or [60000, 80000, 100000, 120000, 150000, 200000]
 _lib.set_option("fwd_alg", 5)      # the symmetric forward whatever the size
 for M in Ms:
     g = torch.Generator().manual_seed(M)
@@ -29,8 +29,9 @@ for M in Ms:
     for name, fn in fns.items():
         best = {}
         for _ in range(3):
-            for rows in (4, 8):
+            for rows, L in ((4, 0), (8, 0), (8, 1), (8, 2)):
                 _lib.set_option("sym_fwd_rows", rows)
+                _lib.set_option("sym_L", L)
                 fn()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
@@ -38,9 +39,9 @@ for M in Ms:
                     fn()
                 e1.record(st)
                 e1.synchronize()
-                best[rows] = min(best.get(rows, 1e9), e0.elapsed_time(e1) / reps)
-        row[name] = {"rows4_ms": round(best[4], 4), "rows8_ms": round(best[8], 4),
-                     "rows8_speedup": round(best[4] / best[8], 4)}
+                best[(rows, L)] = min(best.get((rows, L), 1e9), e0.elapsed_time(e1) / reps)
+        _lib.set_option("sym_L", 0)
+        row[name] = {f"rows{r}_L{L}_ms": round(v, 4) for (r, L), v in best.items()}
     _lib.set_option("sym_fwd_rows", 0)
     print(json.dumps(row), flush=True)
 _lib.set_option("fwd_alg", 2)
