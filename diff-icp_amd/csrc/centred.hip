@@ -189,15 +189,20 @@ namespace {
 
 // rows per lane of the pair-once sums: sym_red_rows 4 / 8 forces, 0 = automatic (8 from
 // DICP_SCX8_MIN_M points)
+// (8 rows measured slower at 100k -- 1.87 against 1.59 ms with 4 rows, L = 2 -- and equal at
+// 200k: profiles/r05_ab_sym_red.jsonl; so 8 only when forced)
 #ifndef DICP_SCX8_MIN_M
-#define DICP_SCX8_MIN_M 60000
+#define DICP_SCX8_MIN_M (int64_t(1) << 40)
 #endif
 bool scx_rows8(int64_t M) {
   if (sym_red_rows() == 4) return false;
   if (sym_red_rows() == 8) return true;
   return M >= DICP_SCX8_MIN_M;
 }
-constexpr int kScxWgMin = 4096;   // sym_geom wg_min (>= 4096 workgroups before halving L stops)
+// sym_geom wg_min: L halves until a launch has >= 8192 workgroups -- L = 2 at 100k (9580
+// workgroups: 1.590 ms against 1.620 with L = 4), L = 1 at 50k, L = 8 from ~190k
+// (profiles/r05_ab_sym_red.jsonl)
+constexpr int kScxWgMin = 8192;
 
 inline SymGeom scx_geom(int64_t M, bool rows8) {
   return sym_geom(M, 1, rows8 ? 2 * kScG : kScG, 4, kScxWgMin);

@@ -365,9 +365,11 @@ bool use_sym_fwd4(int64_t M, bool all, bool raw) {
 
 // 8 rows per lane for the symmetric forward (SymFwdPk8, 512-point groups): from
 // DICP_SYM_FWD8_MIN_M points when the pass runs alone on the chip (batch_share 1, not inside a
-// lockstep batch); sym_fwd_rows 4 / 8 forces (tools/probes/fwd8_ab.py)
+// lockstep batch); sym_fwd_rows 4 / 8 forces (tools/probes/fwd8_ab.py).  Measured r05: 8 rows
+// win ~5% at 120k-200k but lose 3% at the north_star's 100k (3.39 vs 3.29 ms), so the rule
+// starts above it
 #ifndef DICP_SYM_FWD8_MIN_M
-#define DICP_SYM_FWD8_MIN_M 60000
+#define DICP_SYM_FWD8_MIN_M 110000
 #endif
 bool use_sym_fwd8(int64_t M) {
   if (batching()) return false;

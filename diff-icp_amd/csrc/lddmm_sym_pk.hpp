@@ -1019,8 +1019,8 @@ struct SymFwdPk8 {
 };
 
 template <int D, bool DIV>
-__global__ __launch_bounds__(256) void sym_fwd_pk8_kernel(Args a, Scal sc, int64_t M, int nG, int L,
-                                                          float* __restrict__ slab, int64_t slot_stride) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void sym_fwd_pk8_kernel(
+    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride) {
   using P = SymFwdPk8<D, DIV>;
   using P4 = SymFwdPk4<D, DIV>;
   using S = typename P::S;

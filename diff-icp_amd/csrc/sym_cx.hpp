@@ -35,8 +35,11 @@
 namespace dicp {
 
 constexpr int kScG = 256;   // points per group: one wave of 64 lanes x 4 rows
-// record (3 float4): [2Y0, 2Y1, c, c] [2Y2 | fields (D = 3) or fields (D = 2)] [raw y | 0]
-template <int D> constexpr int scx_f = D == 3 ? 5 : 4;     // first field
+// record (3 float4): [2Y0, 2Y1, c, c] [fields (W <= 3) | 2Y2 (D = 3) at .w] [raw y | 0]
+// (2Y2 after the fields: with it in front the hipcc schedule copied the last field out of its
+// register pair with a v_mov per step)
+template <int D> constexpr int scx_f = 4;                  // first field
+constexpr int kScY2 = 7;                                   // 2Y2 (D = 3)
 constexpr int kScRaw = 8;                                  // raw coordinates
 // fields per op: 0 KBase (1: the constant 1), 1 KRedScal (1: d_j), 2 KRed (D: b_j)
 template <int D, int OPK> constexpr int scx_w = OPK == 2 ? D : 1;
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(256) void scx_group_kernel(const float* __restrict_
     for (int k = 0; k < 12; ++k) rec[k] = 0.f;
     rec[0] = 2.f * Yc[u][0];
     rec[1] = 2.f * Yc[u][1];
-    if (D == 3) rec[4] = 2.f * Yc[u][2];
+    if (D == 3) rec[kScY2] = 2.f * Yc[u][2];
     rec[2] = rec[3] = -r2[u] - kCxShift;
 #pragma unroll
     for (int k = 0; k < W; ++k) rec[scx_f<D> + k] = OPK == 0 ? 1.f : f[o[u] * W + k];
@@ -147,6 +150,13 @@ __global__ __launch_bounds__(256) void scx_group_kernel(const float* __restrict_
 // the pair-once kernel.  grid (Kmax, nQ): blockIdx.y = quad Q, blockIdx.x = column chunk kc.
 // RP row pairs per lane: 2 (4 rows, groups of 256) or 4 (8 rows, groups of 512 -- the column
 // side's adds, DPP rotations and LDS addressing then serve 8 rows).
+// LDS ring (DICP_SCX_RING, default): each 64-column quarter of a group is staged twice in a
+// row (128 records), so the record of column (l + k2) mod 64 sits at l + k2 without the wrap:
+// the step's LDS addresses are one lane base plus an immediate offset instead of 3 VALU (an
+// add, an and-or, a shift-add) per step -- 6 of the loop's 70 VALU per 2 steps.
+#ifndef DICP_SCX_RING
+#define DICP_SCX_RING 1
+#endif
 template <int D, int OPK, int RP = 2>
 __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ recs, const float4* __restrict__ gmeta,
                                                   int64_t M, int nG, int L, float alpha,
@@ -155,7 +165,9 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
   constexpr int F0 = scx_f<D>;
   constexpr int NR = 2 * RP;         // rows per lane
   constexpr int G = 64 * NR;         // points per group
-  __shared__ float4 planes[2][3][G];
+  constexpr bool kRing = DICP_SCX_RING != 0;
+  constexpr int GS = kRing ? 2 * G : G;   // staged records per buffer
+  __shared__ float4 planes[2][3][GS];
   __shared__ float colacc[kSymQ][64][W];   // one 64-column quarter at a time
   const int Q = (int)blockIdx.y, kc = (int)blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
@@ -197,18 +209,28 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
 #pragma unroll
     for (int k = 0; k < W; ++k) racc[h][k] = splat(0.f);
 
+  // record slot of column c (0..G-1) of the staged group, first copy; the ring's second copy
+  // of a quarter sits 64 slots after the first
+  auto slot = [](int c) { return kRing ? (c >> 6) * 128 + (c & 63) : c; };
   auto stage = [&](int B, int buf) {
 #pragma unroll
     for (int u = 0; u < G / 256; ++u) {
       const int c = u * 256 + tid;
       const int64_t j = (int64_t)B * G + c;
+      float4 v[3];
       if (j < M) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) planes[buf][k][c] = recs[j * 3 + k];
+        for (int k = 0; k < 3; ++k) v[k] = recs[j * 3 + k];
       } else {   // padding column: K = 0 against every row, zero fields
-        planes[buf][0][c] = make_float4(0.f, 0.f, -1.0e30f, -1.0e30f);
-        planes[buf][1][c] = make_float4(0.f, 0.f, 0.f, 0.f);
-        planes[buf][2][c] = make_float4(kFar, kFar, kFar, 0.f);
+        v[0] = make_float4(0.f, 0.f, -1.0e30f, -1.0e30f);
+        v[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        v[2] = make_float4(kFar, kFar, kFar, 0.f);
+      }
+      const int sl = slot(c);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        planes[buf][k][sl] = v[k];
+        if (kRing) planes[buf][k][sl + 64] = v[k];
       }
     }
   };
@@ -248,13 +270,16 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
       float cacc[W];
 #pragma unroll
       for (int k = 0; k < W; ++k) cacc[k] = 0.f;
+      // the lane's step-k2 column: slot lb + k2 (ring) / the wrapped slot (no ring)
+      const int lb = kRing ? qq * 128 + l : 0;
+      auto csl = [&](int k2) { return kRing ? lb + k2 : qq * 64 + ((l + k2) & 63); };
       if (sym && compact) {
 #pragma unroll 2
         for (int k2 = 0; k2 < 64; ++k2) {
-          const int col = qq * 64 + ((l + k2) & 63);
+          const int col = csl(k2);
           const float4 p0 = planes[buf][0][col], p1 = planes[buf][1][col];
           const float rec[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-          const float y2[3] = {rec[0], rec[1], rec[4]};
+          const float y2[3] = {rec[0], rec[1], rec[kScY2]};
           f2 K[RP];
 #pragma unroll
           for (int h = 0; h < RP; ++h) {
@@ -278,7 +303,7 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
       } else if (sym) {   // wide column group: difference form on the raw coordinates
 #pragma unroll 2
         for (int k2 = 0; k2 < 64; ++k2) {
-          const int col = qq * 64 + ((l + k2) & 63);
+          const int col = csl(k2);
           const float4 p1 = planes[buf][1][col], p2 = planes[buf][2][col];
           const float rec[8] = {p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
           f2 K[RP];
@@ -307,10 +332,10 @@ __global__ __launch_bounds__(256) void scx_kernel(const float4* __restrict__ rec
       } else if (diag) {  // ordered pairs of the group with itself, row side only
 #pragma unroll 2
         for (int k2 = 0; k2 < 64; ++k2) {
-          const int col = qq * 64 + k2;
+          const int col = (kRing ? qq * 128 : qq * 64) + k2;
           const float4 p0 = planes[buf][0][col], p1 = planes[buf][1][col], p2 = planes[buf][2][col];
           const float rec[12] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, p2.x, p2.y, p2.z, p2.w};
-          const float y2[3] = {rec[0], rec[1], rec[4]};
+          const float y2[3] = {rec[0], rec[1], rec[kScY2]};
 #pragma unroll
           for (int h = 0; h < RP; ++h) {
             f2 K;

@@ -1,5 +1,5 @@
 """The symmetric forward with 8 rows per lane (lddmm_sym_pk.hpp SymFwdPk8 / sym_fwd_pk8_kernel,
-512-point groups; dicp_set_option "sym_fwd_rows" 8 forces it, automatic from 60k points)
+512-point groups; dicp_set_option "sym_fwd_rows" 8 forces it, automatic from 110k points)
 at ragged sizes (a partial group, group and quad boundaries) and every output variant of a
 whole pass (v / mG / g, the Hamiltonian rows, the divergence rows zs of the Euler step),
 against the 4-row symmetric form (1e-6: fp32 summation order only) and the fp64 oracle's
@@ -73,18 +73,19 @@ def test_forward_eight_rows(dev, M, D):
     assert rel_err(gd.sum().cpu(), c64) <= tol(c64, c32)
 
 
-def test_forward_eight_rows_automatic_rule(dev):
-    """The default (fwd_alg 2, sym_fwd_rows 0) takes the 8-row form for a whole pass from 60k
-    points: its result equals the forced 8-row form bitwise."""
+@pytest.mark.parametrize("M,rows", [(100000, 4), (120000, 8)])
+def test_forward_eight_rows_automatic_rule(dev, M, rows):
+    """The default (fwd_alg 2, sym_fwd_rows 0) keeps 4 rows at the north_star's 100k (where
+    they measured faster) and takes the 8-row form for a whole pass from 110k points: its
+    result equals the form forced with that many rows bitwise."""
     from difficp_amd import _lib as L
     g = torch.Generator().manual_seed(5)
-    M = 100000
     q = torch.rand(M, 3, generator=g).to(dev)
     p = (0.01 * torch.randn(M, 3, generator=g)).to(dev)
     assert L.get_option("sym_fwd_rows") == 0 and L.get_option("fwd_alg") == 2
     auto = L.euler_step(q, p, 0.1, 0.0, 0.1, True)
     old = L.get_option("sym_fwd_rows")
-    L.set_option("sym_fwd_rows", 8)
+    L.set_option("sym_fwd_rows", rows)
     try:
         forced = L.euler_step(q, p, 0.1, 0.0, 0.1, True)
     finally:
