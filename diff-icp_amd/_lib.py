@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+from collections import OrderedDict
 
 import torch
 
@@ -129,9 +130,20 @@ def get_option(name: str) -> int:
     entry point will run is asked from the library, never mirrored on the Python side (a
     build with other -DDICP_* defaults, or a set_option between a forward and its backward,
     stays consistent)."""
+    if name not in _PER_THREAD:
+        hit = _OPT_CACHE.get(name)
+        if hit is not None and hit[0] == _OPTION_EPOCH[0]:
+            return hit[1]
     v = _INT(0)
     _check_rc(lib().dicp_get_option(name.encode(), ctypes.byref(v)), f"get_option({name})")
+    if name not in _PER_THREAD:
+        # process-wide knobs change only through set_option, which bumps the epoch (a ctypes
+        # round trip less per zs_ok / variant query: ~200 per diff-ICP iteration)
+        _OPT_CACHE[name] = (_OPTION_EPOCH[0], int(v.value))
     return int(v.value)
+
+
+_OPT_CACHE = {}
 
 
 # divergence-row reuse (dicp_lddmm_*_zs_f32): the forward's per-row sums zs_i = sum_j K z_ij
@@ -385,6 +397,14 @@ def _launch(name, pairs, nbytes, fn):
 
 
 _WS_BYTES = {}   # (kind, M, N, D) -> dicp_workspace_bytes; cleared by set_option
+# Scratch workspaces reused per (stream, size): the launches of one stream run in order, so a
+# workspace handed to the next call on the same stream is free by the time that call's kernels
+# run -- one torch.empty less per library call (host floor, tools/host_floor.py).  Never while
+# a launch batch is open (its calls run together at the batch's end and each needs its own);
+# a few recent streams only (concurrent frames open a stream per Reg_opt call).
+_WS_CACHE = OrderedDict()
+_WS_CACHE_MAX = 8
+_ws_lock = threading.Lock()
 
 
 def _workspace(kind: int, M: int, N: int, D: int, device):
@@ -394,11 +414,28 @@ def _workspace(kind: int, M: int, N: int, D: int, device):
         nbytes = _WS_BYTES[key] = int(lib().dicp_workspace_bytes(kind, int(M), int(N), int(D)))
     if nbytes == 0:
         return None, 0
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
     keep = getattr(_tl, "batch_keep", None)
     if keep is not None:   # a batch open on this thread: the launch runs at its end
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
         keep.append(ws)
-    return ws, nbytes
+        return ws, nbytes
+    if torch.cuda.is_current_stream_capturing():
+        # a HIP-graph capture (core/shooting.py): the workspace must come from the graph's own
+        # pool, never a cached tensor that could be freed while the graph still points at it
+        return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
+    ck = (_stream(device), device.index)
+    with _ws_lock:
+        ws = _WS_CACHE.get(ck)
+        if ws is not None:
+            _WS_CACHE.move_to_end(ck)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        with _ws_lock:
+            _WS_CACHE[ck] = ws
+            _WS_CACHE.move_to_end(ck)
+            while len(_WS_CACHE) > _WS_CACHE_MAX:
+                _WS_CACHE.popitem(last=False)
+    return ws, int(ws.numel())
 
 
 # ---------------------------------------------------------------------------------------

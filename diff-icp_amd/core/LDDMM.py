@@ -35,14 +35,83 @@ class Shoot(list):
     (LDDMM.py:286-299).  The states are views into stacked trajectory tensors Q, P, C[, X]
     that stay resident on the device."""
 
+    # The state views are formed when read: a closure reads shoot[-1] (and trajloss shoot[0]),
+    # and forming all 3 (nt+1) views of every shooting was ~1500 tensor selects per diff-ICP
+    # iteration, ~8% of the host floor at 2k points (tools/host_floor.py).  Indexing by an int
+    # forms (and keeps) that state only; any other list operation fills the list first.
     def __init__(self, Q, P, C, X=None, H0=None):
-        nt1 = Q.shape[0]
-        if X is None:
-            super().__init__((Q[t], P[t], C[t]) for t in range(nt1))
-        else:
-            super().__init__((Q[t], P[t], C[t], X[t]) for t in range(nt1))
+        super().__init__()
         self.Q, self.P, self.C, self.X = Q, P, C, X
         self.H0 = H0   # H(q0, p0) from the first ODE evaluation (differentiable), or None
+        self._n = Q.shape[0]
+        self._states = {}
+        self._full = False
+
+    def _state(self, t):
+        if t < 0:
+            t += self._n
+        if not 0 <= t < self._n:
+            raise IndexError("shoot index out of range")
+        s = self._states.get(t)
+        if s is None:
+            Q, P, C, X = self.Q, self.P, self.C, self.X
+            s = (Q[t], P[t], C[t]) if X is None else (Q[t], P[t], C[t], X[t])
+            self._states[t] = s
+        return s
+
+    def _fill(self):
+        if not self._full:
+            self._full = True
+            super().extend([self._state(t) for t in range(self._n)])
+
+    def __getitem__(self, k):
+        if isinstance(k, int):
+            return self._state(k)
+        self._fill()
+        return super().__getitem__(k)
+
+    def __len__(self):
+        return self._n
+
+    def __iter__(self):
+        return (self._state(t) for t in range(self._n))
+
+    def __reversed__(self):
+        return (self._state(t) for t in reversed(range(self._n)))
+
+    def __bool__(self):
+        return self._n > 0
+
+    def __contains__(self, v):
+        self._fill()
+        return super().__contains__(v)
+
+    def __eq__(self, other):
+        self._fill()
+        return super().__eq__(other)
+
+    __hash__ = None
+
+    def __repr__(self):
+        self._fill()
+        return super().__repr__()
+
+    def __setitem__(self, k, v):
+        self._fill()
+        super().__setitem__(k, v)
+        if isinstance(k, int):
+            self._states[k % self._n] = v
+
+    def copy(self):
+        return list(self)
+
+    def index(self, *a):
+        self._fill()
+        return super().index(*a)
+
+    def count(self, v):
+        self._fill()
+        return super().count(v)
 
     def detach(self):
         d = lambda t: None if t is None else t.detach()

@@ -14,6 +14,7 @@ integrator (up to fp32 rounding); the trajectory (nt+1 states) stays resident in
 """
 from __future__ import annotations
 
+import os
 import threading
 import weakref
 from collections import OrderedDict
@@ -399,6 +400,20 @@ class ShootFn(torch.autograd.Function):
         if split is not None and (has_x or scheme != "Euler" or split.world == 1):
             split = None
         ctx.split = split
+        if split is None and not has_x and scheme == "Euler" and _graph_eligible(q0, nt):
+            # small supports: the whole fused shooting replayed as one captured HIP graph
+            order, _ = row_order_for(orders, q0, eta, None, q0.shape[0])
+            r = _graph_forward(ctx, q0, p0, order, sigma, eta, nt, want_div, need_p1, params)
+            if r is not None:
+                outs, saved = r
+                ctx.sigma, ctx.eta, ctx.nt, ctx.scheme, ctx.want_div, ctx.has_x = \
+                    sigma, eta, nt, scheme, want_div, has_x
+                ctx.save_for_backward(*saved)
+                if cache is not None:
+                    kept = tuple(t.detach() for t in outs)
+                    cache.store(q0, p0, x0, params, kept, [t.detach() for t in saved])
+                    return tuple(t.clone() for t in kept)
+                return outs
         M, D = q0.shape
         dev = q0.device
         dt = 1.0 / nt
@@ -445,8 +460,13 @@ class ShootFn(torch.autograd.Function):
                 Q[t_in].view(split.world, n_l, D).copy_(qp_all[:, 0])
                 P[t_in].view(split.world, n_l, D).copy_(qp_all[:, 1])
 
+        # per-step views formed once (unbind: one op, against ~6 indexing selects per step --
+        # host floor, tools/host_floor.py); the views write into Q, P, Gd, Zs
+        Qv, Pv = Q.unbind(0), P.unbind(0)
+        Zv = None if Zs is None else Zs.unbind(0)
+        Gv = None
         for t in range(nt):
-            q, p = Q[t], P[t]
+            q, p = Qv[t], Pv[t]
             x = X[t] if has_x else None
             first = t == 0
             if phased and not first:
@@ -527,12 +547,13 @@ class ShootFn(torch.autograd.Function):
                 # divergence terms go to Gd[t] and the cost is accumulated once after the loop
                 if Gd is None:
                     Gd = torch.empty((nt, M), device=dev, dtype=q0.dtype) if want_div else False
+                    Gv = Gd.unbind(0) if want_div else None
                 last_skip = skip and t == nt - 1
-                _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Q[t + 1], p_out=P[t + 1],
-                                g_out=Gd[t] if want_div else None, order=order, want_p=not last_skip,
-                                zs_out=None if Zs is None else Zs[t])
+                _lib.euler_step(q, p, sigma, eta, dt, want_div, q_out=Qv[t + 1], p_out=Pv[t + 1],
+                                g_out=Gv[t] if want_div else None, order=order, want_p=not last_skip,
+                                zs_out=None if Zv is None else Zv[t])
                 if last_skip:
-                    P[t + 1].fill_(float("nan"))   # not formed: make any read loud
+                    Pv[t + 1].fill_(float("nan"))   # not formed: make any read loud
                 fused_from = t if fused_from is None else fused_from
                 continue
             if has_x:
@@ -648,6 +669,10 @@ class ShootFn(torch.autograd.Function):
         dt = 1.0 / nt
         M, D = Q.shape[1], Q.shape[2]
         dev = Q.device
+        if split is None and scheme == "Euler" and not has_x and _graph_eligible(Q[0], nt):
+            r = _graph_backward(ctx, gQ, gP, gC, gH, saved, Zs)
+            if r is not None:
+                return r
 
         def g_or_zero(G, t, shape):
             if G is None:
@@ -664,8 +689,13 @@ class ShootFn(torch.autograd.Function):
         lx = g_or_zero(gX, nt, tuple(X.shape[1:])).clone() if has_x else None
 
         lc_suffix = None
+        Qv, Pv = Q.unbind(0), P.unbind(0)    # per-step views formed once (as the forward)
+        Zv = None if Zs is None else Zs.unbind(0)
+        gQv = None if gQ is None else gQ.unbind(0)
+        gPv = None if gP is None else gP.unbind(0)
+        lcv = None
         for t in range(nt - 1, -1, -1):
-            q, p = Q[t], P[t]
+            q, p = Qv[t], Pv[t]
             x = X[t] if has_x else None
             if split is not None:
                 # this rank's part of the pair-once VJP, summed over ranks (one all-reduce);
@@ -698,16 +728,17 @@ class ShootFn(torch.autograd.Function):
                 # the cost cotangent at t is the suffix sum of gC (precomputed, no per-step op)
                 if gC is not None and lc_suffix is None:
                     lc_suffix = torch.flip(torch.cumsum(torch.flip(gC, (0,)), 0), (0,))
-                lct = lc if gC is None else lc_suffix[t + 1]
+                    lcv = lc_suffix.unbind(0)
+                lct = lc if gC is None else lcv[t + 1]
                 # last step: the cotangent of q0 is only needed if q0 requires a gradient (the
                 # support points of Reg_opt do not) -- then the gq half is skipped
                 want_lq = t > 0 or ctx.needs_input_grad[0]
                 lq, lp = _lib.euler_adjoint_step(q, p, lq, lp, lct if want_div else None, sigma, eta,
-                                                 dt, None if gQ is None else gQ[t],
-                                                 None if gP is None else gP[t], want_lq=want_lq,
-                                                 zs=None if Zs is None else Zs[t])
+                                                 dt, None if gQv is None else gQv[t],
+                                                 None if gPv is None else gPv[t], want_lq=want_lq,
+                                                 zs=None if Zv is None else Zv[t])
                 if gC is not None:
-                    lc = lc_suffix[t]
+                    lc = lcv[t]
                 continue
             if scheme == "Euler":
                 gq, gp, gx = _vjp(q, p, x, lq, lp, lc, lx, sigma, eta, want_div)
@@ -768,6 +799,172 @@ class ManualCtx:
     @property
     def saved_tensors(self):
         return self._saved
+
+
+# ---- HIP-graph replay of the fused Euler shooting and its adjoint (small supports) ---------
+# At a few thousand support points every pass of a shooting is a ~10-20 us kernel and the
+# host's per-call work (wrapper checks, views, ctypes) is most of a closure (tools/host_floor.py:
+# the strong-scaling floor).  There the fused Euler forward (nt passes,
+# the cost scan) and its adjoint (nt VJP passes) are captured once per configuration -- the
+# very same launches, with their workspaces in the graph's private pool -- and replayed: copy
+# the inputs into the graph's static tensors, one replay, copy the outputs out (fresh tensors,
+# as the direct path returns).  Bitwise the direct path (same kernels, same order: only the
+# host's way of issuing them changes; tests/test_gpu_shoot_graph.py).  Keyed per host thread
+# and stream (autograd runs the adjoint on its device thread), captured at a key's second
+# use (a one-off stream, e.g. a concurrent frame's, is never captured), LRU-bounded.  Off for
+# row splits, external points, Ralston, launch batches, the bench's per-launch accounting,
+# and DICP_SHOOT_GRAPH=0.
+_GRAPH_ON = os.environ.get("DICP_SHOOT_GRAPH", "1") != "0"
+_GRAPH_MAX_M = 32768
+_GRAPH_MAX = 8
+_graphs = OrderedDict()
+_graph_seen = OrderedDict()
+_graph_lock = threading.Lock()
+_graph_tl = threading.local()
+graph_stats = {"captures": 0, "replays": 0}
+
+
+def _graph_eligible(q0, nt):
+    return (_GRAPH_ON and nt >= 2 and q0.is_cuda and q0.shape[0] <= _GRAPH_MAX_M
+            and not getattr(_graph_tl, "inside", False) and _lib._prof is None
+            and getattr(_lib._tl, "batcher", None) is None
+            and getattr(_lib._tl, "batch_keep", None) is None
+            and not torch.cuda.is_current_stream_capturing())
+
+
+class _FixedOrder:
+    """RowOrderCache stand-in inside a capture: the order computed outside it."""
+
+    def __init__(self, order):
+        self.order = order
+
+    def get(self, x, row0=0, n=None):
+        return self.order
+
+
+def _graph_entry(key, capture):
+    """The captured graph of `key`, capturing it at the key's second use (None before)."""
+    with _graph_lock:
+        ent = _graphs.get(key)
+        if ent is not None:
+            _graphs.move_to_end(key)
+            return ent
+        n = _graph_seen.get(key, 0) + 1
+        _graph_seen[key] = n
+        while len(_graph_seen) > 4 * _GRAPH_MAX:
+            _graph_seen.popitem(last=False)
+    if n < 2:
+        return None
+    ent = capture()
+    with _graph_lock:
+        graph_stats["captures"] += 1
+        _graphs[key] = ent
+        while len(_graphs) > _GRAPH_MAX:
+            _graphs.popitem(last=False)
+    return ent
+
+
+def _capture(run, dev):
+    """(graph, run's outputs): run() once on a side stream (first-call host queries, lazy
+    state), then captured; the tensors run() allocates live in the graph's private pool."""
+    _graph_tl.inside = True
+    try:
+        cur = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            run()
+        cur.wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            out = run()
+        return g, out
+    finally:
+        _graph_tl.inside = False
+
+
+def _clone_all(ts):
+    """Fresh copies of a list of tensors (None kept), each distinct tensor copied once."""
+    memo = {}
+    out = []
+    for t in ts:
+        if t is None:
+            out.append(None)
+            continue
+        c = memo.get(id(t))
+        if c is None:
+            c = memo[id(t)] = t.clone()
+        out.append(c)
+    return out
+
+
+def _graph_forward(ctx, q0, p0, order, sigma, eta, nt, want_div, need_p1, params):
+    dev = q0.device
+    key = ("fwd", threading.get_ident(), _lib._stream(dev), dev.index, tuple(q0.shape), q0.dtype,
+           params, bool(need_p1), None if order is None else (order.data_ptr(), order._version))
+
+    def capture():
+        sq0, sp0 = q0.detach().clone(), p0.detach().clone()
+        fixed = None if order is None else _FixedOrder(order)
+
+        def run():
+            ictx = ManualCtx((False, True) + (False,) * 11)
+            ictx.raw, ictx.share = ctx.raw, ctx.share
+            outs = ShootFn._forward(ictx, sq0, sp0, None, sigma, eta, nt, "Euler", want_div, None,
+                                    fixed, None, need_p1)
+            return outs, ictx.saved_tensors, ictx.has_zs
+        g, (outs, saved, has_zs) = _capture(run, dev)
+        return {"g": g, "in": (sq0, sp0), "outs": outs, "saved": saved, "has_zs": has_zs,
+                "order": order}
+
+    ent = _graph_entry(key, capture)
+    if ent is None:
+        return None
+    sq0, sp0 = ent["in"]
+    sq0.copy_(q0)
+    sp0.copy_(p0)
+    ent["g"].replay()
+    graph_stats["replays"] += 1
+    n_out = len(ent["outs"])
+    fresh = _clone_all(list(ent["outs"]) + list(ent["saved"]))
+    ctx.has_zs = ent["has_zs"]
+    return tuple(fresh[:n_out]), fresh[n_out:]
+
+
+def _graph_backward(ctx, gQ, gP, gC, gH, saved, Zs):
+    dev = saved[0].device
+    ins = list(saved[:4]) + [Zs, gQ, gP, gC, gH]
+    key = ("bwd", threading.get_ident(), _lib._stream(dev), dev.index,
+           tuple(None if t is None else (tuple(t.shape), t.dtype) for t in ins),
+           float(ctx.sigma), float(ctx.eta), int(ctx.nt), bool(ctx.want_div),
+           tuple(ctx.needs_input_grad[:1]), bool(getattr(ctx, "raw", False)), int(getattr(ctx, "share", 1)),
+           _lib.option_epoch())
+
+    def capture():
+        st = [None if t is None else t.detach().clone() for t in ins]
+
+        def run():
+            ictx = ManualCtx(ctx.needs_input_grad)
+            ictx.save_for_backward(*([t for t in st[:4]] + ([st[4]] if st[4] is not None else [])))
+            ictx.sigma, ictx.eta, ictx.nt, ictx.scheme, ictx.want_div, ictx.has_x = \
+                ctx.sigma, ctx.eta, ctx.nt, "Euler", ctx.want_div, False
+            ictx.split, ictx.has_zs = None, st[4] is not None
+            ictx.raw, ictx.share = getattr(ctx, "raw", False), getattr(ctx, "share", 1)
+            return ShootFn._backward(ictx, st[5], st[6], st[7], st[8])
+        g, out = _capture(run, dev)
+        return {"g": g, "in": st, "out": out}
+
+    ent = _graph_entry(key, capture)
+    if ent is None:
+        return None
+    for s_, t in zip(ent["in"], ins):
+        if t is not None:
+            s_.copy_(t)
+    ent["g"].replay()
+    graph_stats["replays"] += 1
+    out = ent["out"]
+    lq, lp = _clone_all([out[0], out[1]])
+    return (lq, lp) + tuple(out[2:])
 
 
 def shoot_loss_grad(LM, dataloss, q0, p0):

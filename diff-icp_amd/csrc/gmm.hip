@@ -4,8 +4,8 @@
 //      :296 NDsigma2 with the OLD mu, :303 Y, :312-314 Cfe terms)
 //   M  (rows c, cols n): log sum_n gamma_nc and the gamma-weighted mean of x  (GMM.py:287, :293)
 //   T  (rows n, cols c): targets / free-energy sums with OLD gamma, NEW mu, w  (GMM.py:303-314)
-// LSE passes make one exp2 sweep per pair, shifted by the maximum of the chunk's first column
-// tile (re-referenced on a much larger logit), all in the log2 domain; column chunks (split
+// LSE passes make one exp2 sweep per pair, shifted by the maximum of the chunk's first 64
+// columns (a tile that overflows is re-referenced), all in the log2 domain; column chunks (split
 // mode) carry (shift, sum, acc) partials merged with max-rescaling in a fixed order ->
 // deterministic, no atomics.
 #include "launch.hpp"
@@ -15,7 +15,11 @@ using namespace dicp;
 
 namespace {
 
-constexpr int kRG = 2;  // rows per thread
+#ifndef DICP_LSE_RG
+#define DICP_LSE_RG 2
+#endif
+constexpr int kRG = 2;             // rows per thread (targets pass)
+constexpr int kLseRG = DICP_LSE_RG;  // rows per thread (E and M passes)
 // more column-chunk partials per row than this: the one-wave-per-row merge
 constexpr int kWaveMergeMinSplits = 64;
 
@@ -23,17 +27,25 @@ constexpr int kWaveMergeMinSplits = 64;
 // LSE row-reduction skeleton: part[(s*M + i)*(2+NACC) + ...] = {m, l, acc...} with
 // m = the chunk's shift (log2 domain), l = sum_j 2^(t_ij - m), acc = Op::accum weighted sums.
 // One exp2 sweep: the shift m is the exact maximum over the chunk's first kLseShiftCols
-// columns (a logit-only pass), and a later logit above m + kLseSlack (rare: a component much
-// closer than any of those) re-references the row's sums to it.
-// Terms up to 2^kLseSlack above the shift are summed as they are (no overflow: l stays below
-// 2^(kLseSlack + 30) for 10^9 columns).  Round 4 swept all columns twice (exact maximum, then
-// the exps): the logit, 8 of the E-step's ~25 VALU per pair, was paid twice.
+// columns (a logit-only pass).  Every pair is summed without a test; a tile whose partial
+// l exceeds kLseOverflow (a term above 2^56: a component much closer than any of the first
+// ones, or +inf / NaN from one above 2^128) is re-referenced to its exact maximum and summed
+// again -- rare, one divergent lane, instead of a compare + exec-mask branch per pair (round 4's
+// per-pair test cost ~6 SALU + 1 VALU of the E-step's ~25 issue slots per pair).
+// Op interface (Row carries k = the row's exponent constant minus the shift):
+//   CW4 / NACC / kShifted (the acc slot holding sum e (t - m), re-referenced on merges; -1)
+//   load_row(a, sc, i, row), base(row) (the row constant of the logit), load_col(a, sc, j, rec)
+//   tm(sc, row, rec) = t - m, accum(rec, tm, e, acc), finalize(sc, a, i, m, l, acc, outs)
 // ---------------------------------------------------------------------------------------
-constexpr float kLseSlack = 64.f;
+constexpr float kLseOverflow = 0x1p64f;
 // columns of the chunk's first tile whose logits set the shift (the exact maximum over them):
 // 64 of the <= 256 staged -- a 1/28 logit overhead at the 100k two-set E-step's ~1800-column
 // chunks instead of 1/7; a row whose nearest components come later is re-referenced once
 constexpr int kLseShiftCols = 64;
+// a dead component (w = -inf) enters with this logit instead of -inf, so that e (t - m) is
+// 0 * finite (the e-weighted sums stay finite) and a dead-only shift is re-referenced like any
+// other; every live logit is far above it (|t| < 1e20 needs |x - mu| < 1e10 sigma)
+constexpr float kLseDead = -1e20f;
 
 template <class Op, int R>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
@@ -41,6 +53,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
                                                             float* __restrict__ part) {
   constexpr int CW4 = Op::CW4;
   constexpr int NACC = Op::NACC;
+  constexpr int KS = Op::kShifted;
   constexpr int W = 2 + NACC;
   __shared__ float4 lds[kTile * CW4];
   const int tid = threadIdx.x;
@@ -50,7 +63,8 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   for (int r = 0; r < R; ++r) {
     int64_t i = ibase + (int64_t)r * kBlock;
     if (i >= M) i = M - 1;
-    Op::load_row(args, i, row[r]);
+    Op::load_row(args, sc, i, row[r]);
+    row[r].k = Op::base(row[r]);
   }
   const int64_t j0 = (int64_t)blockIdx.y * chunk;
   int64_t j1 = j0 + chunk;
@@ -58,30 +72,25 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
 
   // the shift: exact maximum of the logits over the chunk's first kLseShiftCols columns
   float m[R];
-  bool none[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) m[r] = -__builtin_huge_valf();
   if (j0 < j1) {
     const int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
-    if (tid < cnt) Op::load_col(args, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+    if (tid < cnt) Op::load_col(args, sc, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
     __syncthreads();
     const int ns = cnt < kLseShiftCols ? cnt : kLseShiftCols;
 #pragma unroll 2
     for (int t = 0; t < ns; ++t) {
       const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float aux;
-        m[r] = fmaxf(m[r], Op::logit(sc, row[r], rec, aux));
-      }
+      for (int r = 0; r < R; ++r) m[r] = fmaxf(m[r], Op::tm(sc, row[r], rec));
     }
   }
-  // an all -inf first tile (dead components only): shift 0, as the exact-maximum form did;
-  // a chunk with no finite logit at all stores -inf (the merge skips it)
+  // -inf (a dead row of the M-step: w2 = -inf): shift 0, its terms are all 0
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    none[r] = m[r] == -__builtin_huge_valf();
-    if (none[r]) m[r] = 0.f;
+    if (m[r] == -__builtin_huge_valf()) m[r] = 0.f;
+    row[r].k -= m[r];
   }
 
   float tot[R][NACC + 1];
@@ -93,7 +102,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
     if (!first) {
-      if (tid < cnt) Op::load_col(args, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+      if (tid < cnt) Op::load_col(args, sc, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
       __syncthreads();
     }
     first = false;
@@ -107,34 +116,39 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
       const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        float aux;
-        const float lg = Op::logit(sc, row[r], rec, aux);
-        float tm = lg - m[r];
-        if (tm > kLseSlack) {   // re-reference this row's sums to the new shift lg
-          const float f = fast_exp2(-tm);
-#pragma unroll
-          for (int k = 0; k <= NACC; ++k) {
-            float a = acc[r][k], b = tot[r][k];
-            if (Op::kShifted >= 0 && k == Op::kShifted + 1) {   // sum e (t - m): t - m' = (t - m) - tm
-              a = fmaf(-tm, acc[r][0], a);
-              b = fmaf(-tm, tot[r][0], b);
-            }
-            acc[r][k] = f * a;
-            tot[r][k] = f * b;
-          }
-          m[r] = lg;
-          none[r] = false;
-          tm = 0.f;
-        }
+        const float tm = Op::tm(sc, row[r], rec);
         const float e = fast_exp2(tm);
         acc[r][0] += e;
-        Op::accum(sc, row[r], rec, tm, aux, e, acc[r] + 1);
+        Op::accum(rec, tm, e, acc[r] + 1);
       }
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R; ++r) {
+      if (!(acc[r][0] <= kLseOverflow)) {   // re-reference the row to the tile's maximum
+        float mt = -__builtin_huge_valf();
+        for (int t = 0; t < cnt; ++t)
+          mt = fmaxf(mt, Op::tm(sc, row[r], reinterpret_cast<const float*>(&lds[t * CW4])));
+        const float f = fast_exp2(-mt), l0 = tot[r][0];
+#pragma unroll
+        for (int k = 0; k <= NACC; ++k) {
+          float b = tot[r][k];
+          if (KS >= 0 && k == KS + 1) b = fmaf(-mt, l0, b);   // sum e (t - m): t - m' = (t - m) - mt
+          tot[r][k] = f == 0.f ? 0.f : f * b;
+          acc[r][k] = 0.f;
+        }
+        m[r] += mt;
+        row[r].k -= mt;
+        for (int t = 0; t < cnt; ++t) {
+          const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
+          const float tm = Op::tm(sc, row[r], rec);
+          const float e = fast_exp2(tm);
+          acc[r][0] += e;
+          Op::accum(rec, tm, e, acc[r] + 1);
+        }
+      }
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) tot[r][k] += acc[r][k];
+    }
     __syncthreads();
   }
 #pragma unroll
@@ -142,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
     const int64_t i = ibase + (int64_t)r * kBlock;
     if (i >= M) continue;
     float* dst = part + ((int64_t)blockIdx.y * M + i) * W;
-    dst[0] = none[r] ? -__builtin_huge_valf() : m[r];
+    dst[0] = tot[r][0] > 0.f ? m[r] : -__builtin_huge_valf();   // an empty partial: skipped
 #pragma unroll
     for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[r][k];
   }
@@ -151,8 +165,8 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
 // Merge S chunk partials of each row (fixed order) and finalize through Op::finalize.
 template <class Op>
 __global__ __launch_bounds__(kBlock) void lse_finalize_kernel(const float* __restrict__ part,
-                                                              int64_t M, int S, Scal sc,
-                                                              Outs outs) {
+                                                              int64_t M, int S, Args args,
+                                                              Scal sc, Outs outs) {
   constexpr int NACC = Op::NACC;
   constexpr int W = 2 + NACC;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -174,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void lse_finalize_kernel(const float* __res
       acc[k] = fmaf(f, a, acc[k]);
     }
   }
-  Op::finalize(sc, i, mx, l, acc, outs);
+  Op::finalize(sc, args, i, mx, l, acc, outs);
 }
 
 // Many chunk partials per row (the M-step: C = 256-512 component rows against 10^5-10^6
@@ -219,8 +233,8 @@ struct LsePart {
 
 template <class Op>
 __global__ __launch_bounds__(kBlock) void lse_finalize_wave_kernel(const float* __restrict__ part,
-                                                                   int64_t M, int S, Scal sc,
-                                                                   Outs outs) {
+                                                                   int64_t M, int S, Args args,
+                                                                   Scal sc, Outs outs) {
   constexpr int NACC = Op::NACC;
   constexpr int W = 2 + NACC;
   const int lane = threadIdx.x & 63;
@@ -240,44 +254,54 @@ __global__ __launch_bounds__(kBlock) void lse_finalize_wave_kernel(const float* 
     const float m2 = __shfl_xor(acc.m, off, 64), l2 = __shfl_xor(acc.l, off, 64);
     acc.merge(m2, l2, a2);
   }
-  if (lane == 0) Op::finalize(sc, i, acc.m, acc.l, acc.a, outs);
+  if (lane == 0) Op::finalize(sc, args, i, acc.m, acc.l, acc.a, outs);
 }
 
 // ---- E-step op ------------------------------------------------------------------------
-// rows x_n ; columns (mu_c, w2_c = (w_c - LSE w) log2 e, |mu_c|^2)
-// logit t2 = w2_c + nc |x_n - mu_c|^2   (log2 domain, without -lgn)
-// acc (STATS): sum e mu_c (D), sum e |mu_c|^2, sum e (t2 - m), sum e w2_c, sum e D2_nc
+// rows x_n ; columns (mu_c, v_c = w2_c / nc)   [w2_c = (w_c - LSE w) log2 e, nc = -log2 e/(2 s^2)]
+// logit t2 = w2_c + nc |x_n - mu_c|^2 = nc (|x_n - mu_c|^2 + v_c)   (log2 domain, without -lgn):
+// 3 sub + 3 fma from v_c, one fma with the row's -m -- 7 VALU (round 4: 8 + a compare).
+// acc (STATS): sum e mu_c (D), sum e (t2 - m), sum e v_c -- the entropy, the log-weight and
+// the squared-distance sums all follow from these at the finalize (round 4 summed e D2 and
+// e |mu|^2 per pair as well): 14 VALU + 1 exp per pair.
 template <int D, bool STATS>
 struct OpGmmE {
-  static constexpr int CW4 = cw4(D + 2);
-  static constexpr int NACC = STATS ? D + 4 : 0;
-  static constexpr int kShifted = STATS ? D + 1 : -1;
-  struct Row { float x[D]; };
-  __device__ static void load_row(const Args& a, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
-  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+  static constexpr int CW4 = cw4(D + 1);
+  static constexpr int NACC = STATS ? D + 2 : 0;
+  static constexpr int kShifted = STATS ? D : -1;
+  struct Row { float x[D]; float k; };
+  __device__ static void load_row(const Args& a, const Scal&, int64_t i, Row& r) { ld<D>(a.r0, i, r.x); }
+  __device__ static float base(const Row&) { return 0.f; }
+  // sc.aux1 = 1 / nc (< 0); a dead component (w2 = -inf) gets the logit kLseDead
+  __device__ static void load_col(const Args& a, const Scal& sc, int64_t j, float* rec) {
     ld<D>(a.c0, j, rec);
-    rec[D] = a.c1[j];
-    rec[D + 1] = a.c2[j];
+    const float cap = fminf(kLseDead * sc.aux1, 1e37f);
+    rec[D] = fminf(a.c1[j] * sc.aux1, cap);
   }
-  __device__ static float logit(const Scal& sc, const Row& r, const float* rec, float& d2) {
-    float z[D];
-    d2 = diff_sq<D>(r.x, rec, z);
-    return fmaf(sc.nc, d2, rec[D]);
+  __device__ static float tm(const Scal& sc, const Row& r, const float* rec) {
+    float c = rec[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float z = r.x[d] - rec[d];
+      c = fmaf(z, z, c);
+    }
+    return fmaf(sc.nc, c, r.k);
   }
-  __device__ static void accum(const Scal&, const Row&, const float* rec, float tm, float d2,
-                               float e, float* acc) {
+  __device__ static void accum(const float* rec, float tm, float e, float* acc) {
     if (!STATS) return;
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = fmaf(e, rec[d], acc[d]);
-    acc[D] = fmaf(e, rec[D + 1], acc[D]);
-    acc[D + 1] = fmaf(e, tm, acc[D + 1]);
-    acc[D + 2] = fmaf(e, rec[D], acc[D + 2]);
-    acc[D + 3] = fmaf(e, d2, acc[D + 3]);
+    acc[D] = fmaf(e, tm, acc[D]);
+    acc[D + 1] = fmaf(e, rec[D], acc[D + 1]);
   }
-  // outs: ptr[0] = T (natural, with -lgn), ptr[1] = T2 (log2, no lgn), ptr[2] = stats (D+4)
+  // outs: ptr[0] = T (natural, with -lgn), ptr[1] = T2 (log2, no lgn), ptr[2] = stats (D+4):
+  //   sum gamma mu (D), sum gamma |mu|^2, sum gamma lgamma, sum gamma lpi, sum gamma D2
+  // with (gamma-means, sum gamma = 1)  <t2 - m> = A, <v> = V:
+  //   lgamma = ln2 (t2 - T2) -> ln2 (A - log2 l);  lpi = ln2 w2 = ln2 nc v -> ln2 nc V;
+  //   D2 = (t2 - w2) / nc -> (A + m) / nc - V;  |mu|^2 = D2 + 2 x.mu - |x|^2 -> D2 + x.(2Y - x)
   // sc.aux0 = lgn
-  __device__ static void finalize(const Scal& sc, int64_t i, float m, float l, const float* acc,
-                                  const Outs& o) {
+  __device__ static void finalize(const Scal& sc, const Args& a, int64_t i, float m, float l,
+                                  const float* acc, const Outs& o) {
     const float lg = fast_log2(l);
     const float T2 = m + lg;
     o.ptr[0][i] = kLn2 * T2 - sc.aux0;
@@ -285,46 +309,59 @@ struct OpGmmE {
     if (STATS && o.ptr[2]) {
       const float il = 1.f / l;
       float* st = o.ptr[2] + i * (D + 4);
+      float x[D], mu2 = 0.f;
+      ld<D>(a.r0, i, x);
+      const float A = acc[D] * il, V = acc[D + 1] * il;
+      const float D2 = fmaf(A + m, sc.aux1, -V);
 #pragma unroll
-      for (int d = 0; d < D; ++d) st[d] = acc[d] * il;
-      st[D] = acc[D] * il;
-      st[D + 1] = kLn2 * (acc[D + 1] * il - lg);  // sum gamma lgamma
-      st[D + 2] = kLn2 * acc[D + 2] * il;         // sum gamma lpi
-      st[D + 3] = acc[D + 3] * il;                // sum gamma D2 (old mu)
+      for (int d = 0; d < D; ++d) {
+        const float y = acc[d] * il;
+        st[d] = y;
+        mu2 = fmaf(x[d], fmaf(2.f, y, -x[d]), mu2);
+      }
+      st[D] = D2 + mu2;
+      st[D + 1] = kLn2 * (A - lg);      // sum gamma lgamma
+      st[D + 2] = kLn2 * sc.nc * V;     // sum gamma lpi
+      st[D + 3] = D2;                   // sum gamma D2 (old mu)
     }
   }
 };
 
 // ---- M-step op (column pass as a row pass over components) ------------------------------
-// rows c: (mu_c, w2_c) ; columns n: (x_n, T2_n)
-// logit lg2 = w2_c + nc |x_n - mu_c|^2 - T2_n = log2 gamma_nc ; acc: sum e x_n (D)
+// rows c: (mu_c, w2_c) ; columns n: (x_n, u_n = -T2_n / nc)
+// logit lg2 = w2_c + nc |x_n - mu_c|^2 - T2_n = nc (|x_n - mu_c|^2 + u_n) + w2_c = log2 gamma_nc
+// (7 VALU, the row constant w2_c - m in the last fma) ; acc: sum e x_n (D)
 template <int D>
 struct OpGmmM {
   static constexpr int CW4 = cw4(D + 1);
   static constexpr int NACC = D;
   static constexpr int kShifted = -1;
-  struct Row { float mu[D]; float w2; };
-  __device__ static void load_row(const Args& a, int64_t i, Row& r) {
+  struct Row { float mu[D]; float w2; float k; };
+  __device__ static void load_row(const Args& a, const Scal&, int64_t i, Row& r) {
     ld<D>(a.r0, i, r.mu);
     r.w2 = a.r1[i];
   }
-  __device__ static void load_col(const Args& a, int64_t j, float* rec) {
+  __device__ static float base(const Row& r) { return r.w2; }
+  __device__ static void load_col(const Args& a, const Scal& sc, int64_t j, float* rec) {
     ld<D>(a.c0, j, rec);
-    rec[D] = a.c1[j];
+    rec[D] = -a.c1[j] * sc.aux1;
   }
-  __device__ static float logit(const Scal& sc, const Row& r, const float* rec, float& d2) {
-    float z[D];
-    d2 = diff_sq<D>(r.mu, rec, z);
-    return fmaf(sc.nc, d2, r.w2 - rec[D]);
+  __device__ static float tm(const Scal& sc, const Row& r, const float* rec) {
+    float c = rec[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float z = r.mu[d] - rec[d];
+      c = fmaf(z, z, c);
+    }
+    return fmaf(sc.nc, c, r.k);
   }
-  __device__ static void accum(const Scal&, const Row&, const float* rec, float, float, float e,
-                               float* acc) {
+  __device__ static void accum(const float* rec, float, float e, float* acc) {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = fmaf(e, rec[d], acc[d]);
   }
   // outs.ptr[0] = colstats (D+1): {log sum gamma, mean x (D)}
-  __device__ static void finalize(const Scal&, int64_t i, float m, float l, const float* acc,
-                                  const Outs& o) {
+  __device__ static void finalize(const Scal&, const Args&, int64_t i, float m, float l,
+                                  const float* acc, const Outs& o) {
     float* st = o.ptr[0] + i * (D + 1);
     st[0] = kLn2 * (m + fast_log2(l));
     const float il = 1.f / l;
@@ -410,10 +447,10 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
   if (rc) return rc;
   if (S > kWaveMergeMinSplits) {
     const int64_t nw = (M + kBlock / 64 - 1) / (kBlock / 64);
-    lse_finalize_wave_kernel<Op><<<dim3((unsigned)nw), dim3(kBlock), 0, st>>>(part, M, S, sc, fin);
+    lse_finalize_wave_kernel<Op><<<dim3((unsigned)nw), dim3(kBlock), 0, st>>>(part, M, S, a, sc, fin);
   } else {
     const int64_t nb = (M + kBlock - 1) / kBlock;
-    lse_finalize_kernel<Op><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(part, M, S, sc, fin);
+    lse_finalize_kernel<Op><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(part, M, S, a, sc, fin);
   }
   return check_launch(name);
 }
@@ -425,9 +462,10 @@ int estep_d(const float* X, int64_t N, const float* mu, const float* w2, const f
   const Args a = {X, nullptr, nullptr, nullptr, mu, w2, mu2, nullptr};
   Scal sc = make_scal(sigma, 0.0);
   sc.aux0 = (float)lgn;
+  sc.aux1 = 1.0f / sc.nc;
   const Outs o = make_outs(T, T2, stats);
-  if (stats) return launch_lse<OpGmmE<D, true>, kRG>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
-  return launch_lse<OpGmmE<D, false>, kRG>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
+  if (stats) return launch_lse<OpGmmE<D, true>, kLseRG>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
+  return launch_lse<OpGmmE<D, false>, kLseRG>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
 }
 
 }  // namespace
@@ -460,11 +498,12 @@ extern "C" int dicp_gmm_mstep_f32(const float* X, const float* T2, int64_t N, co
     return DICP_ERR_INVALID;
   }
   const Args a = {mu, w2, nullptr, nullptr, X, T2, nullptr, nullptr};
-  const Scal sc = make_scal(sigma, 0.0);
+  Scal sc = make_scal(sigma, 0.0);
+  sc.aux1 = 1.0f / sc.nc;
   const Outs o = make_outs(colstats);
   switch (D) {
-    case 2: return launch_lse<OpGmmM<2>, kRG>("gmm_mstep", a, sc, C, N, o, ws, ws_bytes, st);
-    case 3: return launch_lse<OpGmmM<3>, kRG>("gmm_mstep", a, sc, C, N, o, ws, ws_bytes, st);
+    case 2: return launch_lse<OpGmmM<2>, kLseRG>("gmm_mstep", a, sc, C, N, o, ws, ws_bytes, st);
+    case 3: return launch_lse<OpGmmM<3>, kLseRG>("gmm_mstep", a, sc, C, N, o, ws, ws_bytes, st);
     default: set_error("gmm_mstep: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
 }
@@ -495,12 +534,12 @@ size_t dicp_gmm_ws(int kind, int64_t M, int64_t N, int D) {
   if (D != 2 && D != 3) return 0;
   switch (kind) {
     case DICP_WS_GMM_ESTEP: {  // both variants (their occupancies, hence splits, differ)
-      size_t a = D == 2 ? lse_ws_bytes<OpGmmE<2, true>, kRG>(M, N) : lse_ws_bytes<OpGmmE<3, true>, kRG>(M, N);
-      size_t b = D == 2 ? lse_ws_bytes<OpGmmE<2, false>, kRG>(M, N) : lse_ws_bytes<OpGmmE<3, false>, kRG>(M, N);
+      size_t a = D == 2 ? lse_ws_bytes<OpGmmE<2, true>, kLseRG>(M, N) : lse_ws_bytes<OpGmmE<3, true>, kLseRG>(M, N);
+      size_t b = D == 2 ? lse_ws_bytes<OpGmmE<2, false>, kLseRG>(M, N) : lse_ws_bytes<OpGmmE<3, false>, kLseRG>(M, N);
       return a > b ? a : b;
     }
     case DICP_WS_GMM_MSTEP:
-      return D == 2 ? lse_ws_bytes<OpGmmM<2>, kRG>(N, M) : lse_ws_bytes<OpGmmM<3>, kRG>(N, M);
+      return D == 2 ? lse_ws_bytes<OpGmmM<2>, kLseRG>(N, M) : lse_ws_bytes<OpGmmM<3>, kLseRG>(N, M);
     case DICP_WS_GMM_TARGETS:
       return D == 2 ? rowred_ws_bytes<OpGmmTargets<2>, kRG>(M, N)
                     : rowred_ws_bytes<OpGmmTargets<3>, kRG>(M, N);

@@ -10,6 +10,8 @@ columns), so rows whose nearby columns all come later must re-reference their su
 
 Criterion: err vs the float64 oracle (oracle/torch_ref.py em_step, pinned by the
 reference's EM goldens) <= max(2e-5, 2 x the float32 oracle's own deviation)."""
+import math
+
 import pytest
 import torch
 
@@ -53,3 +55,51 @@ def test_em_rescaled_shift(dev, N, C, far, sigma):
             assert abs(a - a64) <= max(2e-5, 2 * abs(a32 - a64) / abs(a64)) * abs(a64), (it, a, a64, a32)
         st64, st32 = n64, n32
         assert torch.isfinite(GM.w).all() and torch.isfinite(Y).all()
+
+
+def _estep64(X, mu, lpi, sigma):
+    """float64 E-step rows (GMM.py:260-282, :296, :303, :312-314): T, T2 and the (D+4) stats."""
+    D = X.shape[1]
+    lgn = D * (math.log(sigma) + 0.5 * math.log(2 * math.pi))
+    D2 = ((X[:, None, :] - mu[None]) ** 2).sum(-1)
+    t = lpi[None] - D2 / (2 * sigma ** 2) - lgn
+    T = t.logsumexp(1)
+    lg = t - T[:, None]
+    gam = lg.exp()
+    live = gam > 0
+    wsum = lambda v: torch.where(live, gam * v, torch.zeros_like(gam)).sum(1)
+    stats = torch.cat([gam @ mu, wsum((mu * mu).sum(-1)[None])[:, None], wsum(lg)[:, None],
+                       wsum(lpi[None].expand_as(gam))[:, None], wsum(D2)[:, None]], 1)
+    return T, (T + lgn) / math.log(2), stats, lgn
+
+
+@pytest.mark.parametrize("D", [2, 3])
+@pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks"])
+def test_estep_stats_match_fp64(dev, D, case):
+    """Every output of dicp_gmm_estep_f32 (T, T2 and the D+4 stats, include/difficp_hip.h)
+    against float64 rows: random weights; dead components (w = -inf, the first 300 of them: a
+    dead-only shift tile, kLseDead); a far cluster in the first columns (the tile-end
+    re-reference); many column chunks (the wave-per-row merge)."""
+    from difficp_amd import _lib
+    g = torch.Generator().manual_seed(11 * D + len(case))
+    N, C, sigma = {"plain": (3000, 700, 0.1), "dead": (3000, 900, 0.1), "far_first": (2500, 800, 0.05),
+                   "chunks": (300, 60000, 0.02)}[case]
+    X = torch.rand(N, D, generator=g, dtype=torch.float64)
+    mu = torch.rand(C, D, generator=g, dtype=torch.float64)
+    w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    if case == "dead":
+        w[:300] = -math.inf
+        w[600:650] = -math.inf
+    if case == "far_first":
+        mu[:400] += 3.0
+    X, mu = X.float().double(), mu.float().double()
+    lpi = w - w.logsumexp(0)
+    T64, T264, st64, lgn = _estep64(X, mu, lpi, sigma)
+    f = lambda t: t.float().to(dev).contiguous()
+    T, T2, st = _lib.gmm_estep(f(X), f(mu), f(lpi / math.log(2)), f((mu * mu).sum(-1)), sigma, lgn, True)
+    T, T2, st = T.cpu().double(), T2.cpu().double(), st.cpu().double()
+    assert rel_err(T, T64) < 1e-5 and rel_err(T2, T264) < 1e-5
+    for k in range(D + 4):
+        assert torch.isfinite(st[:, k]).all(), k
+        # the entropy and the squared distance are sums of O(1/sigma^2)-scaled logits (2e-5)
+        assert rel_err(st[:, k], st64[:, k]) < (2e-5 if k >= D else 1e-5), (k, rel_err(st[:, k], st64[:, k]))

@@ -1,0 +1,79 @@
+"""HIP-graph replay of the fused Euler shooting and its adjoint (core/shooting.py,
+_graph_forward / _graph_backward): for small supports the whole forward (nt fused passes and
+the cost scan) and the whole adjoint are captured once and replayed.  The kernels and their
+order are the direct path's, so everything must be BITWISE the direct path: the trajectory,
+the loss, the gradient (first call direct, second captures, third replays), an L-BFGS
+optimisation (LDDMMModel.Optimize) and a need_p1=False closure shooting completed after
+the fact."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _loss_grad(LM, q0, p0, tgt, need_p1=True):
+    p = p0.clone().requires_grad_(True)
+    sh = LM.Shoot(q0, p, None, need_p1=need_p1)
+    L = LM.trajloss(sh) + ((sh[-1][0] - tgt) ** 2).sum()
+    L.backward()
+    return [sh.Q.detach().clone(), sh.C.detach().clone(), L.detach().clone(), p.grad.clone()] + (
+        [sh.P.detach().clone()] if need_p1 else [])
+
+
+@pytest.mark.parametrize("version", ["classic", "hybrid", "logdet"])
+@pytest.mark.parametrize("M,D", [(2000, 3), (700, 2)])
+@pytest.mark.parametrize("need_p1", [True, False])
+def test_graph_replay_bitwise(dev, version, M, D, need_p1):
+    from difficp_amd.core import shooting
+    from difficp_amd.core.LDDMM import LDDMMModel
+    g = torch.Generator().manual_seed(M + D)
+    q0 = torch.rand(M, D, generator=g).to(dev)
+    p0 = (0.05 * torch.randn(M, D, generator=g)).to(dev)
+    tgt = (q0.cpu() + 0.05 * torch.randn(M, D, generator=g)).to(dev)
+    LM = LDDMMModel(sigma=0.1, D=D, lambd=10.0, version=version, nt=10, scheme="Euler",
+                    spec={"device": dev, "dtype": torch.float32})
+    LM.shoot_cache = None          # every call computes (no trajectory reuse)
+    old = shooting._GRAPH_ON
+    try:
+        shooting._GRAPH_ON = False
+        ref = _loss_grad(LM, q0, p0, tgt, need_p1)
+        shooting._GRAPH_ON = True
+        n0 = dict(shooting.graph_stats)
+        runs = [_loss_grad(LM, q0, p0, tgt, need_p1) for _ in range(3)]
+        assert shooting.graph_stats["captures"] >= n0["captures"] + 2, "no graph was captured"
+        assert shooting.graph_stats["replays"] >= n0["replays"] + 4
+        runs.append(_loss_grad(LM, q0, 1.01 * p0, tgt, need_p1))     # new inputs, same graph
+        shooting._GRAPH_ON = False
+        other = _loss_grad(LM, q0, 1.01 * p0, tgt, need_p1)
+    finally:
+        shooting._GRAPH_ON = old
+    for r in runs[:3]:
+        for a, b in zip(r, ref):
+            assert torch.equal(a, b)
+    for a, b in zip(runs[3], other):
+        assert torch.equal(a, b)
+
+
+def test_graph_optimize_bitwise(dev):
+    """A whole LDDMMModel.Optimize (L-BFGS, strong-Wolfe) with and without the graphs."""
+    from difficp_amd.core import shooting
+    from difficp_amd.core.LDDMM import LDDMMModel
+    g = torch.Generator().manual_seed(3)
+    M = 1500
+    q0 = torch.rand(M, 3, generator=g).to(dev)
+    tgt = (q0.cpu() + 0.05 * torch.randn(M, 3, generator=g)).to(dev)
+    res = []
+    old = shooting._GRAPH_ON
+    try:
+        for on in (False, True):
+            shooting._GRAPH_ON = on
+            LM = LDDMMModel(sigma=0.1, D=3, lambd=10.0, version="hybrid", nt=10, scheme="Euler",
+                            spec={"device": dev, "dtype": torch.float32})
+            dataloss = LM.BasicQuadLossFunctor(tgt)
+            p0, shoot, trajl, datal, nsteps, change = LM.Optimize(dataloss, q0, torch.zeros_like(q0), nmax=3)
+            res.append((p0, shoot.Q, shoot.P, trajl, datal, nsteps))
+    finally:
+        shooting._GRAPH_ON = old
+    a, b = res
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3:] == b[3:]

@@ -29,6 +29,10 @@ q = torch.rand(M, 3, device=dev); p = 0.01 * torch.randn(M, 3, device=dev)
 ga = torch.randn(M, 3, device=dev); gb = torch.randn(M, 3, device=dev); gd = torch.ones(1, device=dev)
 w2 = torch.zeros(M, device=dev); mu2 = (q * q).sum(-1)
 zs = torch.empty_like(q)
+T2 = _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, False)[1]
+X4 = torch.rand(640000, 3, device=dev); mu4 = torch.rand(512, 3, device=dev)       # the C4 EM shape
+w24 = torch.full((512,), -9.0, device=dev); m24 = (mu4 * mu4).sum(-1)
+T24 = _lib.gmm_estep(X4, mu4, w24, m24, 0.05, 0.0, False)[1]
 fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
        "step_zs": lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs),
        "adj_zs": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, zs=zs),
@@ -36,6 +40,9 @@ fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
        "adj_gp": lambda: _lib.euler_adjoint_step(q, p, ga, gb, gd, 0.1, 0.0, 0.1, want_lq=False, zs=zs),
        "bwd": lambda: _lib.ode_self_bwd(q, p, ga, gb, gd, 0.1, 0.0),
        "estep": lambda: _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True),
+       "mstep": lambda: _lib.gmm_mstep(q, T2, q, w2, 0.05),
+       "estep_c4": lambda: _lib.gmm_estep(X4, mu4, w24, m24, 0.05, 0.0, True),
+       "mstep_c4": lambda: _lib.gmm_mstep(X4, T24, mu4, w24, 0.05),
        "kred": lambda: _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)}
 out = {}
 for k, fn in fns.items():

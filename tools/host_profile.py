@@ -1,7 +1,7 @@
-"""cProfile of one diff-ICP iteration at a small point count (device work negligible, so the
-profile is the host path: L-BFGS, autograd, wrappers, launches), on one GPU.
+"""cProfile of one diff-ICP iteration at a small point count on the GPU (device work
+negligible): where the host floor of tools/host_floor.py goes, by own time and cumulative.
 
-    python tools/host_profile.py [--N 2000] [--workload two_set|atlas] [--top 45]
+    python tools/host_profile.py [--N 2000] [--top 45] > profile.txt
 """
 import argparse
 import cProfile
@@ -23,7 +23,8 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     psr = workloads.build_two_set(a.N, dev, seed=0)
-    workloads.psr_iteration(psr)
+    for _ in range(2):
+        workloads.psr_iteration(psr)
     torch.cuda.synchronize()
     pr = cProfile.Profile()
     pr.enable()
@@ -32,7 +33,7 @@ def main():
     pr.disable()
     for key in ("tottime", "cumulative"):
         s = io.StringIO()
-        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(a.top)
+        pstats.Stats(pr, stream=s).strip_dirs().sort_stats(key).print_stats(a.top)
         print(s.getvalue())
 
 
