@@ -405,6 +405,15 @@ _WS_BYTES = {}   # (kind, M, N, D) -> dicp_workspace_bytes; cleared by set_optio
 _WS_CACHE = OrderedDict()
 _WS_CACHE_MAX = 8
 _ws_lock = threading.Lock()
+# debugging aid: DICP_WS_POISON=1 fills every workspace with NaN bytes before its call, so a
+# kernel reading workspace it did not write shows up as NaN instead of stale finite values
+_WS_POISON = os.environ.get("DICP_WS_POISON", "0") != "0"
+
+
+def _poison(ws):
+    if _WS_POISON and ws is not None:
+        ws.fill_(255)
+    return ws
 
 
 def _workspace(kind: int, M: int, N: int, D: int, device):
@@ -416,13 +425,13 @@ def _workspace(kind: int, M: int, N: int, D: int, device):
         return None, 0
     keep = getattr(_tl, "batch_keep", None)
     if keep is not None:   # a batch open on this thread: the launch runs at its end
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        ws = _poison(torch.empty(nbytes, dtype=torch.uint8, device=device))
         keep.append(ws)
         return ws, nbytes
     if torch.cuda.is_current_stream_capturing():
         # a HIP-graph capture (core/shooting.py): the workspace must come from the graph's own
         # pool, never a cached tensor that could be freed while the graph still points at it
-        return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
+        return _poison(torch.empty(nbytes, dtype=torch.uint8, device=device)), nbytes
     ck = (_stream(device), device.index)
     with _ws_lock:
         ws = _WS_CACHE.get(ck)
@@ -435,7 +444,7 @@ def _workspace(kind: int, M: int, N: int, D: int, device):
             _WS_CACHE.move_to_end(ck)
             while len(_WS_CACHE) > _WS_CACHE_MAX:
                 _WS_CACHE.popitem(last=False)
-    return ws, int(ws.numel())
+    return _poison(ws), int(ws.numel())
 
 
 # ---------------------------------------------------------------------------------------

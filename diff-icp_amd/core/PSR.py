@@ -358,7 +358,8 @@ class DiffPSR(MultiPSR):
             st.synchronize()            # results are consumed on `main` afterwards
             return k, out
 
-        with ThreadPoolExecutor(max_workers=nconc) as ex:
+        from .shooting import graphs_blocked
+        with graphs_blocked(), ThreadPoolExecutor(max_workers=nconc) as ex:
             return dict(ex.map(work, frames))
 
     def _batch_frames_ok(self, nframes):
@@ -413,7 +414,8 @@ class DiffPSR(MultiPSR):
             b.stream.synchronize()       # results are consumed on `main` afterwards
             return k, out
 
-        with ThreadPoolExecutor(max_workers=len(frames)) as ex:
+        from .shooting import graphs_blocked
+        with graphs_blocked(), ThreadPoolExecutor(max_workers=len(frames)) as ex:
             res = dict(ex.map(work, frames))
         self.batch_stats = {"groups": len(groups), "batches": sum(b.batches for b in batchers),
                             "calls": sum(b.calls for b in batchers)}

@@ -14,6 +14,7 @@ integrator (up to fp32 rounding); the trajectory (nt+1 states) stays resident in
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 import weakref
@@ -824,8 +825,27 @@ _graph_tl = threading.local()
 graph_stats = {"captures": 0, "replays": 0}
 
 
+# host threads driving GPU work concurrently (PSR's concurrent frames, the lockstep batches):
+# a capture must not begin while another thread issues work to the device (hipStreamBeginCapture
+# fails with hipErrorIllegalState, measured in the 4-rank atlas rehearsal), so those sections
+# switch the graphs off for their duration
+_graph_block = [0]
+
+
+@contextlib.contextmanager
+def graphs_blocked():
+    """No HIP-graph capture or replay of shootings while this is active (any thread)."""
+    with _graph_lock:
+        _graph_block[0] += 1
+    try:
+        yield
+    finally:
+        with _graph_lock:
+            _graph_block[0] -= 1
+
+
 def _graph_eligible(q0, nt):
-    return (_GRAPH_ON and nt >= 2 and q0.is_cuda and q0.shape[0] <= _GRAPH_MAX_M
+    return (_GRAPH_ON and _graph_block[0] == 0 and nt >= 2 and q0.is_cuda and q0.shape[0] <= _GRAPH_MAX_M
             and not getattr(_graph_tl, "inside", False) and _lib._prof is None
             and getattr(_lib._tl, "batcher", None) is None
             and getattr(_lib._tl, "batch_keep", None) is None
@@ -842,6 +862,13 @@ class _FixedOrder:
         return self.order
 
 
+class _CaptureFailed(Exception):
+    pass
+
+
+_graph_failed = []
+
+
 def _graph_entry(key, capture):
     """The captured graph of `key`, capturing it at the key's second use (None before)."""
     with _graph_lock:
@@ -855,7 +882,10 @@ def _graph_entry(key, capture):
             _graph_seen.popitem(last=False)
     if n < 2:
         return None
-    ent = capture()
+    try:
+        ent = capture()
+    except _CaptureFailed:
+        return None
     with _graph_lock:
         graph_stats["captures"] += 1
         _graphs[key] = ent
@@ -876,8 +906,17 @@ def _capture(run, dev):
             run()
         cur.wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            out = run()
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                out = run()
+        except Exception:
+            # a capture that could not begin or complete: the direct path from now on in this
+            # process; the graph object is kept (torch's destructor of a half-registered graph
+            # aborts the process)
+            global _GRAPH_ON
+            _GRAPH_ON = False
+            _graph_failed.append(g)
+            raise _CaptureFailed()
         return g, out
     finally:
         _graph_tl.inside = False

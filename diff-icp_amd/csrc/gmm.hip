@@ -44,8 +44,13 @@ constexpr float kLseOverflow = 0x1p64f;
 constexpr int kLseShiftCols = 64;
 // a dead component (w = -inf) enters with this logit instead of -inf, so that e (t - m) is
 // 0 * finite (the e-weighted sums stay finite) and a dead-only shift is re-referenced like any
-// other; every live logit is far above it (|t| < 1e20 needs |x - mu| < 1e10 sigma)
-constexpr float kLseDead = -1e20f;
+// other.  Not larger: a re-reference moves the shift m by the tile's maximum of t - m, and m
+// + mt is rounded to the float grid at m -- below |m| ~ 2^31 that rounding (<= 64) cannot leave
+// a term above the overflow test; at -1e20 it was ~4e12 and the tile stayed at +inf.  So live
+// components farther than ~1.2e4 sigma from a row weigh like dead ones there (both vanish
+// against any component nearer than that), and rows farther than ~5e4 sigma from every
+// component are outside the single sweep's range (the log-likelihood there is below -1e9).
+constexpr float kLseDead = -1e8f;
 
 template <class Op, int R>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
