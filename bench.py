@@ -606,7 +606,7 @@ def _main(out):
                             "(before the closing barrier), closures = L-BFGS loss evaluations, "
                             "em_steps, collectives (count) and collective_s (host wall time inside "
                             "the blocking ones: the exchange plus waiting for the slowest rank), "
-                            "kernel_busy_s = summed kernel time (timed iterations only)"}
+                            "kernel_busy_s = summed kernel time (timed iterations only; absent when frames run concurrently, whose per-launch event times overlap)"}
         line = {
             "metric": METRIC, "value": round(value, 5), "unit": "PSR iterations/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

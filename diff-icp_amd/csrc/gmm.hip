@@ -10,6 +10,7 @@
 // deterministic, no atomics.
 #include "launch.hpp"
 #include "lddmm_ops.hpp"
+#include "packed.hpp"
 
 using namespace dicp;
 
@@ -20,6 +21,12 @@ namespace {
 #endif
 constexpr int kRG = 2;             // rows per thread (targets pass)
 constexpr int kLseRG = DICP_LSE_RG;  // rows per thread (E and M passes)
+// the E-step against many components (the two-set match: C = N = 10^5) with 4 rows per thread:
+// two independent packed pairs per column hide the dependent v_pk chain's hazard stalls (100k x
+// 100k: 2.63 against 2.73 ms with one pair); against a few hundred (the atlas GMMs, C = 512) one
+// pair per thread keeps twice the workgroups (0.136 against 0.142 ms at 640k x 512, and the
+// M-step, rows = components, 0.146 against 0.217 ms) -- profiles/r05_ab_lse_pk.json
+constexpr int64_t kLseE4MinCols = 8192;
 // more column-chunk partials per row than this: the one-wave-per-row merge
 constexpr int kWaveMergeMinSplits = 64;
 
@@ -167,6 +174,153 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   }
 }
 
+// The same pass with the thread's rows packed in H float2 pairs (Op::Row2, tm2, accum2): the
+// logit, the row sums and their shift arithmetic as v_pk_fma_f32 (two rows per instruction),
+// the exps scalar -- ~13 packed instructions + 2 exp per column for two rows against 28 scalar
+// VALU + 2 exp (E-step).  Same rows, same order, same fmas: bitwise the scalar kernel's partials
+// (tests/test_gpu_em.py).  A pair whose tile overflows in either row is summed again as a pair,
+// only the overflowing row(s) re-referenced (the other row's partials come out unchanged).
+template <class Op, int H>
+__global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal sc,
+                                                               int64_t M, int64_t N, int64_t chunk,
+                                                               float* __restrict__ part) {
+  constexpr int R = 2 * H;
+  constexpr int CW4 = Op::CW4;
+  constexpr int NACC = Op::NACC;
+  constexpr int KS = Op::kShifted;
+  constexpr int W = 2 + NACC;
+  constexpr float kNinf = -__builtin_huge_valf();
+  __shared__ float4 lds[kTile * CW4];
+  const int tid = threadIdx.x;
+  const int64_t ibase = (int64_t)blockIdx.x * (kBlock * R) + tid;
+  typename Op::Row2 row[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    typename Op::Row rr[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      int64_t i = ibase + (int64_t)(2 * h + c) * kBlock;
+      if (i >= M) i = M - 1;
+      Op::load_row(args, sc, i, rr[c]);
+    }
+    Op::pack(rr[0], rr[1], row[h]);
+    row[h].k = Op::base2(row[h]);
+  }
+  const int64_t j0 = (int64_t)blockIdx.y * chunk;
+  int64_t j1 = j0 + chunk;
+  if (j1 > N) j1 = N;
+
+  f2 m[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) m[h] = splat(kNinf);
+  if (j0 < j1) {
+    const int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
+    if (tid < cnt) Op::load_col(args, sc, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+    __syncthreads();
+    const int ns = cnt < kLseShiftCols ? cnt : kLseShiftCols;
+#pragma unroll 2
+    for (int t = 0; t < ns; ++t) {
+      const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const f2 tm = Op::tm2(sc, row[h], rec);
+        m[h] = f2{fmaxf(m[h].x, tm.x), fmaxf(m[h].y, tm.y)};
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    if (m[h].x == kNinf) m[h].x = 0.f;
+    if (m[h].y == kNinf) m[h].y = 0.f;
+    row[h].k = row[h].k - m[h];
+  }
+
+  f2 tot[H][NACC + 1];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int k = 0; k <= NACC; ++k) tot[h][k] = splat(0.f);
+  bool first = true;
+  for (int64_t jt = j0; jt < j1; jt += kTile) {
+    const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
+    if (!first) {
+      if (tid < cnt) Op::load_col(args, sc, jt + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
+      __syncthreads();
+    }
+    first = false;
+    f2 acc[H][NACC + 1];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int k = 0; k <= NACC; ++k) acc[h][k] = splat(0.f);
+#pragma unroll 2
+    for (int t = 0; t < cnt; ++t) {
+      const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const f2 tm = Op::tm2(sc, row[h], rec);
+        const f2 e = f2{fast_exp2(tm.x), fast_exp2(tm.y)};
+        acc[h][0] = acc[h][0] + e;
+        Op::accum2(rec, tm, e, acc[h] + 1);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const bool ox = !(acc[h][0].x <= kLseOverflow), oy = !(acc[h][0].y <= kLseOverflow);
+      if (ox || oy) {
+        f2 mt = splat(kNinf);
+        for (int t = 0; t < cnt; ++t) {
+          const f2 v = Op::tm2(sc, row[h], reinterpret_cast<const float*>(&lds[t * CW4]));
+          mt = f2{fmaxf(mt.x, v.x), fmaxf(mt.y, v.y)};
+        }
+        // the row of the pair that did not overflow keeps its shift (mt = 0: its sums are
+        // scaled by 1 and re-summed with the same operands, in the same order -- unchanged)
+        mt = f2{ox ? mt.x : 0.f, oy ? mt.y : 0.f};
+        const f2 f = f2{fast_exp2(-mt.x), fast_exp2(-mt.y)}, l0 = tot[h][0];
+#pragma unroll
+        for (int k = 0; k <= NACC; ++k) {
+          f2 b = tot[h][k];
+          if (KS >= 0 && k == KS + 1) b = pk_fma(-mt, l0, b);
+          tot[h][k] = f2{f.x == 0.f ? 0.f : f.x * b.x, f.y == 0.f ? 0.f : f.y * b.y};
+          acc[h][k] = splat(0.f);
+        }
+        m[h] = m[h] + mt;
+        row[h].k = row[h].k - mt;
+        for (int t = 0; t < cnt; ++t) {
+          const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
+          const f2 tm = Op::tm2(sc, row[h], rec);
+          const f2 e = f2{fast_exp2(tm.x), fast_exp2(tm.y)};
+          acc[h][0] = acc[h][0] + e;
+          Op::accum2(rec, tm, e, acc[h] + 1);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k <= NACC; ++k) tot[h][k] = tot[h][k] + acc[h][k];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int64_t i = ibase + (int64_t)(2 * h + c) * kBlock;
+      if (i >= M) continue;
+      float* dst = part + ((int64_t)blockIdx.y * M + i) * W;
+      const float l = c ? tot[h][0].y : tot[h][0].x;
+      dst[0] = l > 0.f ? (c ? m[h].y : m[h].x) : kNinf;
+#pragma unroll
+      for (int k = 0; k <= NACC; ++k) dst[1 + k] = c ? tot[h][k].y : tot[h][k].x;
+    }
+}
+
+int& lse_pk_ref() {
+#ifndef DICP_LSE_PK
+#define DICP_LSE_PK 1
+#endif
+  static int v = DICP_LSE_PK;
+  return v;
+}
+
 // Merge S chunk partials of each row (fixed order) and finalize through Op::finalize.
 template <class Op>
 __global__ __launch_bounds__(kBlock) void lse_finalize_kernel(const float* __restrict__ part,
@@ -299,6 +453,30 @@ struct OpGmmE {
     acc[D] = fmaf(e, tm, acc[D]);
     acc[D + 1] = fmaf(e, rec[D], acc[D + 1]);
   }
+  // two rows packed in one VGPR pair (lse_rowred_pk_kernel): the same fmas as v_pk_fma_f32,
+  // the column fields broadcast into both halves -- bitwise the scalar form
+  struct Row2 { f2 x[D]; f2 k; };
+  __device__ static void pack(const Row& a, const Row& b, Row2& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) r.x[d] = f2{a.x[d], b.x[d]};
+  }
+  __device__ static f2 base2(const Row2&) { return splat(0.f); }
+  __device__ static f2 tm2(const Scal& sc, const Row2& r, const float* rec) {
+    f2 c = splat(rec[D]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const f2 z = r.x[d] - splat(rec[d]);
+      c = pk_fma(z, z, c);
+    }
+    return pk_fma(splat(sc.nc), c, r.k);
+  }
+  __device__ static void accum2(const float* rec, f2 tm, f2 e, f2* acc) {
+    if (!STATS) return;
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = pk_fma(e, splat(rec[d]), acc[d]);
+    acc[D] = pk_fma(e, tm, acc[D]);
+    acc[D + 1] = pk_fma(e, splat(rec[D]), acc[D + 1]);
+  }
   // outs: ptr[0] = T (natural, with -lgn), ptr[1] = T2 (log2, no lgn), ptr[2] = stats (D+4):
   //   sum gamma mu (D), sum gamma |mu|^2, sum gamma lgamma, sum gamma lpi, sum gamma D2
   // with (gamma-means, sum gamma = 1)  <t2 - m> = A, <v> = V:
@@ -364,6 +542,26 @@ struct OpGmmM {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = fmaf(e, rec[d], acc[d]);
   }
+  struct Row2 { f2 mu[D]; f2 w2; f2 k; };
+  __device__ static void pack(const Row& a, const Row& b, Row2& r) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) r.mu[d] = f2{a.mu[d], b.mu[d]};
+    r.w2 = f2{a.w2, b.w2};
+  }
+  __device__ static f2 base2(const Row2& r) { return r.w2; }
+  __device__ static f2 tm2(const Scal& sc, const Row2& r, const float* rec) {
+    f2 c = splat(rec[D]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const f2 z = r.mu[d] - splat(rec[d]);
+      c = pk_fma(z, z, c);
+    }
+    return pk_fma(splat(sc.nc), c, r.k);
+  }
+  __device__ static void accum2(const float* rec, f2, f2 e, f2* acc) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = pk_fma(e, splat(rec[d]), acc[d]);
+  }
   // outs.ptr[0] = colstats (D+1): {log sum gamma, mean x (D)}
   __device__ static void finalize(const Scal&, const Args&, int64_t i, float m, float l,
                                   const float* acc, const Outs& o) {
@@ -421,15 +619,18 @@ struct OpGmmTargets {
 };
 
 template <class Op, int R>
-int lse_splits(int64_t M, int64_t N) {
-  static int64_t cap = -1;
-  if (cap < 0) cap = (int64_t)device_cus() * blocks_per_cu(lse_rowred_kernel<Op, R>);
-  return num_splits_cap(M, N, R, cap);
+int lse_splits(int64_t M, int64_t N, bool pk) {
+  static int64_t cap[2] = {-1, -1};
+  if (cap[pk] < 0)
+    cap[pk] = (int64_t)device_cus() * (pk ? blocks_per_cu(lse_rowred_pk_kernel<Op, R / 2>)
+                                          : blocks_per_cu(lse_rowred_kernel<Op, R>));
+  return num_splits_cap(M, N, R, cap[pk]);
 }
 
 template <class Op, int R>
-size_t lse_ws_bytes(int64_t M, int64_t N) {
-  const int S = lse_splits<Op, R>(M, N);
+size_t lse_ws_bytes(int64_t M, int64_t N) {   // either kernel (their occupancies may differ)
+  const int S0 = lse_splits<Op, R>(M, N, false), S1 = lse_splits<Op, R>(M, N, true);
+  const int S = S0 > S1 ? S0 : S1;
   return (size_t)S * (size_t)M * (size_t)(2 + Op::NACC) * sizeof(float);
 }
 
@@ -437,7 +638,8 @@ template <class Op, int R>
 int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64_t N,
                const Outs& fin, void* ws, size_t ws_bytes, hipStream_t st) {
   if (M <= 0) return DICP_OK;
-  const int S = lse_splits<Op, R>(M, N);
+  const bool pk = lse_pk_ref() != 0 && R % 2 == 0;
+  const int S = lse_splits<Op, R>(M, N, pk);
   const int64_t chunk = N > 0 ? chunk_of(N, S) : 0;
   const size_t need = lse_ws_bytes<Op, R>(M, N);
   if (ws == nullptr || ws_bytes < need) {
@@ -446,8 +648,12 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
   }
   const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
   float* part = reinterpret_cast<float*>(ws);
-  lse_rowred_kernel<Op, R><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
-      a, sc, M, N, chunk, part);
+  if (pk)
+    lse_rowred_pk_kernel<Op, R / 2><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
+        a, sc, M, N, chunk, part);
+  else
+    lse_rowred_kernel<Op, R><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
+        a, sc, M, N, chunk, part);
   int rc = check_launch(name);
   if (rc) return rc;
   if (S > kWaveMergeMinSplits) {
@@ -469,11 +675,19 @@ int estep_d(const float* X, int64_t N, const float* mu, const float* w2, const f
   sc.aux0 = (float)lgn;
   sc.aux1 = 1.0f / sc.nc;
   const Outs o = make_outs(T, T2, stats);
+  if (C >= kLseE4MinCols) {   // many components: 4 rows (two packed pairs) per thread
+    if (stats) return launch_lse<OpGmmE<D, true>, 4>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
+    return launch_lse<OpGmmE<D, false>, 4>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
+  }
   if (stats) return launch_lse<OpGmmE<D, true>, kLseRG>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
   return launch_lse<OpGmmE<D, false>, kLseRG>("gmm_estep", a, sc, N, C, o, ws, wsb, st);
 }
 
 }  // namespace
+
+namespace dicp {
+int& lse_pk() { return lse_pk_ref(); }
+}  // namespace dicp
 
 // The Python wrapper precomputes the C-sized column vectors (w2, |mu|^2, lpi) with torch on
 // the device; the kernels here see only device pointers.
@@ -538,10 +752,14 @@ size_t dicp_gmm_ws(int kind, int64_t M, int64_t N, int D) {
   // M = rows of the data (N points), N = components (C) for the GMM kinds
   if (D != 2 && D != 3) return 0;
   switch (kind) {
-    case DICP_WS_GMM_ESTEP: {  // both variants (their occupancies, hence splits, differ)
-      size_t a = D == 2 ? lse_ws_bytes<OpGmmE<2, true>, kLseRG>(M, N) : lse_ws_bytes<OpGmmE<3, true>, kLseRG>(M, N);
-      size_t b = D == 2 ? lse_ws_bytes<OpGmmE<2, false>, kLseRG>(M, N) : lse_ws_bytes<OpGmmE<3, false>, kLseRG>(M, N);
-      return a > b ? a : b;
+    case DICP_WS_GMM_ESTEP: {  // every variant (their occupancies, hence splits, differ)
+      size_t m = 0;
+      for (size_t v : {D == 2 ? lse_ws_bytes<OpGmmE<2, true>, kLseRG>(M, N) : lse_ws_bytes<OpGmmE<3, true>, kLseRG>(M, N),
+                       D == 2 ? lse_ws_bytes<OpGmmE<2, false>, kLseRG>(M, N) : lse_ws_bytes<OpGmmE<3, false>, kLseRG>(M, N),
+                       D == 2 ? lse_ws_bytes<OpGmmE<2, true>, 4>(M, N) : lse_ws_bytes<OpGmmE<3, true>, 4>(M, N),
+                       D == 2 ? lse_ws_bytes<OpGmmE<2, false>, 4>(M, N) : lse_ws_bytes<OpGmmE<3, false>, 4>(M, N)})
+        m = v > m ? v : m;
+      return m;
     }
     case DICP_WS_GMM_MSTEP:
       return D == 2 ? lse_ws_bytes<OpGmmM<2>, kLseRG>(N, M) : lse_ws_bytes<OpGmmM<3>, kLseRG>(N, M);

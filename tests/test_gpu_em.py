@@ -103,3 +103,36 @@ def test_estep_stats_match_fp64(dev, D, case):
         assert torch.isfinite(st[:, k]).all(), k
         # the entropy and the squared distance are sums of O(1/sigma^2)-scaled logits (2e-5)
         assert rel_err(st[:, k], st64[:, k]) < (2e-5 if k >= D else 1e-5), (k, rel_err(st[:, k], st64[:, k]))
+
+
+@pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks"])
+def test_lse_packed_rows_bitwise(dev, case):
+    """The packed-row E and M passes (lse_rowred_pk_kernel, option lse_pk 1: two rows per
+    v_pk_fma_f32) against the scalar-row kernel (lse_pk 0): same rows, same order, same fmas --
+    bitwise, including dead components and re-referenced tiles."""
+    from difficp_amd import _lib
+    g = torch.Generator().manual_seed(len(case))
+    N, C, sigma = {"plain": (3001, 701, 0.1), "dead": (3000, 900, 0.1), "far_first": (2500, 800, 0.05),
+                   "chunks": (301, 60000, 0.02)}[case]
+    X = torch.rand(N, 3, generator=g)
+    mu = torch.rand(C, 3, generator=g)
+    w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    if case == "dead":
+        w[:300] = -math.inf
+    if case == "far_first":
+        mu[:400] += 3.0
+    lpi = (w - w.logsumexp(0)).float()
+    f = lambda t: t.float().to(dev).contiguous()
+    args = (f(X), f(mu), f(lpi / math.log(2)), f((mu * mu).sum(-1)), sigma, 0.5)
+    old = _lib.get_option("lse_pk")
+    out = {}
+    try:
+        for pk in (0, 1):
+            _lib.set_option("lse_pk", pk)
+            T, T2, st = _lib.gmm_estep(*args, True)
+            col = _lib.gmm_mstep(args[0], T2, args[1], args[2], sigma)
+            out[pk] = (T, T2, st, col)
+    finally:
+        _lib.set_option("lse_pk", old)
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(b, nan=7.0))
