@@ -399,9 +399,11 @@ def _launch(name, pairs, nbytes, fn):
 _WS_BYTES = {}   # (kind, M, N, D) -> dicp_workspace_bytes; cleared by set_option
 # Scratch workspaces reused per (stream, size): the launches of one stream run in order, so a
 # workspace handed to the next call on the same stream is free by the time that call's kernels
-# run -- one torch.empty less per library call (host floor, tools/host_floor.py).  Never while
-# a launch batch is open (its calls run together at the batch's end and each needs its own);
-# a few recent streams only (concurrent frames open a stream per Reg_opt call).
+# run -- one torch.empty less per library call (host floor, tools/host_floor.py).  Never for a
+# call that may run inside a launch batch (a batch open on this thread, or a frame thread of
+# the lockstep batches, whose calls from several frames share one stream and run together:
+# each needs its own -- tests/test_gpu_batch.py caught the shared one), nor inside a graph
+# capture; a few recent streams only (concurrent frames open a stream per Reg_opt call).
 _WS_CACHE = OrderedDict()
 _WS_CACHE_MAX = 8
 _ws_lock = threading.Lock()
@@ -428,6 +430,11 @@ def _workspace(kind: int, M: int, N: int, D: int, device):
         ws = _poison(torch.empty(nbytes, dtype=torch.uint8, device=device))
         keep.append(ws)
         return ws, nbytes
+    if getattr(_tl, "batcher", None) is not None:
+        # a frame of lockstep launch batches (core/batching.py): its launch may be recorded
+        # into one batch together with other frames' calls on the batcher's shared stream --
+        # each call needs a workspace of its own (the call's closure keeps it alive)
+        return _poison(torch.empty(nbytes, dtype=torch.uint8, device=device)), nbytes
     if torch.cuda.is_current_stream_capturing():
         # a HIP-graph capture (core/shooting.py): the workspace must come from the graph's own
         # pool, never a cached tensor that could be freed while the graph still points at it

@@ -11,6 +11,7 @@ backward) instead of the reference's per-reduction integrator loop.
 from __future__ import annotations
 
 import math
+import os
 import threading
 import weakref
 
@@ -29,6 +30,10 @@ from .shooting import (HamiltonianFn, OdeExtFn, OdeFn, RowOrderCache, ShootCache
 # per host thread: (q0 weak reference, q0 version, sigma, extent / sigma) of the last support
 # whose extent was read (LDDMMModel._raw_for): one device read per new q0 tensor
 _EXTENT_MEMO = threading.local()
+
+# Optimize's closures form loss and gradient without the autograd engine where the loss allows
+# (shooting.shoot_loss_grad; env DICP_DIRECT_LOSSGRAD=0: always through autograd)
+_DIRECT_LOSSGRAD = os.environ.get("DICP_DIRECT_LOSSGRAD", "1") != "0"
 
 class Shoot(list):
     """A "shoot" variable: list of (q, p, cost[, x]) states at the nt+1 integration times
@@ -394,18 +399,27 @@ class LDDMMModel:
             return self.trajloss(shoot) + dataloss(last)
 
         lossgrad = None
-        if getattr(_lib._tl, "batcher", None) is not None and not is_x:
-            # a frame of a lockstep launch batch (core/batching.py): the shooting's adjoint must
-            # run on this thread (autograd would run it on the engine's device thread, every
-            # frame in turn), so the closure forms loss and gradient directly -- bitwise the
-            # values of lossfunc(p0).backward()
+        batcher = getattr(_lib._tl, "batcher", None)
+        # the closure forms loss and gradient directly (shooting.shoot_loss_grad: ShootFn's
+        # forward and exact adjoint on THIS thread, bitwise the values of
+        # lossfunc(p0).backward()) for a frame of a lockstep launch batch (core/batching.py),
+        # whose adjoint must run on the frame's thread, and for every dense Euler shooting on
+        # the device whose loss is lam H0 + cost + data: no autograd engine (its device-thread
+        # hand-off and graph bookkeeping, ~0.1 ms of host time per closure -- the host floor,
+        # tools/host_floor.py), and concurrent frames' adjoints no longer queue on the
+        # engine's one device thread
+        direct = (_DIRECT_LOSSGRAD and not is_x and self.scheme == "Euler" and self.row_split is None
+                  and not (self.withlogdet and self.gradcomponent and self.try_trajcost_optim)
+                  and q0.is_cuda)
+        if (batcher is not None and not is_x) or direct:
             from .shooting import shoot_loss_grad
 
-            batcher = _lib._tl.batcher
-
             def lossgrad(p0):
-                with batcher.closure():   # a member of the launch batches while it evaluates
+                if batcher is None:
                     L, g, shoot = shoot_loss_grad(self, dataloss, q0, p0)
+                else:
+                    with batcher.closure():   # a member of the launch batches while it evaluates
+                        L, g, shoot = shoot_loss_grad(self, dataloss, q0, p0)
                 last_eval["p0"], last_eval["shoot"] = p0.detach().clone(), shoot
                 last_eval["p1_missing"] = getattr(shoot, "p1_missing", False)
                 return L, [g]

@@ -60,7 +60,10 @@ def test_graph_replay_bitwise(dev, version, M, D, need_p1):
 
 
 def test_graph_optimize_bitwise(dev):
-    """A whole LDDMMModel.Optimize (L-BFGS, strong-Wolfe) with and without the graphs."""
+    """A whole LDDMMModel.Optimize (L-BFGS, strong-Wolfe) with and without the graphs, and with
+    the closures' loss and gradient through autograd or formed directly (shoot_loss_grad,
+    LDDMM._DIRECT_LOSSGRAD): all four bitwise equal."""
+    from difficp_amd.core import LDDMM as LDm
     from difficp_amd.core import shooting
     from difficp_amd.core.LDDMM import LDDMMModel
     g = torch.Generator().manual_seed(3)
@@ -68,17 +71,19 @@ def test_graph_optimize_bitwise(dev):
     q0 = torch.rand(M, 3, generator=g).to(dev)
     tgt = (q0.cpu() + 0.05 * torch.randn(M, 3, generator=g)).to(dev)
     res = []
-    old = shooting._GRAPH_ON
+    old = shooting._GRAPH_ON, LDm._DIRECT_LOSSGRAD
     try:
         for on in (False, True):
-            shooting._GRAPH_ON = on
-            LM = LDDMMModel(sigma=0.1, D=3, lambd=10.0, version="hybrid", nt=10, scheme="Euler",
-                            spec={"device": dev, "dtype": torch.float32})
-            dataloss = LM.BasicQuadLossFunctor(tgt)
-            p0, shoot, trajl, datal, nsteps, change = LM.Optimize(dataloss, q0, torch.zeros_like(q0), nmax=3)
-            res.append((p0, shoot.Q, shoot.P, trajl, datal, nsteps))
+            for direct in (False, True):
+                shooting._GRAPH_ON, LDm._DIRECT_LOSSGRAD = on, direct
+                LM = LDDMMModel(sigma=0.1, D=3, lambd=10.0, version="hybrid", nt=10, scheme="Euler",
+                                spec={"device": dev, "dtype": torch.float32})
+                dataloss = LM.BasicQuadLossFunctor(tgt)
+                p0, shoot, trajl, datal, nsteps, change = LM.Optimize(dataloss, q0, torch.zeros_like(q0), nmax=3)
+                res.append((p0, shoot.Q, shoot.P, trajl, datal, nsteps))
     finally:
-        shooting._GRAPH_ON = old
-    a, b = res
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
-    assert a[3:] == b[3:]
+        shooting._GRAPH_ON, LDm._DIRECT_LOSSGRAD = old
+    a = res[0]
+    for b in res[1:]:
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+        assert a[3:] == b[3:]
