@@ -389,6 +389,15 @@ int dicp_supports_dim(int D);
  *                  1e9 pairs over the sharing calls; else 1), 1 or 2 forced
  *   "red_alg"      KBase / KRedScal / KRed / GradKRed and the external-point forward: 0 never
  *                  the centred expansion, 1 automatic by size (default), 2 always
+ *   "sym_red"      KBase / KRedScal / KRed with the rows equal to the columns (x == y): 0 never
+ *                  the pair-once symmetric centred sum, 1 automatic (default: wherever the
+ *                  centred expansion applies -- "red_alg" -- i.e. from 50k x 50k), 2 always
+ *                  (x == y only)
+ *   "sym_red_rows" rows per lane of the pair-once sums: 0 automatic (4), 4 or 8 forced
+ *   "sym_fwd_rows" rows per lane of the symmetric eta = 0 forward: 0 automatic (8 from 110k
+ *                  points alone on the chip, else 4), 4 or 8 forced
+ *   "lse_pk"       GMM E / M passes: 1 rows packed in float2 pairs (v_pk_fma_f32, default),
+ *                  0 scalar rows (bitwise equal)
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
  *   "mfma_rmax_x100"  matrix-core forward (fwd_alg 3): largest workgroup row spread (scaled
  *                  units x 100) that takes the MFMA branch; >= 100000 always, 0 never (default 300)
