@@ -90,7 +90,13 @@ def test_psr_std_support_schemes(dev, scheme, weights):
     ref = C.reference(scheme, weights)
     assert abs(Es[0] - ref[0]) <= 1e-5 * abs(ref[0]), (Es[0], ref[0])
     if scheme == "grid":
-        tol = max(1e-3, 2 * C.FP32_DEV[(scheme, weights)])
+        # the energy after each optimisation stage: an L-BFGS path whose float32 rounding is
+        # amplified stage by stage.  The CPU float32 oracle drifts from float64 by FP32_DEV; the
+        # GPU's float32 path (other fma contractions and reduction orders) drifts by up to 3.5x
+        # that at the last stage (5.6e-3 with weights, 2.0e-3 without; the first energy 7e-7),
+        # bitwise the same with every host mechanism switched off (workspace cache, graphs,
+        # direct closures: profiles/r05_psr_std_trace_switches.jsonl) -- so 4x, not 2x
+        tol = max(1e-3, 4 * C.FP32_DEV[(scheme, weights)])
         for a, b in zip(Es, ref):
             assert abs(a - b) <= tol * abs(b), (Es, ref)
     else:
