@@ -12,6 +12,8 @@
 #include "lddmm_ops.hpp"
 #include "packed.hpp"
 
+#include <type_traits>
+
 using namespace dicp;
 
 namespace {
@@ -118,22 +120,40 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
       __syncthreads();
     }
     first = false;
+    // a tile of equal weights (every column's v = v0): its sum e v is v0 sum e (lse_uniform)
+    float v0 = 0.f;
+    bool uni = false;
+    if (Op::kUni >= 0 && R >= 4) {   // the many-component E-step (kLseE4MinCols) only
+      v0 = Op::uni_value(args, sc, jt);
+      uni = !__syncthreads_or(tid < cnt && Op::uni_value(args, sc, jt + tid) != v0);
+    }
     float acc[R][NACC + 1];
+    auto pass = [&](auto U, int r0, int r1) {
+      constexpr bool kU = decltype(U)::value;
+#pragma unroll 2
+      for (int t = 0; t < cnt; ++t) {
+        const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r < r0 || r >= r1) continue;
+          const float tm = Op::tm(sc, row[r], rec);
+          const float e = fast_exp2(tm);
+          acc[r][0] += e;
+          Op::template accum<kU>(rec, tm, e, acc[r] + 1);
+        }
+      }
+      if (kU) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (r >= r0 && r < r1) acc[r][1 + Op::kUni] = v0 * acc[r][0];
+      }
+    };
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) acc[r][k] = 0.f;
-#pragma unroll 2
-    for (int t = 0; t < cnt; ++t) {
-      const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float tm = Op::tm(sc, row[r], rec);
-        const float e = fast_exp2(tm);
-        acc[r][0] += e;
-        Op::accum(rec, tm, e, acc[r] + 1);
-      }
-    }
+    if (uni) pass(std::true_type{}, 0, R);
+    else pass(std::false_type{}, 0, R);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (!(acc[r][0] <= kLseOverflow)) {   // re-reference the row to the tile's maximum
@@ -150,13 +170,8 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
         }
         m[r] += mt;
         row[r].k -= mt;
-        for (int t = 0; t < cnt; ++t) {
-          const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
-          const float tm = Op::tm(sc, row[r], rec);
-          const float e = fast_exp2(tm);
-          acc[r][0] += e;
-          Op::accum(rec, tm, e, acc[r] + 1);
-        }
+        if (uni) pass(std::true_type{}, r, r + 1);
+        else pass(std::false_type{}, r, r + 1);
       }
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) tot[r][k] += acc[r][k];
@@ -248,22 +263,39 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
       __syncthreads();
     }
     first = false;
+    float v0 = 0.f;
+    bool uni = false;
+    if (Op::kUni >= 0 && H >= 2) {   // the many-component E-step (kLseE4MinCols) only
+      v0 = Op::uni_value(args, sc, jt);
+      uni = !__syncthreads_or(tid < cnt && Op::uni_value(args, sc, jt + tid) != v0);
+    }
     f2 acc[H][NACC + 1];
+    auto pass = [&](auto U, int h0, int h1) {
+      constexpr bool kU = decltype(U)::value;
+#pragma unroll 2
+      for (int t = 0; t < cnt; ++t) {
+        const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          if (h < h0 || h >= h1) continue;
+          const f2 tm = Op::tm2(sc, row[h], rec);
+          const f2 e = f2{fast_exp2(tm.x), fast_exp2(tm.y)};
+          acc[h][0] = acc[h][0] + e;
+          Op::template accum2<kU>(rec, tm, e, acc[h] + 1);
+        }
+      }
+      if (kU) {
+#pragma unroll
+        for (int h = 0; h < H; ++h)
+          if (h >= h0 && h < h1) acc[h][1 + Op::kUni] = splat(v0) * acc[h][0];
+      }
+    };
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) acc[h][k] = splat(0.f);
-#pragma unroll 2
-    for (int t = 0; t < cnt; ++t) {
-      const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
-#pragma unroll
-      for (int h = 0; h < H; ++h) {
-        const f2 tm = Op::tm2(sc, row[h], rec);
-        const f2 e = f2{fast_exp2(tm.x), fast_exp2(tm.y)};
-        acc[h][0] = acc[h][0] + e;
-        Op::accum2(rec, tm, e, acc[h] + 1);
-      }
-    }
+    if (uni) pass(std::true_type{}, 0, H);
+    else pass(std::false_type{}, 0, H);
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       const bool ox = !(acc[h][0].x <= kLseOverflow), oy = !(acc[h][0].y <= kLseOverflow);
@@ -286,13 +318,8 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
         }
         m[h] = m[h] + mt;
         row[h].k = row[h].k - mt;
-        for (int t = 0; t < cnt; ++t) {
-          const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
-          const f2 tm = Op::tm2(sc, row[h], rec);
-          const f2 e = f2{fast_exp2(tm.x), fast_exp2(tm.y)};
-          acc[h][0] = acc[h][0] + e;
-          Op::accum2(rec, tm, e, acc[h] + 1);
-        }
+        if (uni) pass(std::true_type{}, h, h + 1);
+        else pass(std::false_type{}, h, h + 1);
       }
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) tot[h][k] = tot[h][k] + acc[h][k];
@@ -434,8 +461,7 @@ struct OpGmmE {
   // sc.aux1 = 1 / nc (< 0); a dead component (w2 = -inf) gets the logit kLseDead
   __device__ static void load_col(const Args& a, const Scal& sc, int64_t j, float* rec) {
     ld<D>(a.c0, j, rec);
-    const float cap = fminf(kLseDead * sc.aux1, 1e37f);
-    rec[D] = fminf(a.c1[j] * sc.aux1, cap);
+    rec[D] = uni_value(a, sc, j);
   }
   __device__ static float tm(const Scal& sc, const Row& r, const float* rec) {
     float c = rec[D];
@@ -446,12 +472,24 @@ struct OpGmmE {
     }
     return fmaf(sc.nc, c, r.k);
   }
+  // kUni: the acc slot of sum e v, which a tile of equal weights (v = v0 for every column:
+  // the two-set match's frozen uniform GMM) forms as v0 sum e after the tile instead of one
+  // fma per pair (uni_value(j) = column j's v, as load_col computes it).  Taken by the
+  // many-component E-step (4 rows per thread, C >= kLseE4MinCols: 2.61 -> 2.47 ms at 100k x
+  // 100k); a few hundred components gain nothing measurable from it, and keep their rounding
+  // (the Chui two-set trace's EM stop test at tol 1e-3 flips one EM step on rounding-level
+  // changes -- profiles/r05_chui_uniform_flip.txt)
+  static constexpr int kUni = STATS ? D + 1 : -1;
+  __device__ static float uni_value(const Args& a, const Scal& sc, int64_t j) {
+    return fminf(a.c1[j] * sc.aux1, fminf(kLseDead * sc.aux1, 1e37f));
+  }
+  template <bool U = false>
   __device__ static void accum(const float* rec, float tm, float e, float* acc) {
     if (!STATS) return;
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = fmaf(e, rec[d], acc[d]);
     acc[D] = fmaf(e, tm, acc[D]);
-    acc[D + 1] = fmaf(e, rec[D], acc[D + 1]);
+    if (!U) acc[D + 1] = fmaf(e, rec[D], acc[D + 1]);
   }
   // two rows packed in one VGPR pair (lse_rowred_pk_kernel): the same fmas as v_pk_fma_f32,
   // the column fields broadcast into both halves -- bitwise the scalar form
@@ -470,12 +508,13 @@ struct OpGmmE {
     }
     return pk_fma(splat(sc.nc), c, r.k);
   }
+  template <bool U = false>
   __device__ static void accum2(const float* rec, f2 tm, f2 e, f2* acc) {
     if (!STATS) return;
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = pk_fma(e, splat(rec[d]), acc[d]);
     acc[D] = pk_fma(e, tm, acc[D]);
-    acc[D + 1] = pk_fma(e, splat(rec[D]), acc[D + 1]);
+    if (!U) acc[D + 1] = pk_fma(e, splat(rec[D]), acc[D + 1]);
   }
   // outs: ptr[0] = T (natural, with -lgn), ptr[1] = T2 (log2, no lgn), ptr[2] = stats (D+4):
   //   sum gamma mu (D), sum gamma |mu|^2, sum gamma lgamma, sum gamma lpi, sum gamma D2
@@ -538,6 +577,9 @@ struct OpGmmM {
     }
     return fmaf(sc.nc, c, r.k);
   }
+  static constexpr int kUni = -1;
+  __device__ static float uni_value(const Args&, const Scal&, int64_t) { return 0.f; }
+  template <bool U = false>
   __device__ static void accum(const float* rec, float, float e, float* acc) {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = fmaf(e, rec[d], acc[d]);
@@ -558,6 +600,7 @@ struct OpGmmM {
     }
     return pk_fma(splat(sc.nc), c, r.k);
   }
+  template <bool U = false>
   __device__ static void accum2(const float* rec, f2, f2 e, f2* acc) {
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[d] = pk_fma(e, splat(rec[d]), acc[d]);

@@ -74,7 +74,7 @@ def _estep64(X, mu, lpi, sigma):
 
 
 @pytest.mark.parametrize("D", [2, 3])
-@pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks"])
+@pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks", "uniform"])
 def test_estep_stats_match_fp64(dev, D, case):
     """Every output of dicp_gmm_estep_f32 (T, T2 and the D+4 stats, include/difficp_hip.h)
     against float64 rows: random weights; dead components (w = -inf, the first 300 of them: a
@@ -83,10 +83,12 @@ def test_estep_stats_match_fp64(dev, D, case):
     from difficp_amd import _lib
     g = torch.Generator().manual_seed(11 * D + len(case))
     N, C, sigma = {"plain": (3000, 700, 0.1), "dead": (3000, 900, 0.1), "far_first": (2500, 800, 0.05),
-                   "chunks": (300, 60000, 0.02)}[case]
+                   "chunks": (300, 60000, 0.02), "uniform": (2000, 20000, 0.05)}[case]
     X = torch.rand(N, D, generator=g, dtype=torch.float64)
     mu = torch.rand(C, D, generator=g, dtype=torch.float64)
     w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    if case == "uniform":     # equal weights: the tiles' sum e v formed as v0 sum e
+        w = torch.zeros(C, dtype=torch.float64)
     if case == "dead":
         w[:300] = -math.inf
         w[600:650] = -math.inf
@@ -105,7 +107,7 @@ def test_estep_stats_match_fp64(dev, D, case):
         assert rel_err(st[:, k], st64[:, k]) < (2e-5 if k >= D else 1e-5), (k, rel_err(st[:, k], st64[:, k]))
 
 
-@pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks"])
+@pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks", "uniform"])
 def test_lse_packed_rows_bitwise(dev, case):
     """The packed-row E and M passes (lse_rowred_pk_kernel, option lse_pk 1: two rows per
     v_pk_fma_f32) against the scalar-row kernel (lse_pk 0): same rows, same order, same fmas --
@@ -113,10 +115,12 @@ def test_lse_packed_rows_bitwise(dev, case):
     from difficp_amd import _lib
     g = torch.Generator().manual_seed(len(case))
     N, C, sigma = {"plain": (3001, 701, 0.1), "dead": (3000, 900, 0.1), "far_first": (2500, 800, 0.05),
-                   "chunks": (301, 60000, 0.02)}[case]
+                   "chunks": (301, 60000, 0.02), "uniform": (2001, 20000, 0.05)}[case]
     X = torch.rand(N, 3, generator=g)
     mu = torch.rand(C, 3, generator=g)
     w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    if case == "uniform":
+        w = torch.zeros(C, dtype=torch.float64)
     if case == "dead":
         w[:300] = -math.inf
     if case == "far_first":
