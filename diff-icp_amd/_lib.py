@@ -49,6 +49,7 @@ _SIGNATURES = {
     "dicp_lddmm_ode_ext_bwd_f32": [_P, _I64, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P,
                                    _P, _SZ, _P],
     "dicp_gmm_estep_f32": [_P, _I64, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _SZ, _P],
+    "dicp_gmm_estep_hint_f32": [_P, _I64, _P, _P, _P, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P, _P, _SZ, _P],
     "dicp_gmm_mstep_f32": [_P, _P, _I64, _P, _P, _I64, _INT, _DBL, _P, _P, _SZ, _P],
     "dicp_gmm_targets_f32": [_P, _P, _I64, _P, _P, _DBL, _P, _P, _I64, _INT, _P, _P, _SZ, _P],
     "dicp_lddmm_ode_self_fwd_rows_f32": [_P, _P, _I64, _I64, _I64, _INT, _DBL, _DBL, _P, _P, _P, _P,
@@ -699,7 +700,9 @@ def ode_ext_bwd(x, q, p, gvx, gdiv, sigma: float, eta: float, gq, gp):
 # ---------------------------------------------------------------------------------------
 # GMM EM passes
 # ---------------------------------------------------------------------------------------
-def gmm_estep(X, mu, w2, mu2, sigma: float, lgn: float, want_stats: bool):
+def gmm_estep(X, mu, w2, mu2, sigma: float, lgn: float, want_stats: bool, hint=None):
+    """hint: optional (N,) float32 device tensor, the rows' expected log2 LSE (e.g. the T2 of the
+    previous EM step over the same rows) -- dicp_gmm_estep_hint_f32's shift hint."""
     X = _dev(X, "X")
     mu = _dev(mu, "mu")
     w2 = _dev(w2, "w2")
@@ -707,6 +710,10 @@ def gmm_estep(X, mu, w2, mu2, sigma: float, lgn: float, want_stats: bool):
     N, D = X.shape
     C = mu.shape[0]
     dev = X.device
+    if hint is not None:
+        hint = _dev(hint, "hint")
+        if hint.shape != (N,):
+            raise ValueError(f"gmm_estep: hint must be shaped ({N},)")
     T = torch.empty(N, device=dev, dtype=torch.float32)
     T2 = torch.empty(N, device=dev, dtype=torch.float32)
     stats = torch.empty((N, D + 4), device=dev, dtype=torch.float32) if want_stats else None
@@ -714,9 +721,9 @@ def gmm_estep(X, mu, w2, mu2, sigma: float, lgn: float, want_stats: bool):
         return T, T2, stats
     ws, nb = _workspace(WS_GMM_ESTEP, N, C, D, dev)
     rc = _launch("gmm_estep", N * C, 4 * (N * (2 * D + 6) + C * (D + 2)),
-                 lambda: lib().dicp_gmm_estep_f32(_ptr(X), N, _ptr(mu), _ptr(w2), _ptr(mu2), C, D, float(sigma),
-                                  float(lgn), _ptr(T), _ptr(T2), _ptr(stats), _ptr(ws), nb,
-                                  _stream(dev)))
+                 lambda: lib().dicp_gmm_estep_hint_f32(_ptr(X), N, _ptr(mu), _ptr(w2), _ptr(mu2), C, D,
+                                                       float(sigma), float(lgn), _ptr(hint), _ptr(T), _ptr(T2),
+                                                       _ptr(stats), _ptr(ws), nb, _stream(dev)))
     _check_rc(rc, "gmm_estep")
     return T, T2, stats
 

@@ -213,7 +213,13 @@ class GaussianMixtureUnif(torch.nn.Module):
         lpi_old, w2_old, mu2_old = self._columns(mu_old, w_old)
 
         # ---- E step: T_n and responsibility-weighted row sums (old params) ----
-        T, T2, stats = _lib.gmm_estep(X, mu_old, w2_old, mu2_old, sigma_old, lgn_old, True)
+        # the previous E-step's T2 over the same rows shifts the single exp sweep (a change of
+        # reference: dicp_gmm_estep_hint_f32 -- without it a small sigma re-references most rows'
+        # tiles; any hint is safe, a stale one only costs re-referencing)
+        prev = getattr(self, "_estep_hint", None)
+        hint = prev[2] if (prev is not None and prev[0] == N and prev[1] == X.device) else None
+        T, T2, stats = _lib.gmm_estep(X, mu_old, w2_old, mu2_old, sigma_old, lgn_old, True, hint=hint)
+        self._estep_hint = (N, X.device, T2)
         E_row = stats[:, D + 1]                   # sum_c gamma lgamma
 
         if self.outliers is not None:

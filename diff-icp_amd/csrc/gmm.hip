@@ -36,17 +36,24 @@ constexpr int kWaveMergeMinSplits = 64;
 // LSE row-reduction skeleton: part[(s*M + i)*(2+NACC) + ...] = {m, l, acc...} with
 // m = the chunk's shift (log2 domain), l = sum_j 2^(t_ij - m), acc = Op::accum weighted sums.
 // One exp2 sweep: the shift m is the exact maximum over the chunk's first kLseShiftCols
-// columns (a logit-only pass).  Every pair is summed without a test; a tile whose partial
-// l exceeds kLseOverflow (a term above 2^56: a component much closer than any of the first
-// ones, or +inf / NaN from one above 2^128) is re-referenced to its exact maximum and summed
-// again -- rare, one divergent lane, instead of a compare + exec-mask branch per pair (round 4's
-// per-pair test cost ~6 SALU + 1 VALU of the E-step's ~25 issue slots per pair).
+// columns (a logit-only pass) -- or, with a hint (the previous EM step's T2), near the row's
+// LSE -- and a logit far above it re-references the row's sums (adaptive, see kLseSlack).
 // Op interface (Row carries k = the row's exponent constant minus the shift):
 //   CW4 / NACC / kShifted (the acc slot holding sum e (t - m), re-referenced on merges; -1)
 //   load_row(a, sc, i, row), base(row) (the row constant of the logit), load_col(a, sc, j, rec)
 //   tm(sc, row, rec) = t - m, accum(rec, tm, e, acc), finalize(sc, a, i, m, l, acc, outs)
 // ---------------------------------------------------------------------------------------
+// Re-referencing, adaptive per workgroup: first at the tile's end (a partial above
+// kLseOverflow -- a term above 2^56, or inf / NaN -- sends the row's tile through again,
+// re-referenced to its exact maximum: free while events are rare); after lse_adapt() tiles
+// that needed it anywhere in the workgroup, a per-pair test (a logit more than kLseSlack above
+// the shift re-references the row's sums in the loop, ~20 instructions per event, a compare per
+// pair).  Measured at 100k x 100k (tools/probes/estep_sigma.py): tile-end only 2.54 ms at sigma
+// 0.05 but 5.9 at 0.01 (a random 64-column sample then sits ~450 log2 units below the nearest
+// component: events in most tiles of most waves, each a tile summed again); per-pair only
+// 3.40-3.70 ms at every sigma.
 constexpr float kLseOverflow = 0x1p64f;
+constexpr float kLseSlack = 64.f;
 // columns of the chunk's first tile whose logits set the shift (the exact maximum over them):
 // 64 of the <= 256 staged -- a 1/28 logit overhead at the 100k two-set E-step's ~1800-column
 // chunks instead of 1/7; a row whose nearest components come later is re-referenced once
@@ -61,10 +68,22 @@ constexpr int kLseShiftCols = 64;
 // component are outside the single sweep's range (the log-likelihood there is below -1e9).
 constexpr float kLseDead = -1e8f;
 
+// The shift of a row given a hint of its LSE (the previous EM step's T2): the row's largest
+// term then sits near 2^8, every term of the chunk stays below the 2^56 re-reference test
+// unless the logits rose by ~48 since the hint, and the clamp to [m64, m64 + 100] (m64 = the
+// exact maximum of the chunk's first 64 logits) keeps any hint safe: the shift is never below
+// a logit of the chunk, and never so far above one that it underflows (2^-100 > 2^-126);
+// terms more than 126 below the shift are below 2^-126 of the row's sum, as in any shift.
+// A non-finite hint leaves m64.
+__device__ __forceinline__ float lse_hinted_shift(float m64, float hint) {
+  if (!(hint > -1e30f && hint < 1e30f)) return m64;
+  return fminf(fmaxf(hint - 8.f, m64), m64 + 100.f);
+}
+
 template <class Op, int R>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
                                                             int64_t M, int64_t N, int64_t chunk,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part, int adapt) {
   constexpr int CW4 = Op::CW4;
   constexpr int NACC = Op::NACC;
   constexpr int KS = Op::kShifted;
@@ -101,9 +120,15 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
     }
   }
   // -inf (a dead row of the M-step: w2 = -inf): shift 0, its terms are all 0
+  const float* hint = Op::hint(args);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (m[r] == -__builtin_huge_valf()) m[r] = 0.f;
+    if (hint != nullptr) {   // the row's expected LSE: m = clamp(hint - 8, m64, m64 + 100)
+      int64_t i = ibase + (int64_t)r * kBlock;
+      if (i >= M) i = M - 1;
+      m[r] = lse_hinted_shift(m[r], hint[i]);
+    }
     row[r].k -= m[r];
   }
 
@@ -112,6 +137,8 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int k = 0; k <= NACC; ++k) tot[r][k] = 0.f;
+  bool pair_mode = adapt <= 0;
+  int reref_tiles = 0;
   bool first = true;   // the first tile is already in LDS
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
@@ -128,15 +155,31 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
       uni = !__syncthreads_or(tid < cnt && Op::uni_value(args, sc, jt + tid) != v0);
     }
     float acc[R][NACC + 1];
-    auto pass = [&](auto U, int r0, int r1) {
-      constexpr bool kU = decltype(U)::value;
+    auto pass = [&](auto U, auto P, int r0, int r1) {
+      constexpr bool kU = decltype(U)::value, kP = decltype(P)::value;
 #pragma unroll 2
       for (int t = 0; t < cnt; ++t) {
         const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           if (r < r0 || r >= r1) continue;
-          const float tm = Op::tm(sc, row[r], rec);
+          float tm = Op::tm(sc, row[r], rec);
+          if (kP && tm > kLseSlack) {   // re-reference the row to tm (as lse_reref_lane_t)
+            const float f = fast_exp2(-tm), t0 = tot[r][0], a0 = acc[r][0];
+#pragma unroll
+            for (int q = 0; q <= NACC; ++q) {
+              float b = tot[r][q], a = acc[r][q];
+              if (KS >= 0 && q == KS + 1) {
+                b = fmaf(-tm, t0, b);
+                a = fmaf(-tm, a0, a);
+              }
+              tot[r][q] = b * f;
+              acc[r][q] = a * f;
+            }
+            m[r] += tm;
+            row[r].k -= tm;
+            tm = 0.f;
+          }
           const float e = fast_exp2(tm);
           acc[r][0] += e;
           Op::template accum<kU>(rec, tm, e, acc[r] + 1);
@@ -148,35 +191,45 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
           if (r >= r0 && r < r1) acc[r][1 + Op::kUni] = v0 * acc[r][0];
       }
     };
+    auto run = [&](auto P, int r0, int r1) {
+      if (uni) pass(std::true_type{}, P, r0, r1);
+      else pass(std::false_type{}, P, r0, r1);
+    };
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) acc[r][k] = 0.f;
-    if (uni) pass(std::true_type{}, 0, R);
-    else pass(std::false_type{}, 0, R);
+    bool reref = false;
+    if (pair_mode) {
+      run(std::true_type{}, 0, R);
+    } else {
+      run(std::false_type{}, 0, R);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (!(acc[r][0] <= kLseOverflow)) {   // re-reference the row to the tile's maximum
-        float mt = -__builtin_huge_valf();
-        for (int t = 0; t < cnt; ++t)
-          mt = fmaxf(mt, Op::tm(sc, row[r], reinterpret_cast<const float*>(&lds[t * CW4])));
-        const float f = fast_exp2(-mt), l0 = tot[r][0];
+      for (int r = 0; r < R; ++r) {
+        if (!(acc[r][0] <= kLseOverflow)) {   // re-reference the row to the tile's maximum
+          reref = true;
+          float mt = -__builtin_huge_valf();
+          for (int t = 0; t < cnt; ++t)
+            mt = fmaxf(mt, Op::tm(sc, row[r], reinterpret_cast<const float*>(&lds[t * CW4])));
+          const float f = fast_exp2(-mt), l0 = tot[r][0];
 #pragma unroll
-        for (int k = 0; k <= NACC; ++k) {
-          float b = tot[r][k];
-          if (KS >= 0 && k == KS + 1) b = fmaf(-mt, l0, b);   // sum e (t - m): t - m' = (t - m) - mt
-          tot[r][k] = f == 0.f ? 0.f : f * b;
-          acc[r][k] = 0.f;
+          for (int k = 0; k <= NACC; ++k) {
+            float b = tot[r][k];
+            if (KS >= 0 && k == KS + 1) b = fmaf(-mt, l0, b);   // sum e (t - m): t - m' = (t - m) - mt
+            tot[r][k] = f == 0.f ? 0.f : f * b;
+            acc[r][k] = 0.f;
+          }
+          m[r] += mt;
+          row[r].k -= mt;
+          run(std::false_type{}, r, r + 1);
         }
-        m[r] += mt;
-        row[r].k -= mt;
-        if (uni) pass(std::true_type{}, r, r + 1);
-        else pass(std::false_type{}, r, r + 1);
       }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) tot[r][k] += acc[r][k];
-    }
-    __syncthreads();
+    if (__syncthreads_or(reref) && ++reref_tiles >= adapt) pair_mode = true;
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -195,10 +248,33 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
 // VALU + 2 exp (E-step).  Same rows, same order, same fmas: bitwise the scalar kernel's partials
 // (tests/test_gpu_em.py).  A pair whose tile overflows in either row is summed again as a pair,
 // only the overflowing row(s) re-referenced (the other row's partials come out unchanged).
+// Re-reference one lane (c = 0: .x, 1: .y) of a packed row pair to a logit tm above the shift
+// by more than kLseSlack: the row's sums so far (tile and total) are scaled by 2^-tm, the
+// e (t - m) sum also moved by -tm times the row's count, and the shift rises by tm (then tm = 0).
+template <int NACC, int KS, int C>
+__device__ __forceinline__ void lse_reref_lane_t(f2& tm2, f2& m2, f2& k2, f2* tot, f2* acc) {
+  const float tm = C ? tm2.y : tm2.x;
+  if (!(tm > kLseSlack)) return;
+  const float f = fast_exp2(-tm);
+  const float t0 = C ? tot[0].y : tot[0].x, a0 = C ? acc[0].y : acc[0].x;
+#pragma unroll
+  for (int q = 0; q <= NACC; ++q) {
+    float b = C ? tot[q].y : tot[q].x, a = C ? acc[q].y : acc[q].x;
+    if (KS >= 0 && q == KS + 1) {
+      b = fmaf(-tm, t0, b);
+      a = fmaf(-tm, a0, a);
+    }
+    b *= f;
+    a *= f;
+    if (C) { tot[q].y = b; acc[q].y = a; } else { tot[q].x = b; acc[q].x = a; }
+  }
+  if (C) { m2.y += tm; k2.y -= tm; tm2.y = 0.f; } else { m2.x += tm; k2.x -= tm; tm2.x = 0.f; }
+}
+
 template <class Op, int H>
 __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal sc,
                                                                int64_t M, int64_t N, int64_t chunk,
-                                                               float* __restrict__ part) {
+                                                               float* __restrict__ part, int adapt) {
   constexpr int R = 2 * H;
   constexpr int CW4 = Op::CW4;
   constexpr int NACC = Op::NACC;
@@ -243,10 +319,17 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
       }
     }
   }
+  const float* hint = Op::hint(args);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     if (m[h].x == kNinf) m[h].x = 0.f;
     if (m[h].y == kNinf) m[h].y = 0.f;
+    if (hint != nullptr) {
+      int64_t i0 = ibase + (int64_t)(2 * h) * kBlock, i1 = ibase + (int64_t)(2 * h + 1) * kBlock;
+      if (i0 >= M) i0 = M - 1;
+      if (i1 >= M) i1 = M - 1;
+      m[h] = f2{lse_hinted_shift(m[h].x, hint[i0]), lse_hinted_shift(m[h].y, hint[i1])};
+    }
     row[h].k = row[h].k - m[h];
   }
 
@@ -255,6 +338,8 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
   for (int h = 0; h < H; ++h)
 #pragma unroll
     for (int k = 0; k <= NACC; ++k) tot[h][k] = splat(0.f);
+  bool pair_mode = adapt <= 0;
+  int reref_tiles = 0;
   bool first = true;
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
@@ -270,15 +355,21 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
       uni = !__syncthreads_or(tid < cnt && Op::uni_value(args, sc, jt + tid) != v0);
     }
     f2 acc[H][NACC + 1];
-    auto pass = [&](auto U, int h0, int h1) {
-      constexpr bool kU = decltype(U)::value;
+    // U: uniform-weight tile; P: per-pair re-reference test (else: the tile-end test);
+    // [h0, h1): the row pairs summed (a tile-end re-reference sums one pair again)
+    auto pass = [&](auto U, auto P, int h0, int h1) {
+      constexpr bool kU = decltype(U)::value, kP = decltype(P)::value;
 #pragma unroll 2
       for (int t = 0; t < cnt; ++t) {
         const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
 #pragma unroll
         for (int h = 0; h < H; ++h) {
           if (h < h0 || h >= h1) continue;
-          const f2 tm = Op::tm2(sc, row[h], rec);
+          f2 tm = Op::tm2(sc, row[h], rec);
+          if (kP && (tm.x > kLseSlack || tm.y > kLseSlack)) {   // re-reference the row(s) to tm
+            lse_reref_lane_t<NACC, KS, 0>(tm, m[h], row[h].k, tot[h], acc[h]);
+            lse_reref_lane_t<NACC, KS, 1>(tm, m[h], row[h].k, tot[h], acc[h]);
+          }
           const f2 e = f2{fast_exp2(tm.x), fast_exp2(tm.y)};
           acc[h][0] = acc[h][0] + e;
           Op::template accum2<kU>(rec, tm, e, acc[h] + 1);
@@ -290,41 +381,53 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
           if (h >= h0 && h < h1) acc[h][1 + Op::kUni] = splat(v0) * acc[h][0];
       }
     };
+    auto run = [&](auto P, int h0, int h1) {
+      if (uni) pass(std::true_type{}, P, h0, h1);
+      else pass(std::false_type{}, P, h0, h1);
+    };
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) acc[h][k] = splat(0.f);
-    if (uni) pass(std::true_type{}, 0, H);
-    else pass(std::false_type{}, 0, H);
+    bool reref = false;
+    if (pair_mode) {
+      run(std::true_type{}, 0, H);
+    } else {
+      run(std::false_type{}, 0, H);
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const bool ox = !(acc[h][0].x <= kLseOverflow), oy = !(acc[h][0].y <= kLseOverflow);
-      if (ox || oy) {
-        f2 mt = splat(kNinf);
-        for (int t = 0; t < cnt; ++t) {
-          const f2 v = Op::tm2(sc, row[h], reinterpret_cast<const float*>(&lds[t * CW4]));
-          mt = f2{fmaxf(mt.x, v.x), fmaxf(mt.y, v.y)};
-        }
-        // the row of the pair that did not overflow keeps its shift (mt = 0: its sums are
-        // scaled by 1 and re-summed with the same operands, in the same order -- unchanged)
-        mt = f2{ox ? mt.x : 0.f, oy ? mt.y : 0.f};
-        const f2 f = f2{fast_exp2(-mt.x), fast_exp2(-mt.y)}, l0 = tot[h][0];
+      for (int h = 0; h < H; ++h) {   // tile-end test: a term above 2^56 (or inf / NaN)
+        const bool ox = !(acc[h][0].x <= kLseOverflow), oy = !(acc[h][0].y <= kLseOverflow);
+        if (ox || oy) {
+          reref = true;
+          f2 mt = splat(kNinf);
+          for (int t = 0; t < cnt; ++t) {
+            const f2 v = Op::tm2(sc, row[h], reinterpret_cast<const float*>(&lds[t * CW4]));
+            mt = f2{fmaxf(mt.x, v.x), fmaxf(mt.y, v.y)};
+          }
+          // the row of the pair that did not overflow keeps its shift (its sums come out
+          // unchanged: scaled by 1, summed again in the same order)
+          mt = f2{ox ? mt.x : 0.f, oy ? mt.y : 0.f};
+          const f2 f = f2{fast_exp2(-mt.x), fast_exp2(-mt.y)}, l0 = tot[h][0];
 #pragma unroll
-        for (int k = 0; k <= NACC; ++k) {
-          f2 b = tot[h][k];
-          if (KS >= 0 && k == KS + 1) b = pk_fma(-mt, l0, b);
-          tot[h][k] = f2{f.x == 0.f ? 0.f : f.x * b.x, f.y == 0.f ? 0.f : f.y * b.y};
-          acc[h][k] = splat(0.f);
+          for (int k = 0; k <= NACC; ++k) {
+            f2 b = tot[h][k];
+            if (KS >= 0 && k == KS + 1) b = pk_fma(-mt, l0, b);
+            tot[h][k] = f2{f.x == 0.f ? 0.f : f.x * b.x, f.y == 0.f ? 0.f : f.y * b.y};
+            acc[h][k] = splat(0.f);
+          }
+          m[h] = m[h] + mt;
+          row[h].k = row[h].k - mt;
+          run(std::false_type{}, h, h + 1);
         }
-        m[h] = m[h] + mt;
-        row[h].k = row[h].k - mt;
-        if (uni) pass(std::true_type{}, h, h + 1);
-        else pass(std::false_type{}, h, h + 1);
       }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h)
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) tot[h][k] = tot[h][k] + acc[h][k];
-    }
-    __syncthreads();
+    // lse_adapt() tiles that needed a tile-end re-reference somewhere in the workgroup: the
+    // rest of the chunk tests per pair (events are then common: small sigma against the shift)
+    if (__syncthreads_or(reref) && ++reref_tiles >= adapt) pair_mode = true;
   }
 #pragma unroll
   for (int h = 0; h < H; ++h)
@@ -338,6 +441,16 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
 #pragma unroll
       for (int k = 0; k <= NACC; ++k) dst[1 + k] = c ? tot[h][k].y : tot[h][k].x;
     }
+}
+
+// Tiles with a tile-end re-reference (anywhere in the workgroup) before the rest of the chunk
+// tests per pair (0: per pair from the start); env DICP_LSE_ADAPT, option "lse_adapt"
+int& lse_adapt_ref() {
+  static int v = [] {
+    const char* e = getenv("DICP_LSE_ADAPT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 int& lse_pk_ref() {
@@ -480,6 +593,8 @@ struct OpGmmE {
   // (the Chui two-set trace's EM stop test at tol 1e-3 flips one EM step on rounding-level
   // changes -- profiles/r05_chui_uniform_flip.txt)
   static constexpr int kUni = STATS ? D + 1 : -1;
+  // per-row shift hint (dicp_gmm_estep_hint_f32): Args::r1, or NULL
+  __device__ static const float* hint(const Args& a) { return a.r1; }
   __device__ static float uni_value(const Args& a, const Scal& sc, int64_t j) {
     return fminf(a.c1[j] * sc.aux1, fminf(kLseDead * sc.aux1, 1e37f));
   }
@@ -579,6 +694,7 @@ struct OpGmmM {
   }
   static constexpr int kUni = -1;
   __device__ static float uni_value(const Args&, const Scal&, int64_t) { return 0.f; }
+  __device__ static const float* hint(const Args&) { return nullptr; }
   template <bool U = false>
   __device__ static void accum(const float* rec, float, float e, float* acc) {
 #pragma unroll
@@ -693,10 +809,10 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
   float* part = reinterpret_cast<float*>(ws);
   if (pk)
     lse_rowred_pk_kernel<Op, R / 2><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
-        a, sc, M, N, chunk, part);
+        a, sc, M, N, chunk, part, lse_adapt_ref());
   else
     lse_rowred_kernel<Op, R><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
-        a, sc, M, N, chunk, part);
+        a, sc, M, N, chunk, part, lse_adapt_ref());
   int rc = check_launch(name);
   if (rc) return rc;
   if (S > kWaveMergeMinSplits) {
@@ -711,9 +827,9 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
 
 template <int D>
 int estep_d(const float* X, int64_t N, const float* mu, const float* w2, const float* mu2,
-            int64_t C, double sigma, double lgn, float* T, float* T2, float* stats, void* ws,
-            size_t wsb, hipStream_t st) {
-  const Args a = {X, nullptr, nullptr, nullptr, mu, w2, mu2, nullptr};
+            int64_t C, double sigma, double lgn, const float* hint, float* T, float* T2,
+            float* stats, void* ws, size_t wsb, hipStream_t st) {
+  const Args a = {X, hint, nullptr, nullptr, mu, w2, mu2, nullptr};
   Scal sc = make_scal(sigma, 0.0);
   sc.aux0 = (float)lgn;
   sc.aux1 = 1.0f / sc.nc;
@@ -730,24 +846,33 @@ int estep_d(const float* X, int64_t N, const float* mu, const float* w2, const f
 
 namespace dicp {
 int& lse_pk() { return lse_pk_ref(); }
+int& lse_adapt() { return lse_adapt_ref(); }
 }  // namespace dicp
 
 // The Python wrapper precomputes the C-sized column vectors (w2, |mu|^2, lpi) with torch on
 // the device; the kernels here see only device pointers.
-extern "C" int dicp_gmm_estep_f32(const float* X, int64_t N, const float* mu, const float* w2,
-                                  const float* mu2, int64_t C, int D, double sigma, double lgn,
-                                  float* T, float* T2, float* stats, void* ws, size_t ws_bytes,
-                                  dicp_stream_t stream) {
+extern "C" int dicp_gmm_estep_hint_f32(const float* X, int64_t N, const float* mu, const float* w2,
+                                       const float* mu2, int64_t C, int D, double sigma, double lgn,
+                                       const float* hint, float* T, float* T2, float* stats, void* ws,
+                                       size_t ws_bytes, dicp_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (N < 0 || C <= 0 || (N > 0 && (!X || !T)) || !mu || !w2 || !mu2 || !(sigma > 0)) {
     set_error("dicp_gmm_estep_f32: invalid arguments");
     return DICP_ERR_INVALID;
   }
   switch (D) {
-    case 2: return estep_d<2>(X, N, mu, w2, mu2, C, sigma, lgn, T, T2, stats, ws, ws_bytes, st);
-    case 3: return estep_d<3>(X, N, mu, w2, mu2, C, sigma, lgn, T, T2, stats, ws, ws_bytes, st);
+    case 2: return estep_d<2>(X, N, mu, w2, mu2, C, sigma, lgn, hint, T, T2, stats, ws, ws_bytes, st);
+    case 3: return estep_d<3>(X, N, mu, w2, mu2, C, sigma, lgn, hint, T, T2, stats, ws, ws_bytes, st);
     default: set_error("gmm_estep: D=%d unsupported", D); return DICP_ERR_UNSUPPORTED;
   }
+}
+
+extern "C" int dicp_gmm_estep_f32(const float* X, int64_t N, const float* mu, const float* w2,
+                                  const float* mu2, int64_t C, int D, double sigma, double lgn,
+                                  float* T, float* T2, float* stats, void* ws, size_t ws_bytes,
+                                  dicp_stream_t stream) {
+  return dicp_gmm_estep_hint_f32(X, N, mu, w2, mu2, C, D, sigma, lgn, nullptr, T, T2, stats, ws,
+                                 ws_bytes, stream);
 }
 
 extern "C" int dicp_gmm_mstep_f32(const float* X, const float* T2, int64_t N, const float* mu,

@@ -209,6 +209,7 @@ int& red_alg();
 // pair-once centred sums when the rows are the columns (sym_cx.hpp): 0 off, 1 auto, 2 always
 int& sym_red();
 int& sym_red_rows();   // rows per lane of the pair-once sums: 0 auto, 4, 8
+int& lse_adapt();      // E / M passes: eventful tiles before the per-pair re-reference test
 int& lse_pk();         // E / M passes: 1 packed row pairs (v_pk_*), 0 scalar rows
 int& cx_rho_x100();
 // rows M, columns N; ext: the external-point forward (its non-centred kernel is the packed one)

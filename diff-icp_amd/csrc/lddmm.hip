@@ -230,6 +230,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     sym_red() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "lse_adapt")) {
+    if (value < 0) return DICP_ERR_INVALID;
+    lse_adapt() = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "lse_pk")) {
     if (value < 0 || value > 1) return DICP_ERR_INVALID;
     lse_pk() = value;
@@ -266,6 +271,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "cx_rho_x100")) { *value = cx_rho_x100(); return DICP_OK; }
   if (!strcmp(name, "sym_red")) { *value = sym_red(); return DICP_OK; }
   if (!strcmp(name, "lse_pk")) { *value = lse_pk(); return DICP_OK; }
+  if (!strcmp(name, "lse_adapt")) { *value = lse_adapt(); return DICP_OK; }
   if (!strcmp(name, "sym_red_rows")) { *value = sym_red_rows(); return DICP_OK; }
   if (!strcmp(name, "sym_fwd_rows")) { *value = sym_fwd_rows(); return DICP_OK; }
   if (!strcmp(name, "ext_alg")) { *value = g_ext_alg; return DICP_OK; }

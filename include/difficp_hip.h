@@ -289,6 +289,19 @@ int dicp_gmm_estep_f32(const float* X, int64_t N, const float* mu, const float* 
                        const float* mu2, int64_t C, int D, double sigma, double lgn, float* T,
                        float* T2, float* stats, void* ws, size_t ws_bytes, dicp_stream_t stream);
 
+/* The same E-step with an optional per-row shift hint (extension; NULL = dicp_gmm_estep_f32):
+ * shift_hint[n] ~ the row's log2-domain LSE, e.g. the T2 of the previous EM step over the same
+ * rows.  The single exp sweep shifts each row's terms by
+ *     m = clamp(shift_hint[n] - 8, m64, m64 + 100),  m64 = max of the chunk's first 64 logits
+ * instead of m64 alone, so a small sigma (nearest component far closer than any of a random
+ * 64-column sample) no longer forces a re-referenced tile per record; any hint is safe (the
+ * clamp), a good one makes re-referencing rare.  Results agree with the hint-less call to
+ * float32 rounding (the shift is a change of reference, not an approximation). */
+int dicp_gmm_estep_hint_f32(const float* X, int64_t N, const float* mu, const float* w2,
+                            const float* mu2, int64_t C, int D, double sigma, double lgn,
+                            const float* shift_hint, float* T, float* T2, float* stats, void* ws,
+                            size_t ws_bytes, dicp_stream_t stream);
+
 /* M-step column pass over components c (evaluated as a row pass, log domain, robust for
  * empty components like softmax(lgamma, dim=0)):
  *   colstats[c*(D+1) + ...] = { log sum_n gamma_nc          (= new w_c,  GMM.py:293),
@@ -398,6 +411,9 @@ int dicp_supports_dim(int D);
  *                  points alone on the chip, else 4), 4 or 8 forced
  *   "lse_pk"       GMM E / M passes: 1 rows packed in float2 pairs (v_pk_fma_f32, default),
  *                  0 scalar rows (bitwise equal)
+ *   "lse_adapt"    GMM E / M passes: tiles with a tile-end re-reference (anywhere in the
+ *                  workgroup) before the rest of the chunk tests per pair; 0 per pair from the
+ *                  start (default 1; env DICP_LSE_ADAPT)
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
  *   "mfma_rmax_x100"  matrix-core forward (fwd_alg 3): largest workgroup row spread (scaled
  *                  units x 100) that takes the MFMA branch; >= 100000 always, 0 never (default 300)

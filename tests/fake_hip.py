@@ -219,7 +219,7 @@ def ode_ext_bwd(x, q, p, gvx, gdiv, sigma, eta, gq, gp):
     return _out(ggx, x)
 
 
-def gmm_estep(X, mu, w2, mu2, sigma, lgn, want_stats):
+def gmm_estep(X, mu, w2, mu2, sigma, lgn, want_stats, hint=None):   # hint: a shift only (no effect)
     Xd, M, W2 = _d(X), _d(mu), _d(w2)
     D2 = ((Xd[:, None, :] - M[None, :, :]) ** 2).sum(-1)
     t2 = W2[None, :] - D2 * LOG2E / (2 * sigma ** 2)
