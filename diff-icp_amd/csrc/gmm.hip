@@ -54,6 +54,16 @@ constexpr int kWaveMergeMinSplits = 64;
 // 3.40-3.70 ms at every sigma.
 constexpr float kLseOverflow = 0x1p64f;
 constexpr float kLseSlack = 64.f;
+// With the hint: a workgroup where at least 1 / kLseClampedShare of the threads hold a row whose
+// hint was clamped (lse_hint_clamped) tests per pair from the start; the others count
+// kLseAdaptHinted eventful tiles before switching (a clamped row re-references in the few tiles
+// holding its nearest columns; a stale hint rarely at all).
+// Measured at 100k x 100k with the hint: tile-end 2.41 / 3.34 / 5.77 ms at sigma 0.05 / 0.02 /
+// 0.01, per pair 3.42 / 3.41 / 3.49 (profiles/r05_estep_adapt_count_rule.jsonl); this rule 2.40-2.45
+// / 3.46-3.49 / 3.46, the bench workload's E-step 3.30 ms (tile-end 3.05, per pair 3.46, counting
+// alone 3.66; profiles/r05_estep_adapt.jsonl).
+constexpr int kLseAdaptHinted = 4;
+constexpr int kLseClampedShare = 4;
 // columns of the chunk's first tile whose logits set the shift (the exact maximum over them):
 // 64 of the <= 256 staged -- a 1/28 logit overhead at the 100k two-set E-step's ~1800-column
 // chunks instead of 1/7; a row whose nearest components come later is re-referenced once
@@ -78,6 +88,11 @@ constexpr float kLseDead = -1e8f;
 __device__ __forceinline__ float lse_hinted_shift(float m64, float hint) {
   if (!(hint > -1e30f && hint < 1e30f)) return m64;
   return fminf(fmaxf(hint - 8.f, m64), m64 + 100.f);
+}
+// The hint sits beyond the clamp: the row's nearest columns are far closer than the sampled
+// ones, and re-reference events are to be expected in the chunk.
+__device__ __forceinline__ bool lse_hint_clamped(float m64, float hint) {
+  return hint > -1e30f && hint < 1e30f && hint - 8.f > m64 + 100.f;
 }
 
 template <class Op, int R>
@@ -121,12 +136,14 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   }
   // -inf (a dead row of the M-step: w2 = -inf): shift 0, its terms are all 0
   const float* hint = Op::hint(args);
+  bool clamped = false;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (m[r] == -__builtin_huge_valf()) m[r] = 0.f;
     if (hint != nullptr) {   // the row's expected LSE: m = clamp(hint - 8, m64, m64 + 100)
       int64_t i = ibase + (int64_t)r * kBlock;
       if (i >= M) i = M - 1;
+      clamped = clamped || lse_hint_clamped(m[r], hint[i]);
       m[r] = lse_hinted_shift(m[r], hint[i]);
     }
     row[r].k -= m[r];
@@ -139,6 +156,11 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
     for (int k = 0; k <= NACC; ++k) tot[r][k] = 0.f;
   bool pair_mode = adapt <= 0;
   int reref_tiles = 0;
+  if (hint != nullptr) {   // a hinted workgroup: per pair at once where many rows' hints were
+    // clamped (their nearest columns lie far above the sample); else count more eventful tiles
+    if (__syncthreads_count(clamped) * kLseClampedShare >= kBlock) pair_mode = true;
+    else if (adapt > 0 && adapt < kLseAdaptHinted) adapt = kLseAdaptHinted;
+  }
   bool first = true;   // the first tile is already in LDS
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
@@ -320,6 +342,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
     }
   }
   const float* hint = Op::hint(args);
+  bool clamped = false;
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     if (m[h].x == kNinf) m[h].x = 0.f;
@@ -328,6 +351,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
       int64_t i0 = ibase + (int64_t)(2 * h) * kBlock, i1 = ibase + (int64_t)(2 * h + 1) * kBlock;
       if (i0 >= M) i0 = M - 1;
       if (i1 >= M) i1 = M - 1;
+      clamped = clamped || lse_hint_clamped(m[h].x, hint[i0]) || lse_hint_clamped(m[h].y, hint[i1]);
       m[h] = f2{lse_hinted_shift(m[h].x, hint[i0]), lse_hinted_shift(m[h].y, hint[i1])};
     }
     row[h].k = row[h].k - m[h];
@@ -340,6 +364,11 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
     for (int k = 0; k <= NACC; ++k) tot[h][k] = splat(0.f);
   bool pair_mode = adapt <= 0;
   int reref_tiles = 0;
+  if (hint != nullptr) {   // a hinted workgroup: per pair at once where many rows' hints were
+    // clamped (their nearest columns lie far above the sample); else count more eventful tiles
+    if (__syncthreads_count(clamped) * kLseClampedShare >= kBlock) pair_mode = true;
+    else if (adapt > 0 && adapt < kLseAdaptHinted) adapt = kLseAdaptHinted;
+  }
   bool first = true;
   for (int64_t jt = j0; jt < j1; jt += kTile) {
     const int cnt = (int)((j1 - jt) < kTile ? (j1 - jt) : kTile);
