@@ -95,6 +95,41 @@ __device__ __forceinline__ bool lse_hint_clamped(float m64, float hint) {
   return hint > -1e30f && hint < 1e30f && hint - 8.f > m64 + 100.f;
 }
 
+// Store a chunk partial {m, l, acc}.  The merge weighs a partial by 2^(m_s - max m): with the
+// shift up to 100 above a chunk's largest term (a clamped hint) and the sums up to 2^77 (terms
+// below the re-reference slack), that factor could underflow while the partial's share did not
+// (a stale-high hint lost up to 90% of a row's mass: test_estep_reref_modes).  So a partial
+// whose sum lies outside [2^-24, 2^24] is stored normalised to l in [0.5, 1): m + e for
+// l = f 2^e, the sums scaled by 2^-e (exact), the shifted slot re-referenced to m + e; the
+// others as they are (their m is within 24 of their own log-sum).  An empty partial (l = 0,
+// or NaN) stores the shift -inf and is skipped.
+template <int NACC, int KS>
+__device__ __forceinline__ void lse_store_part(float* dst, float m, const float* tot) {
+  const float l = tot[0];
+  if (!(l > 0.f)) {
+    dst[0] = -__builtin_huge_valf();
+#pragma unroll
+    for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[k];
+    return;
+  }
+  if (l >= 0x1p-24f && l <= 0x1p24f) {
+    dst[0] = m;
+#pragma unroll
+    for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[k];
+    return;
+  }
+  int e;
+  (void)frexpf(l, &e);
+  const float fe = (float)e;
+  dst[0] = m + fe;
+#pragma unroll
+  for (int k = 0; k <= NACC; ++k) {
+    float v = tot[k];
+    if (KS >= 0 && k == KS + 1) v = fmaf(-fe, l, v);   // sum e (t - m) -> sum e (t - (m + e))
+    dst[1 + k] = ldexpf(v, -e);
+  }
+}
+
 template <class Op, int R>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
                                                             int64_t M, int64_t N, int64_t chunk,
@@ -257,10 +292,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
   for (int r = 0; r < R; ++r) {
     const int64_t i = ibase + (int64_t)r * kBlock;
     if (i >= M) continue;
-    float* dst = part + ((int64_t)blockIdx.y * M + i) * W;
-    dst[0] = tot[r][0] > 0.f ? m[r] : -__builtin_huge_valf();   // an empty partial: skipped
-#pragma unroll
-    for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[r][k];
+    lse_store_part<NACC, KS>(part + ((int64_t)blockIdx.y * M + i) * W, m[r], tot[r]);
   }
 }
 
@@ -464,11 +496,10 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
     for (int c = 0; c < 2; ++c) {
       const int64_t i = ibase + (int64_t)(2 * h + c) * kBlock;
       if (i >= M) continue;
-      float* dst = part + ((int64_t)blockIdx.y * M + i) * W;
-      const float l = c ? tot[h][0].y : tot[h][0].x;
-      dst[0] = l > 0.f ? (c ? m[h].y : m[h].x) : kNinf;
+      float t[NACC + 1];
 #pragma unroll
-      for (int k = 0; k <= NACC; ++k) dst[1 + k] = c ? tot[h][k].y : tot[h][k].x;
+      for (int k = 0; k <= NACC; ++k) t[k] = c ? tot[h][k].y : tot[h][k].x;
+      lse_store_part<NACC, KS>(part + ((int64_t)blockIdx.y * M + i) * W, c ? m[h].y : m[h].x, t);
     }
 }
 

@@ -1,12 +1,15 @@
 """EM passes on inputs that exercise the single-sweep LSE's re-referencing (csrc/gmm.hip
-lse_rowred_kernel): the shift of a column chunk is the maximum of its FIRST tile (256
-columns), so rows whose nearby columns all come later must re-reference their sums.
+lse_rowred_kernel): the shift of a column chunk is the maximum over its first 64 columns, so
+rows whose nearby columns come later re-reference their sums (tile-end or per pair,
+csrc/gmm.hip kLseSlack; both modes forced in test_estep_reref_modes).
 
-  * E-step (rows = points, columns = components): the first 256 components sit far from the
+  * E-step (rows = points, columns = components): the first components sit far from the
     points of one cluster (~2^-1000 of the near ones);
   * M-step (rows = components, columns = points): the first points are far from the
     components of the other cluster;
-  * the wave-per-row merge of many column chunks (the M-step at the atlas shape).
+  * the wave-per-row merge of many column chunks (the M-step at the atlas shape);
+  * small sigma against the sample's spacing (events in most tiles), with and without the
+    shift hint (exact, and 300 too high: the chunk partials' normalised store).
 
 Criterion: err vs the float64 oracle (oracle/torch_ref.py em_step, pinned by the
 reference's EM goldens) <= max(2e-5, 2 x the float32 oracle's own deviation)."""
@@ -77,9 +80,9 @@ def _estep64(X, mu, lpi, sigma):
 @pytest.mark.parametrize("case", ["plain", "dead", "far_first", "chunks", "uniform"])
 def test_estep_stats_match_fp64(dev, D, case):
     """Every output of dicp_gmm_estep_f32 (T, T2 and the D+4 stats, include/difficp_hip.h)
-    against float64 rows: random weights; dead components (w = -inf, the first 300 of them: a
-    dead-only shift tile, kLseDead); a far cluster in the first columns (the tile-end
-    re-reference); many column chunks (the wave-per-row merge)."""
+    against float64 rows: random weights; dead components (w = -inf, 350 of them, kLseDead);
+    a far cluster in the first columns; many column chunks (the wave-per-row merge; sigma small
+    against the shift sample's spacing: re-references)."""
     from difficp_amd import _lib
     g = torch.Generator().manual_seed(11 * D + len(case))
     N, C, sigma = {"plain": (3000, 700, 0.1), "dead": (3000, 900, 0.1), "far_first": (2500, 800, 0.05),
@@ -140,3 +143,37 @@ def test_lse_packed_rows_bitwise(dev, case):
         _lib.set_option("lse_pk", old)
     for a, b in zip(out[0], out[1]):
         assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(b, nan=7.0))
+
+
+@pytest.mark.parametrize("adapt", [0, 1, 1000])
+@pytest.mark.parametrize("hinted", [False, True])
+def test_estep_reref_modes(dev, adapt, hinted):
+    """The E-step at sigma 0.01 over 40k random components (the 64-column shift sample sits
+    hundreds of log2 units below most rows' nearest component): per-pair re-referencing from the
+    start (lse_adapt 0), the adaptive default (1), tile-end only (1000); with and without the
+    shift hint (the float64 T2, and the hint shifted up by 300: clamped) -- every output against
+    float64 rows."""
+    from difficp_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    N, C, D, sigma = 1500, 40000, 3, 0.01
+    X = torch.rand(N, D, generator=g, dtype=torch.float64).float().double()
+    mu = torch.rand(C, D, generator=g, dtype=torch.float64).float().double()
+    w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    lpi = w - w.logsumexp(0)
+    T64, T264, st64, lgn = _estep64(X, mu, lpi, sigma)
+    f = lambda t: t.float().to(dev).contiguous()
+    old = _lib.get_option("lse_adapt")
+    try:
+        _lib.set_option("lse_adapt", adapt)
+        hints = [None] if not hinted else [f(T264), f(T264 + 300.0)]
+        for hint in hints:
+            T, T2, st = _lib.gmm_estep(f(X), f(mu), f(lpi / math.log(2)), f((mu * mu).sum(-1)), sigma,
+                                       lgn, True, hint=hint)
+            T, T2, st = T.cpu().double(), T2.cpu().double(), st.cpu().double()
+            assert rel_err(T, T64) < 1e-5 and rel_err(T2, T264) < 1e-5
+            for k in range(D + 4):
+                assert torch.isfinite(st[:, k]).all(), k
+                assert rel_err(st[:, k], st64[:, k]) < (2e-5 if k >= D else 1e-5), (k, rel_err(st[:, k], st64[:, k]))
+    finally:
+        _lib.set_option("lse_adapt", old)
+
