@@ -404,7 +404,11 @@ _WS_BYTES = {}   # (kind, M, N, D) -> dicp_workspace_bytes; cleared by set_optio
 # call that may run inside a launch batch (a batch open on this thread, or a frame thread of
 # the lockstep batches, whose calls from several frames share one stream and run together:
 # each needs its own -- tests/test_gpu_batch.py caught the shared one), nor inside a graph
-# capture; a few recent streams only (concurrent frames open a stream per Reg_opt call).
+# capture; a few recent streams only (concurrent frames open a stream per Reg_opt call).  The
+# cache is keyed by host thread too (ctypes releases the GIL, so two threads issuing calls on
+# one stream could otherwise interleave the kernels of two multi-kernel calls on one buffer).
+# A cached workspace is valid within ONE library call only: a workspace that must survive
+# between calls (euler_step_phase_ws) is requested with exclusive=True and bypasses the cache.
 _WS_CACHE = OrderedDict()
 _WS_CACHE_MAX = 8
 _ws_lock = threading.Lock()
@@ -419,7 +423,7 @@ def _poison(ws):
     return ws
 
 
-def _workspace(kind: int, M: int, N: int, D: int, device):
+def _workspace(kind: int, M: int, N: int, D: int, device, exclusive: bool = False):
     key = (kind, int(M), int(N), int(D))
     nbytes = _WS_BYTES.get(key)
     if nbytes is None:
@@ -436,11 +440,12 @@ def _workspace(kind: int, M: int, N: int, D: int, device):
         # into one batch together with other frames' calls on the batcher's shared stream --
         # each call needs a workspace of its own (the call's closure keeps it alive)
         return _poison(torch.empty(nbytes, dtype=torch.uint8, device=device)), nbytes
-    if torch.cuda.is_current_stream_capturing():
+    if exclusive or torch.cuda.is_current_stream_capturing():
         # a HIP-graph capture (core/shooting.py): the workspace must come from the graph's own
-        # pool, never a cached tensor that could be freed while the graph still points at it
+        # pool, never a cached tensor that could be freed while the graph still points at it;
+        # exclusive: the caller keeps it across several library calls
         return _poison(torch.empty(nbytes, dtype=torch.uint8, device=device)), nbytes
-    ck = (_stream(device), device.index)
+    ck = (_stream(device), device.index, threading.get_ident())
     with _ws_lock:
         ws = _WS_CACHE.get(ck)
         if ws is not None:
@@ -899,8 +904,9 @@ def euler_step_rows(q, p, row0: int, nrows: int, sigma: float, eta: float, dt: f
 
 def euler_step_phase_ws(nrows: int, M: int, D: int, device):
     """A workspace for the two calls of euler_step_phase (the partial slots of phase 0 must
-    survive until phase 1 has merged them)."""
-    return _workspace(WS_ODE_SELF_FWD_PHASED, nrows, M, D, device)[0]
+    survive until phase 1 has merged them, whatever runs on the stream in between: a fresh
+    buffer, never the per-stream cache)."""
+    return _workspace(WS_ODE_SELF_FWD_PHASED, nrows, M, D, device, exclusive=True)[0]
 
 
 def euler_step_phase(phase: int, q_loc, p_loc, q, p, row0: int, nrows: int, sigma: float, eta: float,

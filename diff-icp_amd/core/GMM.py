@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import copy
 import math
+import weakref
 
 import numpy as np
 import torch
@@ -174,6 +175,11 @@ class GaussianMixtureUnif(torch.nn.Module):
             s += "    eta0 [outlier vs GMM log-ratio]:" + str(self.outliers["eta0"]) + "\n"
         return s
 
+    def __getstate__(self):
+        d = self.__dict__.copy()
+        d.pop("_estep_hint", None)   # a weak reference to a point set: not state
+        return d
+
     def __setstate__(self, state):
         self.__dict__.update(state)
         self.spec = defspec
@@ -216,10 +222,15 @@ class GaussianMixtureUnif(torch.nn.Module):
         # the previous E-step's T2 over the same rows shifts the single exp sweep (a change of
         # reference: dicp_gmm_estep_hint_f32 -- without it a small sigma re-references most rows'
         # tiles; any hint is safe, a stale one only costs re-referencing)
+        # The hint is taken only from an earlier E-step over the SAME X tensor, unmodified
+        # (weak reference + version counter): the steps of one EM_optimization loop.  An E-step
+        # result then depends on its inputs and the loop's own history only, never on EM calls
+        # made earlier on other point sets of the same size.
         prev = getattr(self, "_estep_hint", None)
-        hint = prev[2] if (prev is not None and prev[0] == N and prev[1] == X.device) else None
+        hint = (prev[2] if (prev is not None and prev[0]() is X and prev[1] == X._version)
+                else None)
         T, T2, stats = _lib.gmm_estep(X, mu_old, w2_old, mu2_old, sigma_old, lgn_old, True, hint=hint)
-        self._estep_hint = (N, X.device, T2)
+        self._estep_hint = (weakref.ref(X), X._version, T2)
         E_row = stats[:, D + 1]                   # sum_c gamma lgamma
 
         if self.outliers is not None:

@@ -43,7 +43,9 @@ class Shoot(list):
     # The state views are formed when read: a closure reads shoot[-1] (and trajloss shoot[0]),
     # and forming all 3 (nt+1) views of every shooting was ~1500 tensor selects per diff-ICP
     # iteration, ~8% of the host floor at 2k points (tools/host_floor.py).  Indexing by an int
-    # forms (and keeps) that state only; any other list operation fills the list first.
+    # forms (and keeps) that state only.  Any other list operation first fills the list's own
+    # storage with every state; from then on (`_full`) the storage is authoritative, so list
+    # mutators, concatenation and comparisons behave as on a plain list.
     def __init__(self, Q, P, C, X=None, H0=None):
         super().__init__()
         self.Q, self.P, self.C, self.X = Q, P, C, X
@@ -66,57 +68,62 @@ class Shoot(list):
 
     def _fill(self):
         if not self._full:
+            items = [self._state(t) for t in range(self._n)]
+            super().clear()
+            super().extend(items)
             self._full = True
-            super().extend([self._state(t) for t in range(self._n)])
 
     def __getitem__(self, k):
+        if self._full:
+            return super().__getitem__(k)
         if isinstance(k, int):
             return self._state(k)
         self._fill()
         return super().__getitem__(k)
 
     def __len__(self):
-        return self._n
+        return super().__len__() if self._full else self._n
 
     def __iter__(self):
+        if self._full:
+            return super().__iter__()
         return (self._state(t) for t in range(self._n))
 
     def __reversed__(self):
+        if self._full:
+            return super().__reversed__()
         return (self._state(t) for t in reversed(range(self._n)))
 
     def __bool__(self):
-        return self._n > 0
-
-    def __contains__(self, v):
-        self._fill()
-        return super().__contains__(v)
-
-    def __eq__(self, other):
-        self._fill()
-        return super().__eq__(other)
+        return len(self) > 0
 
     __hash__ = None
 
-    def __repr__(self):
-        self._fill()
-        return super().__repr__()
-
-    def __setitem__(self, k, v):
-        self._fill()
-        super().__setitem__(k, v)
-        if isinstance(k, int):
-            self._states[k % self._n] = v
+    def __radd__(self, other):
+        # other + shoot: list.__add__ would read this object's (possibly unfilled) storage
+        return list(other) + list(self)
 
     def copy(self):
         return list(self)
 
-    def index(self, *a):
-        self._fill()
-        return super().index(*a)
+    def __reduce__(self):
+        """Pickle / deepcopy: the stacked tensors and attributes, plus the states themselves
+        once the list was filled (it may have been mutated since)."""
+        state = {k: v for k, v in self.__dict__.items() if k != "_states"}
+        if self._full:
+            state["_items"] = list(super().__iter__())
+        return (Shoot, (self.Q, self.P, self.C, self.X, self.H0), state)
 
-    def count(self, v):
-        self._fill()
-        return super().count(v)
+    def __setstate__(self, state):
+        items = state.pop("_items", None)
+        self.__dict__.update(state)
+        self._states = {}
+        super().clear()
+        if items is not None:
+            super().extend(items)
+            self._full = True
+        else:
+            self._full = False
 
     def detach(self):
         d = lambda t: None if t is None else t.detach()
@@ -125,6 +132,30 @@ class Shoot(list):
             if hasattr(self, k):
                 setattr(sh, k, getattr(self, k))
         return sh
+
+
+def _fill_first(name):
+    """list method `name` on a Shoot, after its storage is filled with every state."""
+    base = getattr(list, name)
+
+    def f(self, *a, **k):
+        self._fill()
+        for o in a:   # list's C methods read another Shoot's storage directly
+            if isinstance(o, Shoot):
+                o._fill()
+        return base(self, *a, **k)
+
+    f.__name__ = name
+    f.__doc__ = base.__doc__
+    return f
+
+
+for _m in ("append", "extend", "insert", "pop", "remove", "sort", "reverse", "clear", "index",
+           "count", "__setitem__", "__delitem__", "__iadd__", "__imul__", "__add__", "__mul__",
+           "__rmul__", "__contains__", "__eq__", "__ne__", "__lt__", "__le__", "__gt__", "__ge__",
+           "__repr__"):
+    setattr(Shoot, _m, _fill_first(_m))
+del _m
 
 
 class LDDMMModel:

@@ -1032,9 +1032,18 @@ def shoot_loss_grad(LM, dataloss, q0, p0):
         H0r = H0.detach().requires_grad_(True)
         C1 = C.detach().requires_grad_(True)
         L = LM.lam * H0r + C1[nt] + dataloss(q1)
-        gq1, gH, gC = torch.autograd.grad(L, (q1, H0r, C1), torch.ones_like(L))
+        # backward() rather than autograd.grad: the gradient also accumulates into any other
+        # leaf the data loss reads (as the reference's L.backward(), optim.py:46, would), and a
+        # data loss that does not depend on q1 (a frame without data points) gives no gq1
+        L.backward(torch.ones_like(L))
+    gq1, gH, gC = q1.grad, H0r.grad, C1.grad
     gQ = torch.zeros_like(Q)
-    gQ[nt].copy_(gq1)
+    if gq1 is not None:
+        gQ[nt].copy_(gq1)
+    if gH is None:
+        gH = torch.zeros_like(H0)
+    if gC is None:
+        gC = torch.zeros_like(C)
     with _lib.coord_mode(raw), _lib.thread_option(ctx.share, "batch_share"):
         grads = ShootFn._backward(ctx, gQ, None, gC, gH)
     return L.detach(), grads[1], sh

@@ -101,12 +101,19 @@ __device__ __forceinline__ bool lse_hint_clamped(float m64, float hint) {
 // (a stale-high hint lost up to 90% of a row's mass: test_estep_reref_modes).  So a partial
 // whose sum lies outside [2^-24, 2^24] is stored normalised to l in [0.5, 1): m + e for
 // l = f 2^e, the sums scaled by 2^-e (exact), the shifted slot re-referenced to m + e; the
-// others as they are (their m is within 24 of their own log-sum).  An empty partial (l = 0,
-// or NaN) stores the shift -inf and is skipped.
+// others as they are (their m is within 24 of their own log-sum).  An empty partial (l = 0)
+// stores the shift -inf and is skipped; a NaN one (NaN rows) stores the shift NaN, which both
+// merges turn into NaN sums (fmaxf skips it for the maximum, exp2(NaN - max) is NaN).
 template <int NACC, int KS>
 __device__ __forceinline__ void lse_store_part(float* dst, float m, const float* tot) {
   const float l = tot[0];
-  if (!(l > 0.f)) {
+  if (l != l) {   // NaN inputs (x or mu): a NaN shift, so the merge carries NaN on to T and T2
+    dst[0] = __builtin_nanf("");
+#pragma unroll
+    for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[k];
+    return;
+  }
+  if (l == 0.f) {
     dst[0] = -__builtin_huge_valf();
 #pragma unroll
     for (int k = 0; k <= NACC; ++k) dst[1 + k] = tot[k];

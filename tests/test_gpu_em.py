@@ -177,3 +177,60 @@ def test_estep_reref_modes(dev, adapt, hinted):
     finally:
         _lib.set_option("lse_adapt", old)
 
+
+
+def test_em_hint_history_independent(dev):
+    """the E-step's shift hint comes only from the same (unmodified) point set, so
+    an EM run gives bitwise the same result and step count whether or not the model ran EM
+    on another point set of the same size before."""
+    import copy
+    from difficp_amd.core.GMM import GaussianMixtureUnif
+    X, mu0 = _two_clusters(20000, 256, 1.0, dev, seed=3)
+    Xo, _ = _two_clusters(20000, 256, 1.0, dev, seed=4)
+    GM = GaussianMixtureUnif(mu0, sigma=0.02, spec={"device": dev, "dtype": torch.float32})
+    GM.to_optimize = dict(OPT)
+    G1, G2 = copy.deepcopy(GM), copy.deepcopy(GM)
+    G2.EM_step(Xo)                     # history: an E-step over another set of the same N
+    G2.mu, G2.sigma, G2.w = G1.mu.clone(), G1.sigma, G1.w.clone()
+    r1 = G1.EM_optimization(X, max_iterations=6, tol=1e-9)
+    r2 = G2.EM_optimization(X, max_iterations=6, tol=1e-9)
+    assert torch.equal(G1.mu, G2.mu) and G1.sigma == G2.sigma and torch.equal(G1.w, G2.w)
+    for a, b in zip(r1, r2):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b)
+        else:
+            assert a == b
+    # within one EM loop the hint is used (same X object, unmodified)
+    assert G1._estep_hint[0]() is X
+
+
+@pytest.mark.parametrize("where", ["x", "mu"])
+def test_estep_nan_propagates(dev, where):
+    """a NaN point (or component) comes out as NaN in T / T2 (not as an empty row
+    with T = -inf), the way the reference's torch EM propagates it; the other rows' T are those
+    of the same call without the NaN (row-wise independent)."""
+    from difficp_amd import _lib
+    g = torch.Generator().manual_seed(9)
+    N, C, D, sigma = 3000, 700, 3, 0.05
+    X = torch.rand(N, D, generator=g)
+    mu = torch.rand(C, D, generator=g)
+    lpi = torch.full((C,), -math.log(C))
+    f = lambda t: t.to(dev).contiguous()
+    Xn, mun = X.clone(), mu.clone()
+    if where == "x":
+        Xn[17, 1] = float("nan")
+    else:
+        mun[300, 0] = float("nan")
+    outs = []
+    for XX, mm in ((X, mu), (Xn, mun)):
+        T, T2, st = _lib.gmm_estep(f(XX), f(mm), f(lpi / math.log(2)), f((mm * mm).sum(-1)), sigma, 0.0, True)
+        outs.append((T.cpu(), T2.cpu(), st.cpu()))
+    (T, T2, st), (Tn, T2n, stn) = outs
+    if where == "x":
+        assert torch.isnan(Tn[17]) and torch.isnan(T2n[17]), (Tn[17], T2n[17])
+        keep = torch.arange(N) != 17
+        assert torch.isfinite(Tn[keep]).all()
+        assert rel_err(Tn[keep], T[keep]) < 1e-6
+    else:
+        # every row's LSE reads the NaN component
+        assert torch.isnan(Tn).all() and torch.isnan(T2n).all()

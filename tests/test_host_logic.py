@@ -505,6 +505,19 @@ def test_shoot_loss_grad_bitwise_autograd(fake, version):
     L2, g2, sh2 = shoot_loss_grad(LM, dataloss, q0, p0.clone())
     assert torch.equal(L.detach(), L2) and torch.equal(p.grad, g2)
     assert torch.equal(sh.Q.detach(), sh2.Q) and sh2.p1_missing
+    # a data loss that does not read q1 (a frame without data points) and one that
+    # also reads another leaf: the gradient of trajloss alone, and .grad accumulated into it
+    for const in (True, False):
+        w = torch.tensor(2.0, requires_grad=True)
+        dl = (lambda q: w * 3.0) if const else (lambda q: w * dataloss(q))
+        p = p0.clone().requires_grad_(True)
+        sh = LM.Shoot(q0, p, need_p1=False)
+        L = LM.trajloss(sh) + dl(sh[-1][0])
+        L.backward()
+        wg = w.grad.clone()
+        w.grad = None
+        L3, g3, _ = shoot_loss_grad(LM, dl, q0, p0.clone())
+        assert torch.equal(L.detach(), L3) and torch.equal(p.grad, g3) and torch.equal(w.grad, wg)
     # Optimize with the same-thread closure (what a frame under a LaunchBatcher runs)
     res = {}
     for mode in ("autograd", "manual"):
@@ -615,3 +628,51 @@ def test_psr_std_support_fp32_oracle_deviation(fake):
     print("FP32DEV", worst)
     for k, v in worst.items():
         assert v <= C.FP32_DEV[k], (k, v)
+
+
+def test_shoot_list_semantics_and_pickle():
+    """the lazily formed Shoot behaves as a plain list of its states under every
+    list operation, slicing and pickling (PSR objects holding a shoot are pickled)."""
+    import copy
+    import pickle
+    from difficp_amd.core.LDDMM import Shoot
+    n, M = 4, 5
+    Q = torch.arange(n * M * 2, dtype=torch.float32).reshape(n, M, 2)
+    P, C = -Q, torch.arange(n, dtype=torch.float32).reshape(n, 1)
+
+    def plain(sh):
+        return [tuple(t.clone() for t in s) for s in sh]
+
+    def same(a, b):
+        return len(a) == len(b) and all(all(torch.equal(x, y) for x, y in zip(s, t)) for s, t in zip(a, b))
+
+    ref = plain(Shoot(Q, P, C))
+    for op in ("slice", "pickle", "deepcopy", "add", "radd", "append", "pop", "repr"):
+        sh = Shoot(Q, P, C)
+        if op == "slice":
+            assert same(sh[1:3], ref[1:3]) and same(sh[:], ref) and len(sh) == n
+        elif op in ("pickle", "deepcopy"):
+            for fill in (False, True):
+                sh = Shoot(Q, P, C)
+                if fill:
+                    sh[:]
+                    sh.append(sh[0])
+                r = pickle.loads(pickle.dumps(sh)) if op == "pickle" else copy.deepcopy(sh)
+                want = ref + ref[:1] if fill else ref
+                assert isinstance(r, Shoot) and len(r) == len(want) and same(r[:], want) and same(list(r), want)
+                assert torch.equal(r[-1][0], want[-1][0])
+        elif op == "add":
+            assert same(sh + [ref[0]], ref + [ref[0]])
+        elif op == "radd":
+            assert same([ref[0]] + sh, [ref[0]] + ref)
+        elif op == "append":
+            sh.append(ref[0])
+            assert len(sh) == n + 1 and same(sh[:], ref + [ref[0]]) and same(list(sh), ref + [ref[0]])
+            assert torch.equal(sh[-1][0], ref[0][0])
+        elif op == "pop":
+            last = sh.pop()
+            assert torch.equal(last[0], ref[-1][0]) and len(sh) == n - 1 and same(list(sh), ref[:-1])
+        elif op == "repr":
+            assert repr(sh) == repr(Shoot(Q, P, C)[:])
+    a, b = Shoot(Q, P, C), Shoot(Q, P, C)
+    assert len(list(a) + list(b)) == 2 * n and len(a + b) == 2 * n
