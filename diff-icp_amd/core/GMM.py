@@ -20,6 +20,7 @@ all_gather and combined in rank order, so every rank holds bit-identical paramet
 from __future__ import annotations
 
 import copy
+import os
 import math
 import weakref
 
@@ -31,6 +32,9 @@ from .. import _lib
 from ..tools.point_sets import intrinsic_scale
 from ..tools import runstats
 from ..tools.spec import defspec
+
+# A/B switch (tools/probes/rowsplit_fe.py): DICP_ESTEP_HINT_ANY=1 restores the round-5 hint rule
+_HINT_ANY = os.environ.get("DICP_ESTEP_HINT_ANY", "0") != "0"
 
 _LOG2E = 1.4426950408889634
 
@@ -206,6 +210,7 @@ class GaussianMixtureUnif(torch.nn.Module):
     # ------------------------------------------------------------------------------------
     def EM_step_hip(self, X, skip_M=False):
         """One E + M step (GMM.py:236-325).  Returns (Y (N,D), Cfe, FE) like EM_step_torch."""
+        X_in = X           # the caller's tensor object: the E-step hint's key (below)
         X = X.detach().contiguous()
         N, D = X.shape
         comm = self.comm
@@ -222,15 +227,18 @@ class GaussianMixtureUnif(torch.nn.Module):
         # the previous E-step's T2 over the same rows shifts the single exp sweep (a change of
         # reference: dicp_gmm_estep_hint_f32 -- without it a small sigma re-references most rows'
         # tiles; any hint is safe, a stale one only costs re-referencing)
-        # The hint is taken only from an earlier E-step over the SAME X tensor, unmodified
-        # (weak reference + version counter): the steps of one EM_optimization loop.  An E-step
+        # The hint is taken only from an earlier E-step over the SAME X tensor object, unmodified
+        # (weak reference to the caller's tensor + version counter): the steps of one
+        # EM_optimization loop.  An E-step
         # result then depends on its inputs and the loop's own history only, never on EM calls
         # made earlier on other point sets of the same size.
         prev = getattr(self, "_estep_hint", None)
-        hint = (prev[2] if (prev is not None and prev[0]() is X and prev[1] == X._version)
+        hint = (prev[2] if (prev is not None and prev[0]() is X_in and prev[1] == X_in._version)
                 else None)
+        if _HINT_ANY and hint is None and prev is not None and prev[2].shape[0] == N:
+            hint = prev[2]      # A/B only: the round-5 rule (any earlier E-step of the same size)
         T, T2, stats = _lib.gmm_estep(X, mu_old, w2_old, mu2_old, sigma_old, lgn_old, True, hint=hint)
-        self._estep_hint = (weakref.ref(X), X._version, T2)
+        self._estep_hint = (weakref.ref(X_in), X_in._version, T2)
         E_row = stats[:, D + 1]                   # sum_c gamma lgamma
 
         if self.outliers is not None:

@@ -322,18 +322,45 @@ __global__ __launch_bounds__(kBlock) void merge_slabs_kernel(MergeSet m, Outs o,
   merge_slabs_body<MIN>(m, o, S, blockIdx.x, blockIdx.y);
 }
 
+// Slabs of double partials (the eta != 0 forward's, packed.hpp rowred_pk_body_f64): summed in
+// double in slab order, the epilogue formed in double, rounded once.
+__device__ __forceinline__ void merge_slabs_f64_body(const MergeSet& m, const Outs& o, int S, unsigned bx, unsigned by) {
+  const int j = by;
+  const int64_t n = m.n[j];
+  const int64_t e = (int64_t)bx * kBlock + threadIdx.x;
+  if (e >= n) return;
+  const double* __restrict__ slab = reinterpret_cast<const double*>(m.slab[j]);
+  double a = slab[e];
+  for (int s = 1; s < S; ++s) a += slab[(int64_t)s * n + e];
+  const int k = m.k[j];
+  double v = (double)o.alpha[k] * a;
+  if (o.base[k]) v += (double)o.base[k][e];
+  if (o.add[k]) v += (double)o.add[k][e];
+  if (o.accumulate[k]) v += (double)o.ptr[k][e];
+  o.ptr[k][e] = (float)v;
+}
+
+template <int I = 0>   // a template: defined in a header included by several objects
+__global__ __launch_bounds__(kBlock) void merge_slabs_f64_kernel(MergeSet m, Outs o, int S) {
+  merge_slabs_f64_body(m, o, S, blockIdx.x, blockIdx.y);
+}
+
 // batched form (batch.hpp): blockIdx.z = the recorded call
 struct MergeEntry {
   MergeSet m;
   Outs o;
   int S;
   unsigned gx, gy;
+  int f64;   // double slabs (merge_slabs_f64_body)
 };
 template <bool MIN>
 __global__ __launch_bounds__(kBlock) void merge_slabs_batch_kernel(BatchTab<MergeEntry> t) {
   const MergeEntry& e = t.e[blockIdx.z];
   if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
-  merge_slabs_body<MIN>(e.m, e.o, e.S, blockIdx.x, blockIdx.y);
+  if (e.f64)
+    merge_slabs_f64_body(e.m, e.o, e.S, blockIdx.x, blockIdx.y);
+  else
+    merge_slabs_body<MIN>(e.m, e.o, e.S, blockIdx.x, blockIdx.y);
 }
 inline int merge_slabs_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
   return batch_launch<MergeEntry>(merge_slabs_batch_kernel<false>, es, st, "merge_slabs");

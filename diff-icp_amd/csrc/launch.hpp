@@ -223,7 +223,14 @@ int cx_ext_fwd(const float* x, int64_t N, const float* q, const float* p, int64_
 size_t cx_red_ws(int64_t M, int64_t N, int D);
 size_t cx_ext_ws(int64_t N, int64_t M, int D);
 
+// sigma and eta of the calling thread's latest make_scal, in double: the launch constants the
+// eta != 0 forward forms in double on the host (packed.hpp eta_consts) read them
+inline thread_local double tl_launch_sigma = 1.0;
+inline thread_local double tl_launch_eta = 0.0;
+
 inline Scal make_scal(double sigma, double eta) {
+  tl_launch_sigma = sigma;
+  tl_launch_eta = eta;
   Scal sc;
   const double s = 1.0 / (sigma * sigma);
   sc.nc = (float)(-1.4426950408889634 * 0.5 * s);

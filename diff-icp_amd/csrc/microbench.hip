@@ -269,7 +269,21 @@ __global__ __launch_bounds__(64) void dpp_probe(int* out) {
   out[l] = __builtin_amdgcn_update_dpp(-1, l, CTRL, 0xF, 0xF, false);
 }
 
+__global__ __launch_bounds__(256) void exp2_eval(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = __builtin_amdgcn_exp2f(x[i]);
+}
+
 }  // namespace
+
+// y[i] = v_exp_f32(x[i]) (the pair kernels' fast_exp2), for accuracy probes
+// (tools/probes/exp2_bias.py)
+extern "C" int dicp_mb_exp2_eval(const float* x, float* y, int64_t n, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  exp2_eval<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(x, y, n);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 // Lane map of a wave-wide DPP rotate: out[l] = source lane read by lane l
 // (which = 0: wave_rol:1 (0x134), 1: wave_ror:1 (0x13C)); one wave64.

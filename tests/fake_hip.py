@@ -4,6 +4,7 @@ host-side logic (shooting adjoint, EM bookkeeping, PSR driver, sharded gloo path
 tested on CPU.  Never used by the product: difficp_amd raises without the HIP library.
 """
 import math
+import os
 
 import torch
 
@@ -13,8 +14,15 @@ LOG2E = 1.4426950408889634
 LN2 = math.log(2.0)
 
 
+# FAKE_HIP_DTYPE: the arithmetic of the oracle-backed entry points.  float64 (default): an
+# executable spec whose only float32 roundings are the outputs'; "float32": the reference's
+# own torch path run in float32 (SURVEY 8(c)'s "oracle32"), for the float32 drift that the
+# GPU parity tolerances of L-BFGS-driven traces are stated against
+_DT = torch.float32 if os.environ.get("FAKE_HIP_DTYPE", "float64") == "float32" else torch.float64
+
+
 def _d(t):
-    return None if t is None else t.detach().double()
+    return None if t is None else t.detach().to(_DT)
 
 
 def _out(t, like):
@@ -57,7 +65,7 @@ def gauss_red(op, x, y, sigma, b=None, c=None):
     elif op == L.MIN_SQDIST_OTHER:
         return _out(R.MinSqDistOther(x.detach()), x)
     elif op == L.MIN_SQDIST:
-        r = R.MinSqDist(X, Y) if Y.shape[0] else torch.full((X.shape[0],), float("inf"), dtype=torch.float64)
+        r = R.MinSqDist(X, Y) if Y.shape[0] else torch.full((X.shape[0],), float("inf"), dtype=_DT)
     else:
         raise NotImplementedError(op)
     return _out(r, x)
@@ -70,7 +78,7 @@ def gauss_red_grad(kind, x, y, sigma, r1=None, r2=None, c1=None, c2=None, cw=Non
     M, D = X.shape
     N = Y.shape[0]
     s = 1.0 / sigma ** 2
-    z0 = lambda n: torch.zeros(n, D, dtype=torch.float64)
+    z0 = lambda n: torch.zeros(n, D, dtype=_DT)
     R1 = _d(r1) if r1 is not None else z0(M)
     C1 = _d(c1) if c1 is not None else z0(N)
     if kind == L.GRAD_HESSW and r2 is None and c2 is None:
@@ -80,7 +88,7 @@ def gauss_red_grad(kind, x, y, sigma, r1=None, r2=None, c1=None, c2=None, cw=Non
     else:
         R2 = _d(r2) if r2 is not None else z0(M)
         C2 = _d(c2) if c2 is not None else z0(N)
-    W = _d(cw) if cw is not None else torch.ones(N, dtype=torch.float64)
+    W = _d(cw) if cw is not None else torch.ones(N, dtype=_DT)
     z = X[:, None, :] - Y[None, :, :]
     r2v = (z * z).sum(-1)
     K = torch.exp(-0.5 * s * r2v)

@@ -9,8 +9,7 @@ the 4-row VJP from ~90k -- against the chunked float64 restatement of tests/full
 cloud (workloads.two_set_points).
 
 Criterion: ||hip - ref64|| / ||ref64|| <= max(1e-5, 2 x the float32
-restatement's own deviation) for q1, cost1, trajloss and grad_p0 (for the logdet model's
-cancellation-dominated scalars cost1 / trajloss / loss: 4 x, see the test).
+restatement's own deviation) for q1, cost1, trajloss, loss and grad_p0, for both models.
 """
 import math
 
@@ -105,10 +104,10 @@ def test_shoot_and_gradient_fullsize(dev, M, version, disp):
     disp_sig = float((r64[0].reshape(q0.shape) - q0).norm(dim=1).max()) / SIG
     print("e2e", M, version, f"disp {disp_sig:.3f} sigma", {k: (f"{e:.2e}", f"{t:.2e}") for k, (e, t) in report.items()})
     for n, (e, t) in report.items():
-        if version == "logdet" and n in ("cost1", "trajloss", "loss"):
-            # from the zero-speed a0 (a ridge solution of an ill-conditioned K, K a0 ~ eta
-            # GradKRed) the cost integral and the Hamiltonian are differences of much larger
-            # terms: the float32 restatement itself is off by ~1.5% (measured 20k: cost1
-            # 1.5e-2, trajloss 1.3e-2), so these scalars get 4 x its deviation, not 2 x
-            t = 2 * t
+        # logdet: from the zero-speed a0 (a ridge solution of an ill-conditioned K, K a0 ~ eta
+        # GradKRed) the velocity, the cost integrand and the Hamiltonian are small differences
+        # of large sums; the eta != 0 forward forms them from double totals with launch
+        # constants exact to float64 (packed.hpp EtaConsts, rowred_pk_body_f64), which puts the
+        # HIP path 2-8x INSIDE the float32 restatement's own deviation (round 6,
+        # tools/probes/logdet_cost_diag.py; round 5 was 1.1-2.5x outside it)
         assert e <= t, (n, e, t, report)

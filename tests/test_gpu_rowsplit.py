@@ -169,15 +169,23 @@ def _free_port():
     return port
 
 
-def _two_set(split, overlap=None):
+def _two_set(split, overlap=None, hint_any=False):
     sys.path.insert(0, ROOT)
     from difficp_amd import workloads
+    from difficp_amd.core import GMM
     dev = torch.device("cuda:0")
-    psr = workloads.build_two_set(3000, dev, seed=4, nt=5)
-    if split:
-        psr.LMi.set_row_split(overlap=overlap)
-    workloads.psr_iteration(psr, max_repeat_GMM=3, tol=1e-6)
-    return {"FE": float(psr.FE), "a0": psr.a0[0].detach().cpu().clone(),
+    old = GMM._HINT_ANY
+    GMM._HINT_ANY = hint_any     # another float32 realisation of the same EM (the E-step shift hint)
+    try:
+        psr = workloads.build_two_set(3000, dev, seed=4, nt=5)
+        if split:
+            psr.LMi.set_row_split(overlap=overlap)
+        psr.GMM_opt(max_iterations=3, tol=1e-6)        # = workloads.psr_iteration(psr, 3, 1e-6)
+        fe_em = float(psr.FE)
+        psr.Reg_opt(tol=1e-6, nmax=1)
+    finally:
+        GMM._HINT_ANY = old
+    return {"FE": float(psr.FE), "FE_em": fe_em, "a0": psr.a0[0].detach().cpu().clone(),
             "x1": psr.x1[0, 0].detach().cpu().clone()}
 
 
@@ -188,7 +196,7 @@ def _worker(rank, world, port, q, overlap=None):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = _two_set(True, overlap)
-        q.put((rank, res["FE"], res["a0"].numpy(), res["x1"].numpy()))
+        q.put((rank, res["FE"], res["a0"].numpy(), res["x1"].numpy(), res["FE_em"]))
     finally:
         dist.destroy_process_group()
 
@@ -196,9 +204,16 @@ def _worker(rank, world, port, q, overlap=None):
 @pytest.mark.parametrize("overlap", [None, True])
 def test_rowsplit_two_set_on_gpu(dev, overlap):
     """overlap None: the default at W = 2 (one-pass steps); True: the forward steps in the two
-    column phases with the all-gather in flight (async work handles)."""
+    column phases with the all-gather in flight (async work handles).
+    The EM stage (before any L-BFGS) agrees to 1e-6.  The final free energy follows one
+    L-BFGS run (Reg_opt), which amplifies rounding-level differences ~1e3-fold (the split sums
+    the EM statistics and the VJP in another order): it is held to max(1e-5, 2 x) the spread
+    between two float32 realisations of the single-device run (E-step shift hint rules: 2e-5
+    relative, measured round 6, tools/probes/rowsplit_fe.py)."""
     import numpy as np
     single = _two_set(False)
+    alt = _two_set(False, hint_any=True)
+    spread = abs(alt["FE"] - single["FE"])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -209,8 +224,10 @@ def test_rowsplit_two_set_on_gpu(dev, overlap):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, fe, a0, x1 in out:
-        assert abs(fe - single["FE"]) < 1e-5 * abs(single["FE"]), (rank, fe, single["FE"])
+    for rank, fe, a0, x1, fe_em in out:
+        assert abs(fe_em - single["FE_em"]) < 1e-6 * abs(single["FE_em"]), (rank, fe_em, single["FE_em"])
+        tol = max(1e-5 * abs(single["FE"]), 2 * spread)
+        assert abs(fe - single["FE"]) < tol, (rank, fe, single["FE"], alt["FE"])
         assert np.abs(x1 - single["x1"].numpy()).max() < 1e-3
     assert out[0][1] == out[1][1]
     assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])

@@ -276,10 +276,130 @@ def vsrc_main():
                           "proj_abs_scale": float(dt * (e.abs() * gq.abs()).sum())}), flush=True)
 
 
+def accum_main():
+    """Which accumulation scheme of the velocity sums V = sum K p, Z = sum K z (float32 pair
+    terms as the kernels form them) removes the systematic v error (vsrc_main): sequential
+    float32 sums over sub-tiles of T columns, sub-tile totals in float32 or float64 -- the
+    first-order effect on the next step's sum g, as vsrc_main."""
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=20000)
+    args = ap.parse_args(sys.argv[2:])
+    from difficp_amd import workloads
+    from difficp_amd.core.LDDMM import LDDMMModel
+    dev = torch.device("cuda:0")
+    M = args.M
+    _, xB = workloads.two_set_points(M, seed=3)
+    q0 = xB.double().to(dev)
+    g = torch.Generator().manual_seed(M)
+    ph = torch.rand(3, generator=g, dtype=torch.float64).to(dev)
+    p0 = 2e-6 * torch.sin(2 * math.pi * (q0[:, [1, 2, 0]] + ph))
+    eta = 1.0 / LAM
+    LM0 = LDDMMModel(sigma=SIG, D=3, lambd=LAM, version="logdet", scheme="Euler", nt=NT,
+                     spec={"device": dev, "dtype": torch.float32})
+    q32 = q0.float().contiguous()
+    a0 = LM0.v2p(q32, torch.zeros_like(q32), version="ridge_keops", alpha=1e-3)
+    p = p0 + a0.double()
+    q = q0
+    s = 1.0 / SIG ** 2
+    qf, pf = q.float(), p.float()
+    gq, _ = F.ode_vjp_full(q, p, torch.zeros_like(q), None, 1.0, SIG, eta, True)
+    v64 = F.ode_full(q, p, SIG, eta, True)[0]
+    dt = 1.0 / NT
+    schemes = [(256, "f32"), (256, "f64"), (64, "f64"), (32, "f64"), (16, "f64"), (8, "f64"),
+               (1, "f64")]
+    B = 256
+    accs = {sc: (torch.zeros(M, 6, dtype=torch.float32, device=dev),
+                 torch.zeros(M, 6, dtype=torch.float64 if sc[1] == "f64" else torch.float32, device=dev))
+            for sc in schemes}
+    for j0 in range(0, M, B):
+        qj, pj = qf[j0:j0 + B], pf[j0:j0 + B]
+        z = qf[:, None, :] - qj[None]                       # (M, B, 3) float32
+        K = torch.exp(-0.5 * s * (z * z).sum(-1))           # float32
+        terms = torch.cat([K[:, :, None] * pj[None], K[:, :, None] * z], 2)   # (M, B, 6) float32
+        for c in range(terms.shape[1]):
+            t = terms[:, c]
+            for (T, tot) in schemes:
+                part, total = accs[(T, tot)]
+                part += t
+                if (c + 1) % T == 0 or c == terms.shape[1] - 1:
+                    total += part.to(total.dtype)
+                    part.zero_()
+    for sc in schemes:
+        tot = accs[sc][1].double()
+        v = tot[:, :3] + eta * s * tot[:, 3:]
+        e = v - v64
+        print(json.dumps({"what": "accum", "M": M, "subtile": sc[0], "total": sc[1], "rel": rel(v, v64),
+                          "proj": float(dt * (e * gq).sum())}), flush=True)
+
+
+def const_main():
+    """Do the float32 roundings of the kernels' launch constants drive the systematic v error?
+    Float64 sums over the float32-rounded points, with (a) the exact exponent and coefficient,
+    (b) the exponent of the float32 coordinate scale alpha32 (K = 2^(-alpha32^2 |z|^2), i.e. a
+    sigma off by alpha's rounding), (c) the coefficient of Z' as the kernel forms it
+    (eta32 * (s / alpha64)_32, applied to sum K alpha32 z), (d) both -- each as vsrc_main's
+    first-order effect on the next step's sum g."""
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=20000)
+    args = ap.parse_args(sys.argv[2:])
+    import numpy as np
+    from difficp_amd import workloads
+    from difficp_amd.core.LDDMM import LDDMMModel
+    dev = torch.device("cuda:0")
+    M = args.M
+    _, xB = workloads.two_set_points(M, seed=3)
+    q0 = xB.double().to(dev)
+    g = torch.Generator().manual_seed(M)
+    ph = torch.rand(3, generator=g, dtype=torch.float64).to(dev)
+    p0 = 2e-6 * torch.sin(2 * math.pi * (q0[:, [1, 2, 0]] + ph))
+    eta = 1.0 / LAM
+    LM0 = LDDMMModel(sigma=SIG, D=3, lambd=LAM, version="logdet", scheme="Euler", nt=NT,
+                     spec={"device": dev, "dtype": torch.float32})
+    q32 = q0.float().contiguous()
+    a0 = LM0.v2p(q32, torch.zeros_like(q32), version="ridge_keops", alpha=1e-3)
+    p = p0 + a0.double()
+    q = q0
+    s = 1.0 / SIG ** 2
+    gq, _ = F.ode_vjp_full(q, p, torch.zeros_like(q), None, 1.0, SIG, eta, True)
+    v64 = F.ode_full(q, p, SIG, eta, True)[0]
+    dt = 1.0 / NT
+    qd, pd = q.float().double(), p.float().double()
+    a64 = math.sqrt(1.4426950408889634 / (2.0 * SIG * SIG))
+    a32 = float(np.float32(a64))
+    sa32 = float(np.float32(s / a64))
+    c_kernel = float(np.float32(np.float32(eta) * np.float32(sa32)))   # eta * sa in the store
+
+    def v_of(alpha_exp, coef, rows=2048, chunk=4096):
+        out = []
+        for r0 in range(0, M, rows):
+            qr = qd[r0:r0 + rows]
+            V = torch.zeros_like(qr)
+            Z = torch.zeros_like(qr)
+            for j0 in range(0, M, chunk):
+                z = qr[:, None, :] - qd[None, j0:j0 + chunk]
+                K = torch.exp2(-(alpha_exp ** 2) * (z * z).sum(-1))
+                V += K @ pd[j0:j0 + chunk]
+                Z += (K[:, :, None] * z).sum(1)
+            out.append(V + coef * Z)
+        return torch.cat(out)
+
+    for name, ae, co in (("exact", a64, eta * s), ("alpha32_exponent", a32, eta * s),
+                         ("kernel_coef", a64, c_kernel * a32), ("both", a32, c_kernel * a32)):
+        v = v_of(ae, co)
+        e = v - v64
+        print(json.dumps({"what": "const", "M": M, "variant": name, "rel": rel(v, v64),
+                          "proj": float(dt * (e * gq).sum()), "alpha_rel": a32 / a64 - 1,
+                          "coef_rel": c_kernel * a32 / (eta * s) - 1}), flush=True)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "mixed":
         mixed_main()
     elif len(sys.argv) > 1 and sys.argv[1] == "vsrc":
         vsrc_main()
+    elif len(sys.argv) > 1 and sys.argv[1] == "accum":
+        accum_main()
+    elif len(sys.argv) > 1 and sys.argv[1] == "const":
+        const_main()
     else:
         main()
