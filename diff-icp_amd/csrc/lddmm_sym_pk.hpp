@@ -977,6 +977,9 @@ struct SymFwdPk4 {
 // pair-equivalents, against 2 x (56 v_pk + 9 + 9 + 4 exp) for the 4-row form.  Own body (the
 // 4-row sym_pk4_body also runs the tuned VJP, whose schedule must not move); slots and merge
 // as the 4-row form with G = 512.
+#ifndef DICP_SYMFWD8_WPE
+#define DICP_SYMFWD8_WPE 1
+#endif
 constexpr int kSymG8 = 512;
 template <int D, bool DIV>
 struct SymFwdPk8 {
@@ -988,29 +991,28 @@ struct SymFwdPk8 {
   __device__ static void pair_sym8(const Row2* r, const float* rec, f2 (*acc)[W], float* ct) {
     f2 cv[2 * D];
     P4::colvec(rec, cv);
-    Sh t[4];
+    // one row pair at a time: its shared terms, row side, and its share of the column side
+    // chained into the column partials (the same h = 0..3 order as summing them afterwards),
+    // so only one pair's temporaries are live (168 VGPRs: 3 waves / SIMD)
+    f2 cV[D], cG[D], cZ[D];
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      P4::shared(r[h], cv, t[h]);
-      P4::row_side(t[h], cv, acc[h]);
+      Sh t;
+      P4::shared(r[h], cv, t);
+      P4::row_side(t, cv, acc[h]);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        // column j's side over the 8 rows; (i, j) -> (j, i) flips z
+        cV[d] = h == 0 ? t.K * r[h].p[d] : pk_fma(t.K, r[h].p[d], cV[d]);
+        cG[d] = h == 0 ? t.Kpp * t.z[d] : pk_fma(t.Kpp, t.z[d], cG[d]);
+        if (DIV) cZ[d] = h == 0 ? t.K * t.z[d] : pk_fma(t.K, t.z[d], cZ[d]);
+      }
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      // column j's side over the 8 rows, chained over the 4 row pairs; (i, j) -> (j, i) flips z
-      f2 cV = t[0].K * r[0].p[d], cG = t[0].Kpp * t[0].z[d];
-#pragma unroll
-      for (int h = 1; h < 4; ++h) {
-        cV = pk_fma(t[h].K, r[h].p[d], cV);
-        cG = pk_fma(t[h].Kpp, t[h].z[d], cG);
-      }
-      ct[d] = cV.x + cV.y;
-      ct[D + d] = -(cG.x + cG.y);
-      if (DIV) {
-        f2 cZ = t[0].K * t[0].z[d];
-#pragma unroll
-        for (int h = 1; h < 4; ++h) cZ = pk_fma(t[h].K, t[h].z[d], cZ);
-        ct[2 * D + d] = -(cZ.x + cZ.y);
-      }
+      ct[d] = cV[d].x + cV[d].y;
+      ct[D + d] = -(cG[d].x + cG[d].y);
+      if (DIV) ct[2 * D + d] = -(cZ[d].x + cZ[d].y);
     }
   }
   __device__ static void pair_row(const Row2& r, const float* rec, f2* acc) {
@@ -1019,7 +1021,7 @@ struct SymFwdPk8 {
 };
 
 template <int D, bool DIV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void sym_fwd_pk8_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD8_WPE, 4))) void sym_fwd_pk8_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride) {
   using P = SymFwdPk8<D, DIV>;
   using P4 = SymFwdPk4<D, DIV>;
@@ -1038,15 +1040,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   const int A = kSymQ * Q + wv;
 
   typename P::Row2 row[4];
-  int64_t ri[8];
-  bool rv[8];
+  // row r of the lane: A * G + r * 64 + l (recomputed at the stores: no index registers live
+  // across the pair loop)
+  const int64_t rbase = (int64_t)A * G + l;
   {
     typename S::Row r8[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      ri[r] = (int64_t)A * G + r * 64 + l;
-      rv[r] = A < nG && ri[r] < M;
-      S::load_row(a, sc, rv[r] ? ri[r] : 0, rv[r], r8[r]);
+      const int64_t ri = rbase + r * 64;
+      const bool rv = A < nG && ri < M;
+      S::load_row(a, sc, rv ? ri : 0, rv, r8[r]);
     }
 #pragma unroll
     for (int h = 0; h < 4; ++h) P4::pack(r8[2 * h], r8[2 * h + 1], row[h]);
@@ -1144,8 +1147,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   }
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    if (!rv[r]) continue;
-    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri[r] * W;
+    const int64_t ri = rbase + r * 64;
+    if (!(A < nG && ri < M)) continue;
+    float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri * W;
     const f2* ra = racc[r >> 1];
 #pragma unroll
     for (int k = 0; k < W; ++k) dst[k] = (r & 1) == 0 ? ra[k].x : ra[k].y;

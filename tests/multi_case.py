@@ -11,12 +11,21 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "multi
 CASES = ("m2d", "m3d")
 
 
-def build(spec, case, z):
-    """The DiffPSR of make_golden.multi_case, with reinitialize_GMM's draws injected."""
+def build(spec, case, z, perturb=None):
+    """The DiffPSR of make_golden.multi_case, with reinitialize_GMM's draws injected; perturb:
+    a seed of std_support_case.ulp_perturb applied to the float32 inputs (None: as stored)."""
+    from std_support_case import ulp_perturb
     from difficp_amd.core.GMM import GaussianMixtureUnif
     from difficp_amd.core.LDDMM import LDDMMModel
     from difficp_amd.core.PSR import DiffPSR
-    T = lambda k: torch.from_numpy(np.asarray(z[k])).to(dtype=spec["dtype"], device=spec["device"])
+    cnt = [0]
+
+    def T(k):
+        t = torch.from_numpy(np.asarray(z[k])).to(dtype=spec["dtype"], device=spec["device"])
+        if perturb is None:
+            return t
+        cnt[0] += 1
+        return ulp_perturb(t, 1000 * perturb + cnt[0])
     x = [[T(f"{case}/x0_{k}_{s}") for s in range(3)] for k in range(3)]
     D = x[0][1].shape[1]
     if case == "m2d":
@@ -41,10 +50,10 @@ def build(spec, case, z):
     return PS
 
 
-def run_multi(spec, case, iters=2, check=None):
+def run_multi(spec, case, iters=2, check=None, perturb=None):
     """check(stage, it, PS, z) after init ("init"), each GMM_opt ("gmm") and Reg_opt ("reg")."""
     z = np.load(GOLD)
-    PS = build(spec, case, z)
+    PS = build(spec, case, z, perturb)
     check("init", -1, PS, z)
     for it in range(iters):
         PS.GMM_opt(max_iterations=10, tol=1e-3)
@@ -93,14 +102,23 @@ def group(name):
     raise KeyError(name)
 
 
-# Worst float32 deviation of the oracle-backed host logic from the float64 trace over the 2
-# iterations, per quantity group (measured by test_host_logic.py::
-# test_multi_structure_fp32_oracle_deviation, rounded up by ~10%; eta0 is absolute, the
-# others relative).  L-BFGS with a strong-Wolfe line search amplifies fp32 rounding into a0
-# (SURVEY 7(c)); the GPU test allows max(1e-4, 2 x these).
-FP32_DEV = {
-    "m2d": {"fe": 1.0e-5, "mu": 3.5e-5, "w": 3.1e-4, "sigma": 4.0e-5, "Cfe": 1.7e-5,
-            "a0": 5.1e-3, "x1": 2.2e-4, "quadloss": 4.6e-4},
-    "m3d": {"fe": 2.2e-4, "mu": 3.9e-4, "w": 4.5e-3, "sigma": 7.7e-4, "Cfe": 4.2e-4,
-            "eta0": 3.4e-2, "a0": 3.9e-3, "x1": 7.7e-4, "quadloss": 1.3e-3},
+# The float32 drift envelope per stage ("gmm0", "reg0", "gmm1", "reg1") and quantity group:
+# the worst deviation from the reference's float64 trace over 7 float32 realisations -- the
+# reference's torch path in float32 (SURVEY 8(c)'s oracle32: fake_hip with
+# FAKE_HIP_DTYPE=float32) on the inputs as stored and on 6 ulp-perturbed copies
+# (std_support_case.ulp_perturb seeds 1..6), rounded up ~10% (eta0 absolute, the others
+# relative).  The strong-Wolfe L-BFGS of the second Reg_opt is bimodal in float32 on m2d: 4 of
+# the 7 realisations land frame 1's momenta 6.8e-2 from the float64 ones (x1 1.2e-3, quadloss
+# 1e-2), 3 land within 9e-3 -- a single realisation is one sample of that spread.
+# tools/probes/fp32_ensemble.py oracle 6, profiles/r06_fp32_ensemble_oracle32.jsonl.  The GPU
+# test allows max(floor, 2 x these).
+FP32_ENV = {
+    "m2d": {"gmm0": {"fe": 9.9e-7, "mu": 3.3e-5, "w": 2.4e-4, "sigma": 3.8e-6, "Cfe": 9.0e-6},
+            "reg0": {"fe": 7.8e-6, "a0": 1.7e-3, "x1": 9.9e-5, "quadloss": 3.0e-4},
+            "gmm1": {"fe": 5.3e-5, "mu": 1.1e-4, "w": 1.7e-3, "sigma": 2.2e-4, "Cfe": 2.6e-4},
+            "reg1": {"fe": 3.4e-4, "a0": 7.7e-2, "x1": 1.5e-3, "quadloss": 1.2e-2}},
+    "m3d": {"gmm0": {"fe": 6.9e-7, "mu": 3.6e-6, "w": 1.2e-4, "sigma": 5.2e-6, "Cfe": 3.0e-6, "eta0": 1.1e-5},
+            "reg0": {"fe": 5.1e-5, "a0": 7.6e-3, "x1": 6.6e-4, "quadloss": 9.7e-4},
+            "gmm1": {"fe": 2.2e-4, "mu": 3.2e-4, "w": 3.0e-3, "sigma": 6.2e-4, "Cfe": 2.7e-4, "eta0": 1.1e-1},
+            "reg1": {"fe": 8.1e-5, "a0": 3.1e-3, "x1": 1.1e-3, "quadloss": 1.9e-3}},
 }

@@ -21,14 +21,33 @@ def inputs():
     return xs, y0
 
 
-def run(spec, scheme, weights, warned=None):
+def ulp_perturb(t, seed):
+    """A float32 realisation of the same inputs: every coordinate moved by -1, 0 or +1 ulp of
+    float32 (seeded), i.e. within the rounding any float32 evaluation makes anyway -- the
+    optimisation traces' spread over such realisations is the float32 drift envelope
+    (tools/probes/fp32_ensemble.py)."""
+    if seed is None:
+        return t
+    g = torch.Generator().manual_seed(int(seed))
+    s = torch.randint(-1, 2, t.shape, generator=g).to(t.device)
+    t32 = t.to(torch.float32)
+    up = torch.nextafter(t32, torch.full_like(t32, float("inf")))
+    dn = torch.nextafter(t32, torch.full_like(t32, float("-inf")))
+    return torch.where(s > 0, up, torch.where(s < 0, dn, t32)).to(t.dtype)
+
+
+def run(spec, scheme, weights, warned=None, perturb=None):
     """Returns (the DiffPSR_std, [E after init, Reg, Template, Reg, Template]); `warned` (a
-    list): the energy-increase warnings raised on the way are appended to it."""
+    list): the energy-increase warnings raised on the way are appended to it; perturb: a seed
+    of ulp_perturb (None: the golden inputs as drawn)."""
     import warnings as W
     from difficp_amd.core.LDDMM import LDDMMModel
     from difficp_amd.core.PSR_standard import DiffPSR_std
     from difficp_amd.tools.kernel import GaussKernel
     xs, y0 = inputs()
+    if perturb is not None:
+        xs = [ulp_perturb(x, 1000 * perturb + k) for k, x in enumerate(xs)]
+        y0 = ulp_perturb(y0, 1000 * perturb + 999)
     T = lambda t: t.to(**spec)
     DK = GaussKernel(0.1, 2, spec=spec)
     LM = LDDMMModel(sigma=0.2, D=2, lambd=2.0, version="classic", scheme="Euler", nt=10, spec=spec)
@@ -38,6 +57,7 @@ def run(spec, scheme, weights, warned=None):
     with W.catch_warnings(record=True) as caught:
         W.simplefilter("always")
         P.set_support_scheme(scheme, rho=1.0)
+        P.n_support0 = P.q0.shape[0]     # the support as set (test_gpu_support.py checks it)
         Es = [P.E]
         for _ in range(2):
             P.Reg_opt(nmax=2, tol=1e-4)
@@ -59,7 +79,24 @@ def reference_warnings(scheme, weights):
     return int(np.load(GOLD)[f"{scheme}_w{int(weights)}/n_increase_warnings"])
 
 
-# worst relative float32 deviation of the oracle-backed host logic from the float64 energies
-# over the 5 recorded stages (test_host_logic.py::test_psr_std_support_fp32_oracle_deviation,
-# rounded up ~10%); the GPU test allows max(1e-3, 2 x these)
-FP32_DEV = {("grid", False): 2.2e-3, ("grid", True): 1.6e-3}
+# The float32 drift envelope of each stage (E after init, Reg_opt, Template_opt, Reg_opt,
+# Template_opt): the worst relative deviation from the reference's float64 energies over 7
+# float32 realisations of the trace -- the reference's torch path in float32 (SURVEY 8(c)'s
+# oracle32: fake_hip with FAKE_HIP_DTYPE=float32) on the inputs as drawn and on 6 ulp-perturbed
+# copies (ulp_perturb seeds 1..6), rounded up ~10%.  Four strong-Wolfe L-BFGS runs amplify
+# float32 rounding: one realisation is a single sample of that spread (the unperturbed oracle32
+# reaches 7.5e-4 at the last grid_w1 stage, seed 5 reaches 1.5e-2; decim is not float32-
+# reproducible past the first Reg_opt at all).  tools/probes/fp32_ensemble.py oracle 6,
+# profiles/r06_fp32_ensemble_oracle32.jsonl.  The GPU test allows max(floor, 2 x these).
+FP32_ENV = {
+    ("grid", False): [1.9e-6, 1.2e-4, 4.4e-4, 1.2e-3, 3.4e-3],
+    ("grid", True): [1.7e-6, 1.3e-4, 5.5e-4, 1.8e-2, 1.7e-2],
+    ("decim", False): [1.9e-6, 2.0e-5, 3.3e-4, 1.1e-1, 2.3e-1],
+    ("decim", True): [1.7e-6, 3.6e-5, 7.0e-4, 8.0e-2, 1.9e-1],
+}
+# the energy-increase warnings (PSR_standard.py:311-315) over the same 7 float32 realisations:
+# the reference's float64 run raises 1 (decim, no weights) and 0 (otherwise); in float32 the
+# decim traces raise 1-2 without and 0-1 with template weights -- a float32 property of the
+# reference algorithm, not of the HIP path
+FP32_WARNINGS = {("grid", False): (0, 0), ("grid", True): (0, 0),
+                 ("decim", False): (1, 2), ("decim", True): (0, 1)}

@@ -578,21 +578,24 @@ def test_multi_structure_reinitialize_gmm_draws(fake):
 
 
 @pytest.mark.parametrize("case", ["m2d", "m3d"])
-def test_multi_structure_fp32_oracle_deviation(fake, case):
-    """The float32 deviation of the oracle-backed host logic from the float64 multi-structure
-    trace; test_gpu_multi.py takes 2 x this (the SURVEY 8c criterion) per quantity."""
+def test_multi_structure_fp32_oracle_deviation(fake, monkeypatch, case):
+    """The float32 oracle (the reference's torch path in float32, FAKE_HIP_DTYPE=float32) on the
+    multi-structure inputs as stored lies inside multi_case.FP32_ENV, the drift envelope of 7
+    float32 realisations that test_gpu_multi.py takes 2 x of (the SURVEY 8c criterion)."""
     import multi_case
+    monkeypatch.setattr(fake_hip, "_DT", torch.float32)
     worst = {}
 
     def check(stage, it, PS, z):
         if stage == "init":
             return
         for k, v in multi_case.deviations(PS, z, case, stage, it).items():
-            worst[k] = max(worst.get(k, 0.0), v)
+            key = (f"{stage}{it}", multi_case.group(k))
+            worst[key] = max(worst.get(key, 0.0), v)
     multi_case.run_multi({"device": "cpu", "dtype": torch.float32}, case, iters=2, check=check)
     print(case, {k: f"{v:.3g}" for k, v in worst.items()})
-    for k, v in worst.items():
-        assert v <= multi_case.FP32_DEV[case][multi_case.group(k)], (k, v)
+    for (st, g), v in worst.items():
+        assert v <= multi_case.FP32_ENV[case][st][g], (st, g, v)
 
 
 def test_psr_std_support_trace_host_logic_fp64(fake):
@@ -612,22 +615,25 @@ def test_psr_std_support_trace_host_logic_fp64(fake):
     assert C.reference_warnings("decim", False) == 1 and len(warned) == 1, warned
 
 
-def test_psr_std_support_fp32_oracle_deviation(fake):
-    """The float32 deviation of the oracle-backed host logic from the float64 grid-support
-    traces: test_gpu_support.py::test_psr_std_support_schemes allows max(1e-3, 2 x) this.
-    (The decim traces -- 4-5 support points for the 120-point template -- are not float32-
-    reproducible at all: measured 0.40 / 0.13 relative after four L-BFGS runs, so the GPU test
-    pins only their initial energy and the reference's own energy-increase warning.)"""
+@pytest.mark.parametrize("scheme", ["grid", "decim"])
+@pytest.mark.parametrize("weights", [False, True])
+def test_psr_std_support_fp32_oracle_deviation(fake, monkeypatch, scheme, weights):
+    """The float32 oracle (the reference's torch path in float32) on the PSR_std support-scheme
+    inputs as drawn lies, stage by stage, inside std_support_case.FP32_ENV -- the drift envelope
+    of 7 float32 realisations that test_gpu_support.py takes 2 x of -- and raises a number of
+    energy-increase warnings inside FP32_WARNINGS (the reference's float64 run: 1 for decim
+    without weights, 0 otherwise)."""
     import std_support_case as C
-    worst = {}
-    for scheme in ("grid",):
-        for weights in (False, True):
-            _, Es = C.run({"device": "cpu", "dtype": torch.float32}, scheme, weights)
-            ref = C.reference(scheme, weights)
-            worst[(scheme, weights)] = max(abs(a - b) / abs(b) for a, b in zip(Es, ref))
-    print("FP32DEV", worst)
-    for k, v in worst.items():
-        assert v <= C.FP32_DEV[k], (k, v)
+    monkeypatch.setattr(fake_hip, "_DT", torch.float32)
+    warned = []
+    _, Es = C.run({"device": "cpu", "dtype": torch.float32}, scheme, weights, warned)
+    ref = C.reference(scheme, weights)
+    dev = [abs(a - b) / abs(b) for a, b in zip(Es, ref)]
+    print("FP32DEV", scheme, weights, dev, len(warned))
+    for i, (v, e) in enumerate(zip(dev, C.FP32_ENV[(scheme, weights)])):
+        assert v <= e, (i, v, e)
+    lo, hi = C.FP32_WARNINGS[(scheme, weights)]
+    assert lo <= len(warned) <= hi, warned
 
 
 def test_shoot_list_semantics_and_pickle():

@@ -43,7 +43,13 @@ fns = {"fwd": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.0, True),
        "mstep": lambda: _lib.gmm_mstep(q, T2, q, w2, 0.05),
        "estep_c4": lambda: _lib.gmm_estep(X4, mu4, w24, m24, 0.05, 0.0, True),
        "mstep_c4": lambda: _lib.gmm_mstep(X4, T24, mu4, w24, 0.05),
-       "kred": lambda: _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)}
+       "kred": lambda: _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p),
+       # the exact ICP_two_set model's forward (eta = 1 / lambda != 0, logdet)
+       "fwd_eta": lambda: _lib.ode_self_fwd(q, p, 0.1, 0.01, True),
+       "step_eta": lambda: _lib.euler_step(q, p, 0.1, 0.01, 0.1, True)}
+only = [k for k in os.environ.get("DICP_AB_ONLY", "").split(",") if k]
+if only:
+    fns = {k: v for k, v in fns.items() if k in only}
 out = {}
 for k, fn in fns.items():
     fn(); fn()
