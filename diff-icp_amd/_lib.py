@@ -302,7 +302,11 @@ FLOPS_PER_PAIR = {
 # (FMA = 2 flop, from the hot loop's instruction counts, tools/isa_loop_stats.py): the
 # symmetric pair-once VJP evaluates each unordered pair once.  bench.py reports the fraction
 # of the peak on both counts (roofline.frac = algorithmic, roofline.frac_executed).
-EXEC_FLOPS_PER_PAIR = {"ode_self_bwd": 53}
+EXEC_FLOPS_PER_PAIR = {"ode_self_bwd": 53,
+                       # the symmetric pair-once forward (from 20k points; the 6-row loop: 60
+                       # v_pk_fma + 24 other v_pk + 18 scalar adds + 6 exp per step of 6
+                       # unordered pairs = 306 flop, i.e. 25.5 per ordered pair)
+                       "ode_self_fwd": 25.5}
 # the gp-only VJP (last adjoint step when q0 needs no gradient): 32 of the 60 packed
 # instructions of the full symmetric loop -> priced at that share of the full VJP's figure
 FLOPS_PER_PAIR["ode_self_bwd_gp"] = round(70 * 32 / 60)

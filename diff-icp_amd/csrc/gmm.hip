@@ -95,6 +95,25 @@ __device__ __forceinline__ bool lse_hint_clamped(float m64, float hint) {
   return hint > -1e30f && hint < 1e30f && hint - 8.f > m64 + 100.f;
 }
 
+// ---- the bound shift (the many-component E-step: C >= kLseE4MinCols) -----------------------
+// Every logit is at most its column's distance-0 value, t_nc <= nc v_c = w2_c, so the shift
+// U = max_c nc v_c - kLseBoundSlack (a tiny pass over the C columns, lse_bound_kernel) can never
+// overflow a sum: no logit-only sample pass and no re-reference events, whatever sigma (a
+// 64-column sample sits hundreds of log2 units below a row's nearest component at the two-set
+// bench's converged sigma).  With a hint the shift is min(hint - 8, U).  The price
+// is underflow where a row's LSE lies far below its shift (nearest component beyond ~11 sigma,
+// or a stale-high hint): terms more than 126 below the shift flush to 0, so a row whose LSE
+// ends more than kLseBoundGap below its shift is appended to a list (the finalize) and summed
+// again exactly -- two sweeps, one workgroup per listed row (lse_fixup_kernel).
+constexpr float kLseBoundSlack = 8.f;
+constexpr float kLseBoundGap = 80.f;
+__device__ __forceinline__ float lse_bound_shift(float U, const float* hint, int64_t i) {
+  if (hint == nullptr) return U;
+  const float h = hint[i];
+  if (!(h > -1e30f && h < 1e30f)) return U;
+  return fminf(h - 8.f, U);
+}
+
 // Store a chunk partial {m, l, acc}.  The merge weighs a partial by 2^(m_s - max m): with the
 // shift up to 100 above a chunk's largest term (a clamped hint) and the sums up to 2^77 (terms
 // below the re-reference slack), that factor could underflow while the partial's share did not
@@ -137,7 +156,7 @@ __device__ __forceinline__ void lse_store_part(float* dst, float m, const float*
   }
 }
 
-template <class Op, int R>
+template <class Op, int R, bool BOUND = false>
 __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
                                                             int64_t M, int64_t N, int64_t chunk,
                                                             float* __restrict__ part, int adapt) {
@@ -168,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
     const int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
     if (tid < cnt) Op::load_col(args, sc, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
     __syncthreads();
-    const int ns = cnt < kLseShiftCols ? cnt : kLseShiftCols;
+    const int ns = BOUND ? 0 : (cnt < kLseShiftCols ? cnt : kLseShiftCols);
 #pragma unroll 2
     for (int t = 0; t < ns; ++t) {
       const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
@@ -182,7 +201,11 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_kernel(Args args, Scal sc,
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (m[r] == -__builtin_huge_valf()) m[r] = 0.f;
-    if (hint != nullptr) {   // the row's expected LSE: m = clamp(hint - 8, m64, m64 + 100)
+    if (BOUND) {   // the bound shift min(hint - 8, U): no sample pass, never an overflow
+      int64_t i = ibase + (int64_t)r * kBlock;
+      if (i >= M) i = M - 1;
+      m[r] = lse_bound_shift(args.r2[0], hint, i);
+    } else if (hint != nullptr) {   // the row's expected LSE: m = clamp(hint - 8, m64, m64 + 100)
       int64_t i = ibase + (int64_t)r * kBlock;
       if (i >= M) i = M - 1;
       clamped = clamped || lse_hint_clamped(m[r], hint[i]);
@@ -332,7 +355,7 @@ __device__ __forceinline__ void lse_reref_lane_t(f2& tm2, f2& m2, f2& k2, f2* to
   if (C) { m2.y += tm; k2.y -= tm; tm2.y = 0.f; } else { m2.x += tm; k2.x -= tm; tm2.x = 0.f; }
 }
 
-template <class Op, int H>
+template <class Op, int H, bool BOUND = false>
 __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal sc,
                                                                int64_t M, int64_t N, int64_t chunk,
                                                                float* __restrict__ part, int adapt) {
@@ -369,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
     const int cnt = (int)((j1 - j0) < kTile ? (j1 - j0) : kTile);
     if (tid < cnt) Op::load_col(args, sc, j0 + tid, reinterpret_cast<float*>(&lds[tid * CW4]));
     __syncthreads();
-    const int ns = cnt < kLseShiftCols ? cnt : kLseShiftCols;
+    const int ns = BOUND ? 0 : (cnt < kLseShiftCols ? cnt : kLseShiftCols);
 #pragma unroll 2
     for (int t = 0; t < ns; ++t) {
       const float* rec = reinterpret_cast<const float*>(&lds[t * CW4]);
@@ -386,7 +409,13 @@ __global__ __launch_bounds__(kBlock) void lse_rowred_pk_kernel(Args args, Scal s
   for (int h = 0; h < H; ++h) {
     if (m[h].x == kNinf) m[h].x = 0.f;
     if (m[h].y == kNinf) m[h].y = 0.f;
-    if (hint != nullptr) {
+    if (BOUND) {   // the bound shift (as lse_rowred_kernel)
+      int64_t i0 = ibase + (int64_t)(2 * h) * kBlock, i1 = ibase + (int64_t)(2 * h + 1) * kBlock;
+      if (i0 >= M) i0 = M - 1;
+      if (i1 >= M) i1 = M - 1;
+      const float U = args.r2[0];
+      m[h] = f2{lse_bound_shift(U, hint, i0), lse_bound_shift(U, hint, i1)};
+    } else if (hint != nullptr) {
       int64_t i0 = ibase + (int64_t)(2 * h) * kBlock, i1 = ibase + (int64_t)(2 * h + 1) * kBlock;
       if (i0 >= M) i0 = M - 1;
       if (i1 >= M) i1 = M - 1;
@@ -520,6 +549,14 @@ int& lse_adapt_ref() {
   return v;
 }
 
+int& lse_bound_ref() {
+  static int v = [] {
+    const char* e = getenv("DICP_LSE_BOUND");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 int& lse_pk_ref() {
 #ifndef DICP_LSE_PK
 #define DICP_LSE_PK 1
@@ -528,11 +565,21 @@ int& lse_pk_ref() {
   return v;
 }
 
+// The bound shift's check at the merge (fix != NULL: {U, count, -, -, rows...} in the
+// workspace, lse_bound_kernel): a row whose LSE ended more than kLseBoundGap below its shift may
+// have lost terms to underflow -- appended to the list that lse_fixup_kernel sums again.  NaN
+// rows are not listed (their NaN goes on to T / T2).
+__device__ __forceinline__ void lse_bound_check(int* fix, const Args& args, int64_t i, float mx, float l) {
+  if (fix == nullptr || !(l == l)) return;
+  const float m0 = lse_bound_shift(reinterpret_cast<const float*>(fix)[0], args.r1, i);
+  if (!(mx + log2f(l) >= m0 - kLseBoundGap)) fix[4 + atomicAdd(&fix[1], 1)] = (int)i;
+}
+
 // Merge S chunk partials of each row (fixed order) and finalize through Op::finalize.
 template <class Op>
 __global__ __launch_bounds__(kBlock) void lse_finalize_kernel(const float* __restrict__ part,
                                                               int64_t M, int S, Args args,
-                                                              Scal sc, Outs outs) {
+                                                              Scal sc, Outs outs, int* fix) {
   constexpr int NACC = Op::NACC;
   constexpr int W = 2 + NACC;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -554,6 +601,7 @@ __global__ __launch_bounds__(kBlock) void lse_finalize_kernel(const float* __res
       acc[k] = fmaf(f, a, acc[k]);
     }
   }
+  lse_bound_check(fix, args, i, mx, l);
   Op::finalize(sc, args, i, mx, l, acc, outs);
 }
 
@@ -600,7 +648,7 @@ struct LsePart {
 template <class Op>
 __global__ __launch_bounds__(kBlock) void lse_finalize_wave_kernel(const float* __restrict__ part,
                                                                    int64_t M, int S, Args args,
-                                                                   Scal sc, Outs outs) {
+                                                                   Scal sc, Outs outs, int* fix) {
   constexpr int NACC = Op::NACC;
   constexpr int W = 2 + NACC;
   const int lane = threadIdx.x & 63;
@@ -620,7 +668,96 @@ __global__ __launch_bounds__(kBlock) void lse_finalize_wave_kernel(const float* 
     const float m2 = __shfl_xor(acc.m, off, 64), l2 = __shfl_xor(acc.l, off, 64);
     acc.merge(m2, l2, a2);
   }
-  if (lane == 0) Op::finalize(sc, args, i, acc.m, acc.l, acc.a, outs);
+  if (lane == 0) {
+    lse_bound_check(fix, args, i, acc.m, acc.l);
+    Op::finalize(sc, args, i, acc.m, acc.l, acc.a, outs);
+  }
+}
+
+// U = max_c Op::col_bound(column c) - kLseBoundSlack over the N columns (one workgroup; the
+// maximum is order-free) and the list's count reset: fix = {U, count, -, -, rows...}
+template <class Op>
+__global__ __launch_bounds__(kBlock) void lse_bound_kernel(Args args, Scal sc, int64_t N, int* fix) {
+  __shared__ float red[kBlock];
+  const int tid = threadIdx.x;
+  float mx = -__builtin_huge_valf();
+  for (int64_t j = tid; j < N; j += kBlock) {
+    float rec[4 * Op::CW4];
+    Op::load_col(args, sc, j, rec);
+    mx = fmaxf(mx, Op::col_bound(sc, rec));
+  }
+  red[tid] = mx;
+  __syncthreads();
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    reinterpret_cast<float*>(fix)[0] = red[0] == -__builtin_huge_valf() ? 0.f : red[0] - kLseBoundSlack;
+    fix[1] = 0;
+  }
+}
+
+// The listed rows summed again exactly: one workgroup per row (grid-stride over the list), the
+// exact maximum over all N columns, then one exp sweep against it; thread-strided partials
+// and fixed trees (deterministic whatever the list's order), finalized as the merge does.
+template <class Op>
+__global__ __launch_bounds__(kBlock) void lse_fixup_kernel(Args args, Scal sc, int64_t N, const int* fix,
+                                                           Outs outs) {
+  constexpr int NACC = Op::NACC;
+  __shared__ float red[NACC + 1][kBlock];
+  const int tid = threadIdx.x;
+  const int n = fix[1];
+  for (int k = blockIdx.x; k < n; k += gridDim.x) {
+    const int64_t i = fix[4 + k];
+    typename Op::Row row;
+    Op::load_row(args, sc, i, row);
+    row.k = Op::base(row);
+    float mx = -__builtin_huge_valf();
+    for (int64_t j = tid; j < N; j += kBlock) {
+      float rec[4 * Op::CW4];
+      Op::load_col(args, sc, j, rec);
+      mx = fmaxf(mx, Op::tm(sc, row, rec));
+    }
+    red[0][tid] = mx;
+    __syncthreads();
+    for (int o = kBlock / 2; o > 0; o >>= 1) {
+      if (tid < o) red[0][tid] = fmaxf(red[0][tid], red[0][tid + o]);
+      __syncthreads();
+    }
+    mx = red[0][0];
+    if (mx == -__builtin_huge_valf()) mx = 0.f;
+    __syncthreads();
+    row.k -= mx;
+    float acc[NACC + 1];
+#pragma unroll
+    for (int q = 0; q <= NACC; ++q) acc[q] = 0.f;
+    for (int64_t j = tid; j < N; j += kBlock) {
+      float rec[4 * Op::CW4];
+      Op::load_col(args, sc, j, rec);
+      const float tm = Op::tm(sc, row, rec);
+      const float e = fast_exp2(tm);
+      acc[0] += e;
+      Op::template accum<false>(rec, tm, e, acc + 1);
+    }
+#pragma unroll
+    for (int q = 0; q <= NACC; ++q) red[q][tid] = acc[q];
+    __syncthreads();
+    for (int o = kBlock / 2; o > 0; o >>= 1) {
+      if (tid < o) {
+#pragma unroll
+        for (int q = 0; q <= NACC; ++q) red[q][tid] += red[q][tid + o];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      float a[NACC > 0 ? NACC : 1];
+#pragma unroll
+      for (int q = 0; q < NACC; ++q) a[q] = red[1 + q][0];
+      Op::finalize(sc, args, i, mx, red[0][0], a, outs);
+    }
+    __syncthreads();
+  }
 }
 
 // ---- E-step op ------------------------------------------------------------------------
@@ -660,6 +797,9 @@ struct OpGmmE {
   // (the Chui two-set trace's EM stop test at tol 1e-3 flips one EM step on rounding-level
   // changes -- profiles/r05_chui_uniform_flip.txt)
   static constexpr int kUni = STATS ? D + 1 : -1;
+  // the bound shift (lse_bound_kernel): the column's distance-0 logit nc v_c = w2_c
+  static constexpr bool kBound = true;
+  __device__ static float col_bound(const Scal& sc, const float* rec) { return sc.nc * rec[D]; }
   // per-row shift hint (dicp_gmm_estep_hint_f32): Args::r1, or NULL
   __device__ static const float* hint(const Args& a) { return a.r1; }
   __device__ static float uni_value(const Args& a, const Scal& sc, int64_t j) {
@@ -853,11 +993,21 @@ int lse_splits(int64_t M, int64_t N, bool pk) {
   return num_splits_cap(M, N, R, cap[pk]);
 }
 
+template <class T, class = void>
+struct op_bound : std::false_type {};
+template <class T>
+struct op_bound<T, std::enable_if_t<T::kBound>> : std::true_type {};
+// the bound shift: ops with Op::kBound at R = 4 rows per thread (the many-component E-step),
+// option "lse_bound" (env DICP_LSE_BOUND; 0: the sampled shift as every other pass)
+template <class Op, int R>
+constexpr bool lse_bound_op() { return op_bound<Op>::value && R == 4; }
+
 template <class Op, int R>
 size_t lse_ws_bytes(int64_t M, int64_t N) {   // either kernel (their occupancies may differ)
   const int S0 = lse_splits<Op, R>(M, N, false), S1 = lse_splits<Op, R>(M, N, true);
   const int S = S0 > S1 ? S0 : S1;
-  return (size_t)S * (size_t)M * (size_t)(2 + Op::NACC) * sizeof(float);
+  const size_t fix = lse_bound_op<Op, R>() ? (size_t)(4 + M) * sizeof(int) : 0;
+  return (size_t)S * (size_t)M * (size_t)(2 + Op::NACC) * sizeof(float) + fix;
 }
 
 template <class Op, int R>
@@ -874,22 +1024,50 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
   }
   const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
   float* part = reinterpret_cast<float*>(ws);
-  if (pk)
+  int* fix = nullptr;
+  Args ab = a;
+  if constexpr (lse_bound_op<Op, R>()) {
+    if (lse_bound_ref() != 0 && N > 0) {   // {U, count, -, -, rows} after the partials
+      fix = reinterpret_cast<int*>(part + (size_t)S * (size_t)M * (size_t)(2 + Op::NACC));
+      lse_bound_kernel<Op><<<dim3(1), dim3(kBlock), 0, st>>>(a, sc, N, fix);
+      ab.r2 = reinterpret_cast<const float*>(fix);
+    }
+  }
+  if (fix != nullptr) {
+    if constexpr (lse_bound_op<Op, R>()) {
+      if (pk)
+        lse_rowred_pk_kernel<Op, R / 2, true><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
+            ab, sc, M, N, chunk, part, lse_adapt_ref());
+      else
+        lse_rowred_kernel<Op, R, true><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
+            ab, sc, M, N, chunk, part, lse_adapt_ref());
+    }
+  } else if (pk) {
     lse_rowred_pk_kernel<Op, R / 2><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
         a, sc, M, N, chunk, part, lse_adapt_ref());
-  else
+  } else {
     lse_rowred_kernel<Op, R><<<dim3((unsigned)bx, (unsigned)S), dim3(kBlock), 0, st>>>(
         a, sc, M, N, chunk, part, lse_adapt_ref());
+  }
   int rc = check_launch(name);
   if (rc) return rc;
   if (S > kWaveMergeMinSplits) {
     const int64_t nw = (M + kBlock / 64 - 1) / (kBlock / 64);
-    lse_finalize_wave_kernel<Op><<<dim3((unsigned)nw), dim3(kBlock), 0, st>>>(part, M, S, a, sc, fin);
+    lse_finalize_wave_kernel<Op><<<dim3((unsigned)nw), dim3(kBlock), 0, st>>>(part, M, S, a, sc, fin, fix);
   } else {
     const int64_t nb = (M + kBlock - 1) / kBlock;
-    lse_finalize_kernel<Op><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(part, M, S, a, sc, fin);
+    lse_finalize_kernel<Op><<<dim3((unsigned)nb), dim3(kBlock), 0, st>>>(part, M, S, a, sc, fin, fix);
   }
-  return check_launch(name);
+  rc = check_launch(name);
+  if (rc) return rc;
+  if constexpr (lse_bound_op<Op, R>()) {
+    if (fix != nullptr) {   // the listed rows again, exactly (a grid-stride over the list)
+      const int64_t nf = M < 1024 ? M : 1024;
+      lse_fixup_kernel<Op><<<dim3((unsigned)nf), dim3(kBlock), 0, st>>>(a, sc, N, fix, fin);
+      rc = check_launch(name);
+    }
+  }
+  return rc;
 }
 
 template <int D>
@@ -914,6 +1092,7 @@ int estep_d(const float* X, int64_t N, const float* mu, const float* w2, const f
 namespace dicp {
 int& lse_pk() { return lse_pk_ref(); }
 int& lse_adapt() { return lse_adapt_ref(); }
+int& lse_bound() { return lse_bound_ref(); }
 }  // namespace dicp
 
 // The Python wrapper precomputes the C-sized column vectors (w2, |mu|^2, lpi) with torch on

@@ -210,6 +210,7 @@ int& red_alg();
 int& sym_red();
 int& sym_red_rows();   // rows per lane of the pair-once sums: 0 auto, 4, 8
 int& lse_adapt();      // E / M passes: eventful tiles before the per-pair re-reference test
+int& lse_bound();      // many-component E-step: 1 the bound shift + exact re-sum of listed rows
 int& lse_pk();         // E / M passes: 1 packed row pairs (v_pk_*), 0 scalar rows
 int& cx_rho_x100();
 // rows M, columns N; ext: the external-point forward (its non-centred kernel is the packed one)

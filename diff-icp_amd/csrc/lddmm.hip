@@ -115,9 +115,12 @@ bool supported_dim(int D) { return D == 2 || D == 3; }
 // aux1 = s / alpha.
 // The coordinate origin is the first column point (a.c0: the support q of the self ops, the
 // support of the external-point x pass, y of KRed), the same for rows and columns.
-void scale_coords(Args& a, Scal& sc, double sigma) {
+// exact (the eta != 0 forward): Args::scale_lo = alpha - scale, so the coordinates carry the
+// exact alpha (common.hpp ld_coord) and the exponent needs no correction (packed.hpp EtaConsts)
+void scale_coords(Args& a, Scal& sc, double sigma, bool exact = false) {
   const double alpha = std::sqrt(1.4426950408889634 / (2.0 * sigma * sigma));
   a.scale = (float)alpha;
+  a.scale_lo = exact ? (float)(alpha - (double)a.scale) : 0.f;
   a.shift = a.c0;
   sc.aux1 = (float)(1.0 / (sigma * sigma) / alpha);
 }
@@ -125,6 +128,7 @@ void scale_coords(Args& a, Scal& sc, double sigma) {
 // original-unit coordinates for the RAW packed kernels: alpha = 1, no shift, aux1 = s / 1
 void raw_coords(Args& a, Scal& sc) {
   a.scale = 1.f;
+  a.scale_lo = 0.f;
   a.shift = nullptr;
   sc.aux1 = sc.s;
 }
@@ -221,7 +225,7 @@ extern "C" int dicp_set_option(const char* name, int value) {
     return DICP_OK;
   }
   if (!strcmp(name, "sym_fwd_rows")) {
-    if (value != 0 && value != 4 && value != 8) return DICP_ERR_INVALID;
+    if (value != 0 && value != 4 && value != 6 && value != 8) return DICP_ERR_INVALID;
     sym_fwd_rows() = value;
     return DICP_OK;
   }
@@ -233,6 +237,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
   if (!strcmp(name, "lse_adapt")) {
     if (value < 0) return DICP_ERR_INVALID;
     lse_adapt() = value;
+    return DICP_OK;
+  }
+  if (!strcmp(name, "lse_bound")) {
+    if (value < 0 || value > 1) return DICP_ERR_INVALID;
+    lse_bound() = value;
     return DICP_OK;
   }
   if (!strcmp(name, "lse_pk")) {
@@ -272,6 +281,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "sym_red")) { *value = sym_red(); return DICP_OK; }
   if (!strcmp(name, "lse_pk")) { *value = lse_pk(); return DICP_OK; }
   if (!strcmp(name, "lse_adapt")) { *value = lse_adapt(); return DICP_OK; }
+  if (!strcmp(name, "lse_bound")) { *value = lse_bound(); return DICP_OK; }
   if (!strcmp(name, "sym_red_rows")) { *value = sym_red_rows(); return DICP_OK; }
   if (!strcmp(name, "sym_fwd_rows")) { *value = sym_fwd_rows(); return DICP_OK; }
   if (!strcmp(name, "ext_alg")) { *value = g_ext_alg; return DICP_OK; }
@@ -375,19 +385,35 @@ bool use_sym_fwd4(int64_t M, bool all, bool raw) {
   return M >= DICP_SYM_FWD4_MIN_M;
 }
 
-// 8 rows per lane for the symmetric forward (SymFwdPk8, 512-point groups): from
-// DICP_SYM_FWD8_MIN_M points when the pass runs alone on the chip (batch_share 1, not inside a
-// lockstep batch); sym_fwd_rows 4 / 8 forces (tools/probes/fwd8_ab.py).  Measured r05: 8 rows
-// win ~5% at 120k-200k but lose 3% at the north_star's 100k (3.39 vs 3.29 ms), so the rule
-// starts above it
-#ifndef DICP_SYM_FWD8_MIN_M
-#define DICP_SYM_FWD8_MIN_M 110000
+// rows per lane of the symmetric forward (SymFwdPkN) when the pass runs alone on the chip
+// (batch_share 1, not inside a lockstep batch): 6 (384-point groups, 3 waves / SIMD) from
+// DICP_SYM_FWD6_MIN_M points, 8 (512-point groups, 2 waves / SIMD) from DICP_SYM_FWD8_MIN_M,
+// else 4; sym_fwd_rows 4 / 6 / 8 forces.  Measured r06 (tools/probes/symfwd_L.py, the Euler
+// step with divergence rows, profiles/r06_symfwd_rows.jsonl): 6 rows against 4 -2% at 40k,
+// -4% at 60k, -5% at 80k-100k (3.235 vs 3.394 ms at the north_star's 100k), -4% / -7% at
+// 120k / 150k; 8 rows lose at 100k (3.86: 2 workgroups per CU, a ragged last round) and win
+// from ~200k (12.67 vs 13.02 ms)
+#ifndef DICP_SYM_FWD6_MIN_M
+#define DICP_SYM_FWD6_MIN_M 40000
 #endif
-bool use_sym_fwd8(int64_t M) {
-  if (batching()) return false;
-  if (sym_fwd_rows() == 8) return true;
-  if (sym_fwd_rows() == 4) return false;
-  return batch_share() <= 1 && M >= DICP_SYM_FWD8_MIN_M;
+#ifndef DICP_SYM_FWD8_MIN_M
+#define DICP_SYM_FWD8_MIN_M 180000
+#endif
+int sym_fwd_rows_for(int64_t M) {
+  if (batching()) return 4;
+  const int f = sym_fwd_rows();
+  if (f == 4 || f == 6 || f == 8) return f;
+  if (batch_share() > 1) return 4;
+  return M >= DICP_SYM_FWD8_MIN_M ? 8 : M >= DICP_SYM_FWD6_MIN_M ? 6 : 4;
+}
+template <int D, bool DIV>
+int launch_sym_fwd_rows(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                        hipStream_t st, bool zs) {
+  switch (sym_fwd_rows_for(M)) {
+    case 8: return launch_sym_fwd8<D, DIV>(a, sc, M, o, ws, wsb, st, zs);
+    case 6: return launch_sym_fwd6<D, DIV>(a, sc, M, o, ws, wsb, st, zs);
+    default: return launch_sym_fwd4<D, DIV>(a, sc, M, o, ws, wsb, st, zs);
+  }
 }
 
 // rows [row0, row0 + nrows) of the pass against all M columns (row-split over ranks);
@@ -403,7 +429,7 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   const bool all = row0 == 0 && nrows == M;
   Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
-  scale_coords(a, sc, sigma);
+  scale_coords(a, sc, sigma, eta != 0.0);
   const bool raw = tl_coord_raw != 0;   // the packed kernels below; the others stay scaled
   if (zs != nullptr) {
     // divergence rows out through the (unused) h slot: the packed passes only
@@ -419,8 +445,7 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
     // (the mG-less last step keeps the ordered pass without the Gs' sums: 2.49 against 3.27 ms
     // for the symmetric pass, which forms them anyway, at 100k)
     if (o.ptr[1] != nullptr && use_sym_fwd4(M, all, raw))
-      return use_sym_fwd8(M) ? launch_sym_fwd8<D, true>(a, sc, M, oz, ws, wsb, st, true)
-                             : launch_sym_fwd4<D, true>(a, sc, M, oz, ws, wsb, st, true);
+      return launch_sym_fwd_rows<D, true>(a, sc, M, oz, ws, wsb, st, true);
     if (o.ptr[1] == nullptr)
       return launch_fwd_pk<OpOdeSelfFwdPk<D, true, false, false, true>, OpOdeSelfFwdPk<D, true, false, false, true, true>>(raw, "ode_self_fwd(pk, no mG, zs)", a, sc, nrows,
                                                                            M, oz, ws, wsb, st);
@@ -447,11 +472,8 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
                ? launch_mfma_fwd<D, true>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order)
                : launch_mfma_fwd<D, false>("ode_self_fwd(mfma)", a, sc, nrows, M, o, ws, wsb, st, order);
   if (use_sym_fwd4(M, all, raw)) {  // symmetric pair-once, 4 (or 8) rows per lane
-    if (use_sym_fwd8(M))
-      return o.ptr[2] != nullptr ? launch_sym_fwd8<D, true>(a, sc, M, o, ws, wsb, st, false)
-                                 : launch_sym_fwd8<D, false>(a, sc, M, o, ws, wsb, st, false);
-    return o.ptr[2] != nullptr ? launch_sym_fwd4<D, true>(a, sc, M, o, ws, wsb, st, false)
-                               : launch_sym_fwd4<D, false>(a, sc, M, o, ws, wsb, st, false);
+    return o.ptr[2] != nullptr ? launch_sym_fwd_rows<D, true>(a, sc, M, o, ws, wsb, st, false)
+                               : launch_sym_fwd_rows<D, false>(a, sc, M, o, ws, wsb, st, false);
   }
   if (g_fwd_alg == 2 || g_fwd_alg == 4 || g_fwd_alg == 5 || g_fwd_alg == 6)
     return o.ptr[2] != nullptr
@@ -1044,8 +1066,8 @@ int euler_step_phase_d(int phase, const float* q_loc, const float* p_loc, const 
   Args a0 = {q_loc, p_loc, nullptr, nullptr, q_loc, p_loc, nullptr, nullptr, 0.f};
   Args a1 = {q ? q + row0 * D : nullptr, p ? p + row0 * D : nullptr, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   const bool raw = tl_coord_raw != 0;
-  scale_coords(a0, sc0, sigma);
-  scale_coords(a1, sc1, sigma);
+  scale_coords(a0, sc0, sigma, eta != 0.0);
+  scale_coords(a1, sc1, sigma, eta != 0.0);
   if (raw) {
     raw_coords(a0, sc0);
     raw_coords(a1, sc1);

@@ -34,8 +34,11 @@ constexpr int kSymG = 128;   // points per group (= rows of one wave)
 constexpr int kSymQ = 4;     // row groups (waves) per workgroup
 constexpr int kSymFwd4WgMin = 4096;   // sym_geom wg_min of the symmetric 4-row forward
 constexpr int kSymFwd8WgMin = 2048;   // ... and of the 8-row forward (512-point groups)
+// ... and of the 6-row forward (384-point groups, 3 workgroups per CU): L = 2 at 100k (4306
+// workgroups; 3.185 ms against 3.25 for L = 4, tools/probes/symfwd_L.py)
+constexpr int kSymFwd6WgMin = 4096;
 // rows per lane of the symmetric forward: dicp_set_option "sym_fwd_rows" 4 or 8 forces, 0 =
-// automatic (8 from DICP_SYM_FWD8_MIN_M points)
+// automatic (6 from DICP_SYM_FWD6_MIN_M, 8 from DICP_SYM_FWD8_MIN_M points, lddmm.hip)
 inline int& sym_fwd_rows() {
   static int v = 0;
   return v;
@@ -849,11 +852,13 @@ inline size_t sym_ws_bytes(int64_t M, int W, int nparts = 1) {
   // 8-row forward)
   const SymGeom g = sym_geom(M, nparts), g4 = sym_geom(M, nparts, 256), g4v = sym_geom(M, nparts, 256, 2),
                 g4f = sym_geom(M, nparts, 256, 4, kSymFwd4WgMin),
-                g8f = sym_geom(M, nparts, 512, 4, kSymFwd8WgMin);
+                g8f = sym_geom(M, nparts, 512, 4, kSymFwd8WgMin),
+                g6f = sym_geom(M, nparts, 384, 4, kSymFwd6WgMin);
   int ns = g.nslot > g4.nslot ? g.nslot : g4.nslot;
   ns = g4v.nslot > ns ? g4v.nslot : ns;
   ns = g4f.nslot > ns ? g4f.nslot : ns;
   ns = g8f.nslot > ns ? g8f.nslot : ns;
+  ns = g6f.nslot > ns ? g6f.nslot : ns;
   return (size_t)ns * (size_t)M * (size_t)W * sizeof(float);
 }
 

@@ -968,41 +968,40 @@ struct SymFwdPk4 {
   }
 };
 
-// ---- the symmetric eta = 0 forward with 8 rows per lane (fwd_alg 2 from DICP_SYM_FWD8_MIN_M
-// points; dicp_set_option "sym_fwd_rows" 4 / 8 forces) -- 512-point groups: a lane holds rows
-// r * 64 + l (r = 0..7) of its group as four float2 row pairs, so each column's record, its LDS
-// reads, and the column side's one scalar add + DPP rotation per accumulator serve 8 rows
-// instead of 4 (~19% of the 4-row loop's issue went to that column side).  Per
-// step: 76 v_pk (row side) + 36 v_pk + 9 adds + 9 DPP (column side) + 8 exp for 16 ordered
-// pair-equivalents, against 2 x (56 v_pk + 9 + 9 + 4 exp) for the 4-row form.  Own body (the
-// 4-row sym_pk4_body also runs the tuned VJP, whose schedule must not move); slots and merge
-// as the 4-row form with G = 512.
-#ifndef DICP_SYMFWD8_WPE
-#define DICP_SYMFWD8_WPE 1
-#endif
+// ---- the symmetric eta = 0 forward with 2 NRP rows per lane (NRP = 4: 8 rows, 512-point
+// groups, fwd from DICP_SYM_FWD8_MIN_M points; NRP = 3: 6 rows, 384-point groups; dicp_set_option
+// "sym_fwd_rows" 4 / 6 / 8 forces) -- a lane holds rows r * 64 + l (r < 2 NRP) of its group as
+// NRP float2 row pairs, so each column's record, its LDS reads, and the column side's one scalar
+// add + DPP rotation per accumulator serve 2 NRP rows instead of 4 (~19% of the
+// 4-row loop's issue went to that column side).  8 rows per step: 76 v_pk (row side) + 36 v_pk
+// + 9 adds + 9 DPP (column side) + 8 exp for 16 ordered pair-equivalents, against 2 x (56 v_pk +
+// 9 + 9 + 4 exp) for the 4-row form.  Own body (the 4-row sym_pk4_body also runs the tuned
+// VJP, whose schedule must not move); slots and merge as the 4-row form with G = 128 NRP.
+// 8 rows need 208 VGPRs (2 waves / SIMD, 2 workgroups per CU); 6 rows fit 3 waves / SIMD.
+template <int NRP>
+constexpr int sym_fwd_group() { return 128 * NRP; }
 constexpr int kSymG8 = 512;
-template <int D, bool DIV>
-struct SymFwdPk8 {
+template <int D, bool DIV, int NRP>
+struct SymFwdPkN {
   using P4 = SymFwdPk4<D, DIV>;
   using S = typename P4::S;
   static constexpr int W = S::W;
   using Row2 = typename P4::Row2;
   using Sh = typename P4::Sh;
-  __device__ static void pair_sym8(const Row2* r, const float* rec, f2 (*acc)[W], float* ct) {
+  __device__ static void pair_sym(const Row2* r, const float* rec, f2 (*acc)[W], float* ct) {
     f2 cv[2 * D];
     P4::colvec(rec, cv);
-    // one row pair at a time: its shared terms, row side, and its share of the column side
-    // chained into the column partials (the same h = 0..3 order as summing them afterwards),
-    // so only one pair's temporaries are live (168 VGPRs: 3 waves / SIMD)
+    // per row pair: its shared terms, row side, and its share of the column side chained into
+    // the column partials in row-pair order
     f2 cV[D], cG[D], cZ[D];
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
+    for (int h = 0; h < NRP; ++h) {
       Sh t;
       P4::shared(r[h], cv, t);
       P4::row_side(t, cv, acc[h]);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        // column j's side over the 8 rows; (i, j) -> (j, i) flips z
+        // column j's side over the 2 NRP rows; (i, j) -> (j, i) flips z
         cV[d] = h == 0 ? t.K * r[h].p[d] : pk_fma(t.K, r[h].p[d], cV[d]);
         cG[d] = h == 0 ? t.Kpp * t.z[d] : pk_fma(t.Kpp, t.z[d], cG[d]);
         if (DIV) cZ[d] = h == 0 ? t.K * t.z[d] : pk_fma(t.K, t.z[d], cZ[d]);
@@ -1020,17 +1019,20 @@ struct SymFwdPk8 {
   }
 };
 
-template <int D, bool DIV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD8_WPE, 4))) void sym_fwd_pk8_kernel(
+#ifndef DICP_SYMFWD8_WPE
+#define DICP_SYMFWD8_WPE 1
+#endif
+template <int D, bool DIV, int NRP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRP == 4 ? DICP_SYMFWD8_WPE : 3, 4))) void sym_fwd_pkn_kernel(
     Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride) {
-  using P = SymFwdPk8<D, DIV>;
+  using P = SymFwdPkN<D, DIV, NRP>;
   using P4 = SymFwdPk4<D, DIV>;
   using S = typename P::S;
   using LY = rec_layout<P4>;
-  constexpr int G = kSymG8;
+  constexpr int G = sym_fwd_group<NRP>(), NR = 2 * NRP;
   constexpr int CW = S::CW, NP = LY::kPlanes, W = P::W;
   __shared__ float4 planes[2][NP][G];
-  __shared__ float colacc[kSymQ][64][W];    // one 64-column quarter of a group at a time
+  __shared__ float colacc[kSymQ][64][W];    // one 64-column slice of a group at a time
 
   const int Q = (int)blockIdx.y, kc = (int)blockIdx.x;
   const int B0 = kSymQ * Q + kc * L;
@@ -1039,31 +1041,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
   const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
   const int A = kSymQ * Q + wv;
 
-  typename P::Row2 row[4];
+  typename P::Row2 row[NRP];
   // row r of the lane: A * G + r * 64 + l (recomputed at the stores: no index registers live
   // across the pair loop)
   const int64_t rbase = (int64_t)A * G + l;
   {
-    typename S::Row r8[8];
+    typename S::Row rr[NR];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int64_t ri = rbase + r * 64;
       const bool rv = A < nG && ri < M;
-      S::load_row(a, sc, rv ? ri : 0, rv, r8[r]);
+      S::load_row(a, sc, rv ? ri : 0, rv, rr[r]);
     }
 #pragma unroll
-    for (int h = 0; h < 4; ++h) P4::pack(r8[2 * h], r8[2 * h + 1], row[h]);
+    for (int h = 0; h < NRP; ++h) P4::pack(rr[2 * h], rr[2 * h + 1], row[h]);
   }
-  f2 racc[4][W];
+  f2 racc[NRP][W];
 #pragma unroll
-  for (int h = 0; h < 4; ++h)
+  for (int h = 0; h < NRP; ++h)
 #pragma unroll
     for (int k = 0; k < W; ++k) racc[h][k] = splat(0.f);
 
   auto stage = [&](int B, int buf) {
 #pragma unroll
-    for (int u = 0; u < G / 256; ++u) {
+    for (int u = 0; u < (G + 255) / 256; ++u) {
       const int c = u * 256 + tid;
+      if (G % 256 != 0 && c >= G) break;
       const int64_t j = (int64_t)B * G + c;
       float rec[4 * CW], ph[4 * NP];
       S::load_col(a, sc, j < M ? j : 0, j < M, rec);
@@ -1100,7 +1103,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
     const bool sym = A < B;          // wave-uniform
     const bool diag = A == B;
 #pragma unroll 1
-    for (int h = 0; h < G / 64; ++h) {   // 64-column quarters of the group
+    for (int h = 0; h < G / 64; ++h) {   // 64-column slices of the group
       {
         float cacc[W];
 #pragma unroll
@@ -1112,7 +1115,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
             float rec[4 * CW + NP];
             ldrec(col, rec);
             float ct[W];
-            P::pair_sym8(row, rec, racc, ct);
+            P::pair_sym(row, rec, racc, ct);
 #pragma unroll
             for (int k = 0; k < W; ++k) cacc[k] = rol1(cacc[k]) + ct[k];
           }
@@ -1125,7 +1128,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
             float rec[4 * CW + NP];
             ldrec(col, rec);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) P::pair_row(row[r], rec, racc[r]);
+            for (int r = 0; r < NRP; ++r) P::pair_row(row[r], rec, racc[r]);
           }
         }
 #pragma unroll
@@ -1133,7 +1136,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
       }
       __syncthreads();
       {
-        // the quarter's 64 column sums of the 4 waves, added in wave order (contiguous stores)
+        // the slice's 64 column sums of the 4 waves, added in wave order (contiguous stores)
         const int64_t j0 = (int64_t)B * G + h * 64;
         float* dst = slab + (int64_t)Q * slot_stride + j0 * W;
         for (int e = tid; e < 64 * W; e += 256) {
@@ -1146,7 +1149,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
     buf ^= 1;
   }
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int r = 0; r < NR; ++r) {
     const int64_t ri = rbase + r * 64;
     if (!(A < nG && ri < M)) continue;
     float* dst = slab + (int64_t)(Q + 1 + kc) * slot_stride + ri * W;
@@ -1157,35 +1160,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DICP_SYMFWD
 }
 
 // zs: the divergence rows out through the h slot (o.ptr[3], M x D), DIV required; the
-// launcher of the 4-row form's contract (launch_sym_fwd4)
-template <int D, bool DIV>
-int launch_sym_fwd8(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+// launcher of the 4-row form's contract (launch_sym_fwd4); NRP row pairs per lane
+template <int D, bool DIV, int NRP = 4>
+int launch_sym_fwdn(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
                     hipStream_t st, bool zs) {
   using S = SymFwd<D, DIV>;
+  constexpr int G = sym_fwd_group<NRP>();
   if (M <= 0) return DICP_OK;
-  if (int rc = no_batch("ode_self_fwd(sym8)")) return rc;
-  const SymGeom g = sym_geom(M, 1, kSymG8, 4, kSymFwd8WgMin);
+  if (int rc = no_batch("ode_self_fwd(sym6/8)")) return rc;
+  const SymGeom g = sym_geom(M, 1, G, 4, NRP == 4 ? kSymFwd8WgMin : kSymFwd6WgMin);
   const size_t need = sym_ws_bytes(M, S::W);
   if (ws == nullptr || wsb < need) {
-    set_error("ode_self_fwd(sym8): workspace too small (%zu < %zu bytes)", wsb, need);
+    set_error("ode_self_fwd(sym6/8): workspace too small (%zu < %zu bytes)", wsb, need);
     return DICP_ERR_WORKSPACE;
   }
   if (o.ptr[0] == nullptr || (zs && (!DIV || o.ptr[3] == nullptr))) {
-    set_error("ode_self_fwd(sym8): v is required, zs needs the divergence sums");
+    set_error("ode_self_fwd(sym6/8): v is required, zs needs the divergence sums");
     return DICP_ERR_INVALID;
   }
   float* slab = reinterpret_cast<float*>(ws);
   const int64_t stride = M * S::W;
   const dim3 grid((unsigned)g.Kmax, (unsigned)g.nQ), mg((unsigned)((M + 255) / 256));
   const float ia = 1.f / a.scale;
-  sym_fwd_pk8_kernel<D, DIV><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride);
-  int rc = check_launch("ode_self_fwd(sym8)");
+  sym_fwd_pkn_kernel<D, DIV, NRP><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride);
+  int rc = check_launch("ode_self_fwd(sym6/8)");
   if (rc) return rc;
   if (zs)
-    sym_fwd4_merge_kernel<D, DIV, true, kSymG8><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
+    sym_fwd4_merge_kernel<D, DIV, true, G><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
   else
-    sym_fwd4_merge_kernel<D, DIV, false, kSymG8><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
-  return check_launch("ode_self_fwd(sym8 merge)");
+    sym_fwd4_merge_kernel<D, DIV, false, G><<<mg, dim3(256), 0, st>>>(slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o);
+  return check_launch("ode_self_fwd(sym6/8 merge)");
+}
+template <int D, bool DIV>
+int launch_sym_fwd8(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                    hipStream_t st, bool zs) {
+  return launch_sym_fwdn<D, DIV, 4>(a, sc, M, o, ws, wsb, st, zs);
+}
+template <int D, bool DIV>
+int launch_sym_fwd6(const Args& a, const Scal& sc, int64_t M, const Outs& o, void* ws, size_t wsb,
+                    hipStream_t st, bool zs) {
+  return launch_sym_fwdn<D, DIV, 3>(a, sc, M, o, ws, wsb, st, zs);
 }
 
 template <int D, bool DIV>

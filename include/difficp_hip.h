@@ -407,13 +407,16 @@ int dicp_supports_dim(int D);
  *                  centred expansion applies -- "red_alg" -- i.e. from 50k x 50k), 2 always
  *                  (x == y only)
  *   "sym_red_rows" rows per lane of the pair-once sums: 0 automatic (4), 4 or 8 forced
- *   "sym_fwd_rows" rows per lane of the symmetric eta = 0 forward: 0 automatic (8 from 110k
- *                  points alone on the chip, else 4), 4 or 8 forced
+ *   "sym_fwd_rows" rows per lane of the symmetric eta = 0 forward: 0 automatic (6 from 40k, 8 from 180k
+ *                  points alone on the chip, else 4), 4, 6 or 8 forced
  *   "lse_pk"       GMM E / M passes: 1 rows packed in float2 pairs (v_pk_fma_f32, default),
  *                  0 scalar rows (bitwise equal)
  *   "lse_adapt"    GMM E / M passes: tiles with a tile-end re-reference (anywhere in the
  *                  workgroup) before the rest of the chunk tests per pair; 0 per pair from the
  *                  start (default 1; env DICP_LSE_ADAPT)
+ *   "lse_bound"    GMM E-step against >= 8192 components: 1 (default; env DICP_LSE_BOUND) the
+ *                  shift min(hint - 8, max_c w2_c - 8), which no logit can overflow, and rows
+ *                  whose LSE ends > 80 below it summed again exactly; 0 the sampled shift
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
  *   "mfma_rmax_x100"  matrix-core forward (fwd_alg 3): largest workgroup row spread (scaled
  *                  units x 100) that takes the MFMA branch; >= 100000 always, 0 never (default 300)

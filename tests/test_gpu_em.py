@@ -9,7 +9,9 @@ csrc/gmm.hip kLseSlack; both modes forced in test_estep_reref_modes).
     components of the other cluster;
   * the wave-per-row merge of many column chunks (the M-step at the atlas shape);
   * small sigma against the sample's spacing (events in most tiles), with and without the
-    shift hint (exact, and 300 too high: the chunk partials' normalised store).
+    shift hint (exact, and 300 too high: the chunk partials' normalised store);
+  * the many-component E-step's bound shift (no sample, no events) and the exact re-sum of the
+    rows whose LSE ends far below it (rows 30 sigma from every component, stale hints).
 
 Criterion: err vs the float64 oracle (oracle/torch_ref.py em_step, pinned by the
 reference's EM goldens) <= max(2e-5, 2 x the float32 oracle's own deviation)."""
@@ -177,6 +179,42 @@ def test_estep_reref_modes(dev, adapt, hinted):
     finally:
         _lib.set_option("lse_adapt", old)
 
+
+
+@pytest.mark.parametrize("bound", [1, 0])
+def test_estep_bound_shift_fixup(dev, bound):
+    """The many-component E-step's bound shift (csrc/gmm.hip lse_bound_kernel, option
+    lse_bound): half of the rows lie 30 sigma from every component (their LSE ends far below
+    the shift: listed and summed again exactly by lse_fixup_kernel), and hints exact, 100 too
+    high (a shift 92 above the LSE: listed) and 300 too high (capped at the bound) -- every
+    output against float64 rows, with the bound shift on and off."""
+    from difficp_amd import _lib
+    g = torch.Generator().manual_seed(21)
+    N, C, D, sigma = 1000, 20000, 3, 0.01
+    X = torch.rand(N, D, generator=g, dtype=torch.float64)
+    X[N // 2:, 0] += 1.3
+    X = X.float().double()
+    mu = torch.rand(C, D, generator=g, dtype=torch.float64).float().double()
+    w = 0.3 * torch.randn(C, generator=g, dtype=torch.float64)
+    lpi = w - w.logsumexp(0)
+    T64, T264, st64, lgn = _estep64(X, mu, lpi, sigma)
+    # the float32 restatement's own deviation (the far rows' entropy sums cancel more)
+    _, _, st32, _ = _estep64(X.float(), mu.float(), lpi.float(), sigma)
+    f = lambda t: t.float().to(dev).contiguous()
+    old = _lib.get_option("lse_bound")
+    try:
+        _lib.set_option("lse_bound", bound)
+        for hint in (None, f(T264), f(T264 + 100.0), f(T264 + 300.0)):
+            T, T2, st = _lib.gmm_estep(f(X), f(mu), f(lpi / math.log(2)), f((mu * mu).sum(-1)), sigma,
+                                       lgn, True, hint=hint)
+            T, T2, st = T.cpu().double(), T2.cpu().double(), st.cpu().double()
+            assert rel_err(T, T64) < 1e-5 and rel_err(T2, T264) < 1e-5
+            for k in range(D + 4):
+                assert torch.isfinite(st[:, k]).all(), k
+                tol = max(2e-5 if k >= D else 1e-5, 2 * rel_err(st32[:, k].double(), st64[:, k]))
+                assert rel_err(st[:, k], st64[:, k]) < tol, (k, rel_err(st[:, k], st64[:, k]), tol)
+    finally:
+        _lib.set_option("lse_bound", old)
 
 
 def test_em_hint_history_independent(dev):

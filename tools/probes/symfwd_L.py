@@ -24,7 +24,9 @@ for M in Ms:
     zs = torch.empty_like(q)
     fn = lambda: _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs)
     reps = max(3, int(3e10 / (M * M)))
-    cfgs = [(4, L) for L in (0, 1, 2, 3, 4, 5, 6, 8)] + [(8, L) for L in (0, 1, 2, 3)]
+    cfgs = [(4, L) for L in (0, 2, 4)] + [(6, L) for L in (0, 1, 2, 3, 4)] + [(8, L) for L in (1, 2)]
+    if os.environ.get("SYMFWD_CFGS"):   # e.g. "4:0,6:0,8:0" (rows:L)
+        cfgs = [tuple(int(v) for v in c.split(":")) for c in os.environ["SYMFWD_CFGS"].split(",")]
     best = {}
     for _ in range(3):
         for rows, L in cfgs:
