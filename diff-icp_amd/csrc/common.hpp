@@ -75,10 +75,6 @@ struct Args {
   // result in exact arithmetic; it keeps |q'| at the cloud's extent over sigma whatever the
   // offset of the coordinates, so the rounding of q' does not grow with that offset.
   const float* shift;
-  // alpha - scale (the float scale's rounding error), set by the eta != 0 forward launchers:
-  // ld_coord then forms q' = alpha (q - shift) with the exact alpha in double, so the exponent
-  // -|q'_i - q'_j|^2 carries no systematic scale error (packed.hpp EtaConsts); 0: float scale
-  float scale_lo;
 };
 
 template <int D>
@@ -91,12 +87,6 @@ template <int D>
 __device__ __forceinline__ void ld_coord(const Args& a, const float* __restrict__ p, int64_t i, float* dst) {
   float c[D];
   load_shift<D>(a, c);
-  if (a.scale_lo != 0.f) {   // wave-uniform; a row / column load, not the pair loop
-    const double al = (double)a.scale + (double)a.scale_lo;
-#pragma unroll
-    for (int d = 0; d < D; ++d) dst[d] = (float)(al * ((double)p[i * D + d] - (double)c[d]));
-    return;
-  }
 #pragma unroll
   for (int d = 0; d < D; ++d) dst[d] = a.scale * (p[i * D + d] - c[d]);
 }

@@ -115,12 +115,9 @@ bool supported_dim(int D) { return D == 2 || D == 3; }
 // aux1 = s / alpha.
 // The coordinate origin is the first column point (a.c0: the support q of the self ops, the
 // support of the external-point x pass, y of KRed), the same for rows and columns.
-// exact (the eta != 0 forward): Args::scale_lo = alpha - scale, so the coordinates carry the
-// exact alpha (common.hpp ld_coord) and the exponent needs no correction (packed.hpp EtaConsts)
-void scale_coords(Args& a, Scal& sc, double sigma, bool exact = false) {
+void scale_coords(Args& a, Scal& sc, double sigma) {
   const double alpha = std::sqrt(1.4426950408889634 / (2.0 * sigma * sigma));
   a.scale = (float)alpha;
-  a.scale_lo = exact ? (float)(alpha - (double)a.scale) : 0.f;
   a.shift = a.c0;
   sc.aux1 = (float)(1.0 / (sigma * sigma) / alpha);
 }
@@ -128,7 +125,6 @@ void scale_coords(Args& a, Scal& sc, double sigma, bool exact = false) {
 // original-unit coordinates for the RAW packed kernels: alpha = 1, no shift, aux1 = s / 1
 void raw_coords(Args& a, Scal& sc) {
   a.scale = 1.f;
-  a.scale_lo = 0.f;
   a.shift = nullptr;
   sc.aux1 = sc.s;
 }
@@ -429,7 +425,7 @@ int ode_self_fwd_d(const float* q, const float* p, int64_t M, double sigma, doub
   const bool all = row0 == 0 && nrows == M;
   Args a = {q + row0 * D, p + row0 * D, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   Scal sc = make_scal(sigma, eta);
-  scale_coords(a, sc, sigma, eta != 0.0);
+  scale_coords(a, sc, sigma);
   const bool raw = tl_coord_raw != 0;   // the packed kernels below; the others stay scaled
   if (zs != nullptr) {
     // divergence rows out through the (unused) h slot: the packed passes only
@@ -1066,8 +1062,8 @@ int euler_step_phase_d(int phase, const float* q_loc, const float* p_loc, const 
   Args a0 = {q_loc, p_loc, nullptr, nullptr, q_loc, p_loc, nullptr, nullptr, 0.f};
   Args a1 = {q ? q + row0 * D : nullptr, p ? p + row0 * D : nullptr, nullptr, nullptr, q, p, nullptr, nullptr, 0.f};
   const bool raw = tl_coord_raw != 0;
-  scale_coords(a0, sc0, sigma, eta != 0.0);
-  scale_coords(a1, sc1, sigma, eta != 0.0);
+  scale_coords(a0, sc0, sigma);
+  scale_coords(a1, sc1, sigma);
   if (raw) {
     raw_coords(a0, sc0);
     raw_coords(a1, sc1);

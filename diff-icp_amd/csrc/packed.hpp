@@ -41,12 +41,10 @@ inline void split_hi_lo(double x, float* hl) {
   hl[1] = (float)(x - (double)hl[0]);
 }
 
-inline EtaConsts eta_consts(const Args& args, bool raw) {
+inline EtaConsts eta_consts(float scale, bool raw) {
   const double sg = tl_launch_sigma, eta = tl_launch_eta;
   const double s = 1.0 / (sg * sg);
-  // the scale the coordinates carry: the exact alpha where the launcher set Args::scale_lo
-  // (then e1 = 0 up to double rounding and the scaled kernel's exponent is plain -r2)
-  const double a = raw ? 1.0 : (double)args.scale + (double)args.scale_lo;
+  const double a = raw ? 1.0 : (double)scale;
   const double nc = -1.4426950408889634 * 0.5 * s;   // K = exp2(nc |z|^2)
   EtaConsts c;
   if (raw) {
@@ -109,7 +107,7 @@ struct OpOdeSelfFwdPk {
   // eta != 0: the launch constants of the model's cancelling sums (EtaConsts)
   static constexpr bool kConsts = ETA;
   using Consts = EtaConsts;
-  static EtaConsts make_consts(const Args& a) { return eta_consts(a, RAW); }
+  static EtaConsts make_consts(const Args& a) { return eta_consts(a.scale, RAW); }
   // LDS column record of the packed pair: D = 3 as [q (3) | q_z | p (3) | p_z], so that the
   // z components are the aligned register pairs (.z, .w) of one ds_read_b128 each instead of
   // broadcasts, which the register allocator materialises with a v_mov per column (the x / y
@@ -217,8 +215,8 @@ struct OpOdeSelfFwdPk {
       r2 = pk_fma(z[d], z[d], r2);
     }
     f2 K;
-    if constexpr (ETA && RAW) {   // the exponent nc r2 with nc as hi + lo (EtaConsts)
-      const f2 e = pk_fma(r2, r.nc, r.e0 * r2);
+    if constexpr (ETA) {   // the exponent of the exact alpha (EtaConsts): one packed FMA more
+      const f2 e = RAW ? pk_fma(r2, r.nc, r.e0 * r2) : pk_fma(r2, r.nc, -r2);
       K = f2{fast_exp2(e.x), fast_exp2(e.y)};
     } else if constexpr (RAW) {
       const f2 e = r.nc * r2;
@@ -469,9 +467,9 @@ struct op_f64<T, std::enable_if_t<T::kF64>> : std::true_type {};
 #endif
 // rowred_pk_body for Op::kF64 ops (with launch constants): the pair loop as rowred_pk_body, but
 // every DICP_PK_F64_SUB columns the float sums of the channels Op::f64_acc are added into double
-// totals (one conversion + one double add per channel and row per sub-tile), the other
-// channels keep one float partial per 256-column tile; Op::store_d forms the outputs in
-// double, and split partials are stored as double (slab width doubled; merge_slabs_f64_kernel).  tools/probes/logdet_cost_diag.py accum_main:
+// totals (one conversion + one double add per channel and row per sub-tile: ~1% of the pair
+// work at 32), Op::store_d forms the outputs in double, and split partials are stored as double
+// (slab width doubled; merge_slabs_f64_kernel).  tools/probes/logdet_cost_diag.py accum_main:
 // float sums over 256-column tiles leave a systematic velocity error that the logdet model's
 // cost integrates; 32-column float sub-tiles with double totals remove most of it.
 template <class Op, int RP, bool WRAP = false>
@@ -537,15 +535,13 @@ __device__ __forceinline__ void rowred_pk_body_f64(Args args, Scal sc, int64_t M
             make_float4(pre[4 * k], pre[4 * k + 1], pre[4 * k + 2], pre[4 * k + 3]);
     }
     const float4* tile = lds[buf];
-    // the float channels: one partial per tile (two-level, as rowred_pk_body); the double
-    // channels: one float partial per sub-tile, flushed into the double totals
-    f2 acc[RP][NACC];
-#pragma unroll
-    for (int h = 0; h < RP; ++h)
-#pragma unroll
-      for (int k = 0; k < NACC; ++k) acc[h][k] = splat(0.f);
     for (int t0 = 0; t0 < cnt; t0 += kSub) {
       const int t1 = t0 + kSub < cnt ? t0 + kSub : cnt;
+      f2 acc[RP][NACC];
+#pragma unroll
+      for (int h = 0; h < RP; ++h)
+#pragma unroll
+        for (int k = 0; k < NACC; ++k) acc[h][k] = splat(0.f);
 #pragma unroll DICP_PK_PAIR_UNROLL
       for (int t = t0; t < t1; ++t) {
         float rec[CW4 * 4];
@@ -567,15 +563,11 @@ __device__ __forceinline__ void rowred_pk_body_f64(Args args, Scal sc, int64_t M
           if (Op::f64_acc(k)) {
             td[h][0][k] += (double)acc[h][k].x;
             td[h][1][k] += (double)acc[h][k].y;
-            acc[h][k] = splat(0.f);
+          } else {
+            tot[h][k] = tot[h][k] + acc[h][k];
           }
         }
     }
-#pragma unroll
-    for (int h = 0; h < RP; ++h)
-#pragma unroll
-      for (int k = 0; k < NACC; ++k)
-        if (!Op::f64_acc(k)) tot[h][k] = tot[h][k] + acc[h][k];
     __syncthreads();
     buf ^= 1;
     cnt = cntn;
