@@ -382,7 +382,8 @@ bool use_sym_fwd4(int64_t M, bool all, bool raw) {
 }
 
 // rows per lane of the symmetric forward (SymFwdPkN) when the pass runs alone on the chip
-// (batch_share 1, not inside a lockstep batch): 6 (384-point groups, 3 waves / SIMD) from
+// (batch_share 1; a lockstep batch takes each frame's own rule, so a batched call equals the
+// call made alone bitwise): 6 (384-point groups, 3 waves / SIMD) from
 // DICP_SYM_FWD6_MIN_M points, 8 (512-point groups, 2 waves / SIMD) from DICP_SYM_FWD8_MIN_M,
 // else 4; sym_fwd_rows 4 / 6 / 8 forces.  Measured r06 (tools/probes/symfwd_L.py, the Euler
 // step with divergence rows, profiles/r06_symfwd_rows.jsonl): 6 rows against 4 -2% at 40k,
@@ -396,7 +397,6 @@ bool use_sym_fwd4(int64_t M, bool all, bool raw) {
 #define DICP_SYM_FWD8_MIN_M 180000
 #endif
 int sym_fwd_rows_for(int64_t M) {
-  if (batching()) return 4;
   const int f = sym_fwd_rows();
   if (f == 4 || f == 6 || f == 8) return f;
   if (batch_share() > 1) return 4;

@@ -991,15 +991,15 @@ struct SymFwdMergeEntry {
   Outs o;
   unsigned gx, gy;
 };
-template <int D, bool DIV, bool ZS>
+template <int D, bool DIV, bool ZS, int G = 256>
 __global__ __launch_bounds__(256) void sym_fwd4_merge_batch_kernel(BatchTab<SymFwdMergeEntry> t) {
   const SymFwdMergeEntry& e = t.e[blockIdx.z];
   if (blockIdx.x >= e.gx) return;
-  sym_fwd4_merge_body<D, DIV, ZS>(e.slab, e.slot_stride, e.M, e.nG, e.L, e.p, e.sa, e.ia, e.o, blockIdx.x);
+  sym_fwd4_merge_body<D, DIV, ZS, G>(e.slab, e.slot_stride, e.M, e.nG, e.L, e.p, e.sa, e.ia, e.o, blockIdx.x);
 }
-template <int D, bool DIV, bool ZS>
+template <int D, bool DIV, bool ZS, int G = 256>
 int sym_fwd4_merge_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
-  return batch_launch<SymFwdMergeEntry>(sym_fwd4_merge_batch_kernel<D, DIV, ZS>, es, st, "sym_fwd4_merge");
+  return batch_launch<SymFwdMergeEntry>(sym_fwd4_merge_batch_kernel<D, DIV, ZS, G>, es, st, "sym_fwd4_merge");
 }
 
 template <int D, bool DIV>

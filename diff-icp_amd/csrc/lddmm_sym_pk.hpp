@@ -1023,8 +1023,9 @@ struct SymFwdPkN {
 #define DICP_SYMFWD8_WPE 1
 #endif
 template <int D, bool DIV, int NRP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRP == 4 ? DICP_SYMFWD8_WPE : 3, 4))) void sym_fwd_pkn_kernel(
-    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride) {
+__device__ __forceinline__ void sym_fwd_pkn_body(const Args& a, const Scal& sc, int64_t M, int nG, int L,
+                                                 float* __restrict__ slab, int64_t slot_stride, unsigned bx,
+                                                 unsigned by) {
   using P = SymFwdPkN<D, DIV, NRP>;
   using P4 = SymFwdPk4<D, DIV>;
   using S = typename P::S;
@@ -1034,7 +1035,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRP == 4 ? 
   __shared__ float4 planes[2][NP][G];
   __shared__ float colacc[kSymQ][64][W];    // one 64-column slice of a group at a time
 
-  const int Q = (int)blockIdx.y, kc = (int)blockIdx.x;
+  const int Q = (int)by, kc = (int)bx;
   const int B0 = kSymQ * Q + kc * L;
   if (B0 >= nG) return;  // uniform for the whole workgroup, before any barrier
   const int B1 = min(B0 + L, nG);
@@ -1159,6 +1160,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRP == 4 ? 
   }
 }
 
+template <int D, bool DIV, int NRP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRP == 4 ? DICP_SYMFWD8_WPE : 3, 4))) void sym_fwd_pkn_kernel(
+    Args a, Scal sc, int64_t M, int nG, int L, float* __restrict__ slab, int64_t slot_stride) {
+  sym_fwd_pkn_body<D, DIV, NRP>(a, sc, M, nG, L, slab, slot_stride, blockIdx.x, blockIdx.y);
+}
+// one grid over the frames of a lockstep launch batch (batch.hpp), as sym_fwd_pk4_batch_kernel
+template <int D, bool DIV, int NRP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NRP == 4 ? DICP_SYMFWD8_WPE : 3, 4))) void sym_fwd_pkn_batch_kernel(
+    BatchTab<SymEntry> t) {
+  const SymEntry& e = t.e[blockIdx.z];
+  if (blockIdx.x >= e.gx || blockIdx.y >= e.gy) return;
+  sym_fwd_pkn_body<D, DIV, NRP>(e.a, e.sc, e.M, e.nG, e.L, e.slab, e.slot_stride, blockIdx.x, blockIdx.y);
+}
+template <int D, bool DIV, int NRP>
+int sym_fwd_pkn_batch_flush(const std::vector<const void*>& es, hipStream_t st) {
+  return batch_launch<SymEntry>(sym_fwd_pkn_batch_kernel<D, DIV, NRP>, es, st, "sym_fwd_pkn");
+}
+
 // zs: the divergence rows out through the h slot (o.ptr[3], M x D), DIV required; the
 // launcher of the 4-row form's contract (launch_sym_fwd4); NRP row pairs per lane
 template <int D, bool DIV, int NRP = 4>
@@ -1167,7 +1186,6 @@ int launch_sym_fwdn(const Args& a, const Scal& sc, int64_t M, const Outs& o, voi
   using S = SymFwd<D, DIV>;
   constexpr int G = sym_fwd_group<NRP>();
   if (M <= 0) return DICP_OK;
-  if (int rc = no_batch("ode_self_fwd(sym6/8)")) return rc;
   const SymGeom g = sym_geom(M, 1, G, 4, NRP == 4 ? kSymFwd8WgMin : kSymFwd6WgMin);
   const size_t need = sym_ws_bytes(M, S::W);
   if (ws == nullptr || wsb < need) {
@@ -1182,6 +1200,16 @@ int launch_sym_fwdn(const Args& a, const Scal& sc, int64_t M, const Outs& o, voi
   const int64_t stride = M * S::W;
   const dim3 grid((unsigned)g.Kmax, (unsigned)g.nQ), mg((unsigned)((M + 255) / 256));
   const float ia = 1.f / a.scale;
+  if (batching()) {
+    int rc = batch_record(sym_fwd_pkn_batch_flush<D, DIV, NRP>,
+                          SymEntry{a, sc, M, g.nG, g.L, slab, stride, 0, 1, grid.x, grid.y});
+    if (!rc) rc = check_launch("ode_self_fwd(sym6/8)");
+    if (rc) return rc;
+    const SymFwdMergeEntry e{slab, stride, M, g.nG, g.L, a.r1, sc.aux1, ia, o, mg.x, 1u};
+    rc = zs ? batch_record(sym_fwd4_merge_batch_flush<D, DIV, true, G>, e)
+            : batch_record(sym_fwd4_merge_batch_flush<D, DIV, false, G>, e);
+    return rc ? rc : check_launch("ode_self_fwd(sym6/8 merge)");
+  }
   sym_fwd_pkn_kernel<D, DIV, NRP><<<grid, dim3(256), 0, st>>>(a, sc, M, g.nG, g.L, slab, stride);
   int rc = check_launch("ode_self_fwd(sym6/8)");
   if (rc) return rc;

@@ -15,13 +15,18 @@ import json
 import os
 import sys
 
-NAMES = {"sym_fwd_pk8_kernel": "ode_self_fwd_sym8", "scx_kernel": "sym_centred_reduction",
+# first match wins: the specific kernel names before the op names they are templated on
+NAMES = {"lse_bound_kernel": "gmm_estep_bound", "lse_fixup_kernel": "gmm_estep_fixup",
+         "lse_finalize": "lse_finalize",
+         "sym_fwd_pkn_kernelILi3ELb1ELi3": "ode_self_fwd_sym6", "sym_fwd_pkn_kernelILi3ELb1ELi4": "ode_self_fwd_sym8",
+         "sym_fwd_pkn_kernel": "ode_self_fwd_symN",
+         "sym_fwd_pk8_kernel": "ode_self_fwd_sym8", "scx_kernel": "sym_centred_reduction",
          "scx_merge": "sym_centred_merge", "sym_fwd_pk_kernel": "ode_self_fwd_sym", "sym_fwd_kernel": "ode_self_fwd_sym",
          "sym_fwd_pk4_kernel": "ode_self_fwd_sym4", "sym_fwd4_merge": "sym_fwd_merge",
          "sym_bwd_pk4_kernel": "ode_self_bwd", "sym_bwd_pk_kernel": "ode_self_bwd", "sym_bwd_kernel": "ode_self_bwd", "sym_merge_kernel": "sym_merge",
          "OpOdeSelfBwd": "ode_self_bwd_ordered", "OpOdeSelfFwd": "ode_self_fwd",
          "OpGmmE": "gmm_estep", "OpGmmM": "gmm_mstep", "OpGmmTargets": "gmm_targets",
-         "merge_slabs": "merge_slabs", "lse_finalize": "lse_finalize",
+         "merge_slabs": "merge_slabs",
          "cx_kernel": "centred_reduction"}
 
 
