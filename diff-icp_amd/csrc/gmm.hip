@@ -95,12 +95,12 @@ __device__ __forceinline__ bool lse_hint_clamped(float m64, float hint) {
   return hint > -1e30f && hint < 1e30f && hint - 8.f > m64 + 100.f;
 }
 
-// ---- the bound shift (the many-component E-step: C >= kLseE4MinCols) -----------------------
+// ---- the bound shift (the hinted many-component E-step: C >= kLseE4MinCols) ----------------
 // Every logit is at most its column's distance-0 value, t_nc <= nc v_c = w2_c, so the shift
-// U = max_c nc v_c - kLseBoundSlack (a tiny pass over the C columns, lse_bound_kernel) can never
-// overflow a sum: no logit-only sample pass and no re-reference events, whatever sigma (a
-// 64-column sample sits hundreds of log2 units below a row's nearest component at the two-set
-// bench's converged sigma).  With a hint the shift is min(hint - 8, U).  The price
+// min(hint - 8, U) with U = max_c nc v_c - kLseBoundSlack (a tiny pass over the C columns,
+// lse_bound_kernel) can never overflow a sum: no logit-only sample pass and no re-reference
+// events, whatever sigma (a 64-column sample sits hundreds of log2 units below a row's nearest
+// component at the two-set bench's converged sigma).  The price
 // is underflow where a row's LSE lies far below its shift (nearest component beyond ~11 sigma,
 // or a stale-high hint): terms more than 126 below the shift flush to 0, so a row whose LSE
 // ends more than kLseBoundGap below its shift is appended to a list (the finalize) and summed
@@ -802,6 +802,7 @@ struct OpGmmE {
   __device__ static float col_bound(const Scal& sc, const float* rec) { return sc.nc * rec[D]; }
   // per-row shift hint (dicp_gmm_estep_hint_f32): Args::r1, or NULL
   __device__ static const float* hint(const Args& a) { return a.r1; }
+  static const float* hint_host(const Args& a) { return a.r1; }
   __device__ static float uni_value(const Args& a, const Scal& sc, int64_t j) {
     return fminf(a.c1[j] * sc.aux1, fminf(kLseDead * sc.aux1, 1e37f));
   }
@@ -1027,7 +1028,11 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
   int* fix = nullptr;
   Args ab = a;
   if constexpr (lse_bound_op<Op, R>()) {
-    if (lse_bound_ref() != 0 && N > 0) {   // {U, count, -, -, rows} after the partials
+    // hinted calls only: unhinted, the bound sits up to ~nc d^2 above a row's largest logit and
+    // the shifted logits t - m then carry that much absolute rounding into the sums e (t - m)
+    // (the sigma update's sum gamma D^2 measured 3e-6 off the sampled shift's on the exact
+    // two-set workload); with a hint the shift is within ~8 + log2 C of the row's maximum
+    if (lse_bound_ref() != 0 && N > 0 && Op::hint_host(a) != nullptr) {   // {U, count, -, -, rows}
       fix = reinterpret_cast<int*>(part + (size_t)S * (size_t)M * (size_t)(2 + Op::NACC));
       lse_bound_kernel<Op><<<dim3(1), dim3(kBlock), 0, st>>>(a, sc, N, fix);
       ab.r2 = reinterpret_cast<const float*>(fix);

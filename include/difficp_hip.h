@@ -414,9 +414,10 @@ int dicp_supports_dim(int D);
  *   "lse_adapt"    GMM E / M passes: tiles with a tile-end re-reference (anywhere in the
  *                  workgroup) before the rest of the chunk tests per pair; 0 per pair from the
  *                  start (default 1; env DICP_LSE_ADAPT)
- *   "lse_bound"    GMM E-step against >= 8192 components: 1 (default; env DICP_LSE_BOUND) the
- *                  shift min(hint - 8, max_c w2_c - 8), which no logit can overflow, and rows
- *                  whose LSE ends > 80 below it summed again exactly; 0 the sampled shift
+ *   "lse_bound"    hinted GMM E-step against >= 8192 components: 1 (default; env
+ *                  DICP_LSE_BOUND) the shift min(hint - 8, max_c w2_c - 8), which no logit can
+ *                  overflow, and rows whose LSE ends > 80 below it summed again exactly; 0 the
+ *                  sampled shift (unhinted calls always take the sampled shift)
  *   "cx_rho_x100"  centred expansion: largest compact sub-tile radius (scaled units x 100)
  *   "mfma_rmax_x100"  matrix-core forward (fwd_alg 3): largest workgroup row spread (scaled
  *                  units x 100) that takes the MFMA branch; >= 100000 always, 0 never (default 300)
