@@ -674,21 +674,19 @@ __global__ __launch_bounds__(kBlock) void lse_finalize_wave_kernel(const float* 
   }
 }
 
-// U = max_c Op::col_bound(column c) - kLseBoundSlack over the N columns (one workgroup; the
-// maximum is order-free) and the list's count reset: fix = {U, count, -, -, rows...}
+// U = max_c Op::col_bound(c) - kLseBoundSlack over the N columns (one 1024-thread workgroup
+// reading one float per column; the maximum is order-free) and the list's count reset:
+// fix = {U, count, -, -, rows...}
+constexpr int kBoundThreads = 1024;
 template <class Op>
-__global__ __launch_bounds__(kBlock) void lse_bound_kernel(Args args, Scal sc, int64_t N, int* fix) {
-  __shared__ float red[kBlock];
+__global__ __launch_bounds__(kBoundThreads) void lse_bound_kernel(Args args, Scal sc, int64_t N, int* fix) {
+  __shared__ float red[kBoundThreads];
   const int tid = threadIdx.x;
   float mx = -__builtin_huge_valf();
-  for (int64_t j = tid; j < N; j += kBlock) {
-    float rec[4 * Op::CW4];
-    Op::load_col(args, sc, j, rec);
-    mx = fmaxf(mx, Op::col_bound(sc, rec));
-  }
+  for (int64_t j = tid; j < N; j += kBoundThreads) mx = fmaxf(mx, Op::col_bound(args, sc, j));
   red[tid] = mx;
   __syncthreads();
-  for (int o = kBlock / 2; o > 0; o >>= 1) {
+  for (int o = kBoundThreads / 2; o > 0; o >>= 1) {
     if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
     __syncthreads();
   }
@@ -799,7 +797,7 @@ struct OpGmmE {
   static constexpr int kUni = STATS ? D + 1 : -1;
   // the bound shift (lse_bound_kernel): the column's distance-0 logit nc v_c = w2_c
   static constexpr bool kBound = true;
-  __device__ static float col_bound(const Scal& sc, const float* rec) { return sc.nc * rec[D]; }
+  __device__ static float col_bound(const Args& a, const Scal& sc, int64_t j) { return sc.nc * uni_value(a, sc, j); }
   // per-row shift hint (dicp_gmm_estep_hint_f32): Args::r1, or NULL
   __device__ static const float* hint(const Args& a) { return a.r1; }
   static const float* hint_host(const Args& a) { return a.r1; }
@@ -1034,7 +1032,7 @@ int launch_lse(const char* name, const Args& a, const Scal& sc, int64_t M, int64
     // two-set workload); with a hint the shift is within ~8 + log2 C of the row's maximum
     if (lse_bound_ref() != 0 && N > 0 && Op::hint_host(a) != nullptr) {   // {U, count, -, -, rows}
       fix = reinterpret_cast<int*>(part + (size_t)S * (size_t)M * (size_t)(2 + Op::NACC));
-      lse_bound_kernel<Op><<<dim3(1), dim3(kBlock), 0, st>>>(a, sc, N, fix);
+      lse_bound_kernel<Op><<<dim3(1), dim3(kBoundThreads), 0, st>>>(a, sc, N, fix);
       ab.r2 = reinterpret_cast<const float*>(fix);
     }
   }

@@ -2,7 +2,7 @@
 # the CPU baseline, rocprofv3 kernel stats of the same bench command
 set -eo pipefail
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r06z
+O=gpurun_out/r06zz
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { rc=$?; echo "suite rc=$rc"; [ $rc -eq 1 ] || exit $rc; }
 tail -3 $O/gpu_tests.log

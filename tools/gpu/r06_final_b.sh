@@ -2,7 +2,7 @@
 # traffic / issue passes, the secondary workload lines and the host floor
 set -eo pipefail
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/r06z
+O=gpurun_out/r06zz
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/batch_tests.log 2>&1 || { rc=$?; echo "batch rc=$rc"; [ $rc -eq 1 ] || exit $rc; }
 tail -2 $O/batch_tests.log

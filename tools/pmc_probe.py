@@ -46,12 +46,19 @@ def main():
             _lib.gauss_red(_lib.KRED, q, q, 0.1, b=p)
         torch.cuda.synchronize()
         return
+    if os.environ.get("PMC_OPS") == "estep":  # the E-step as the EM loop runs it: unhinted, then hinted
+        T2 = _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True)[1]
+        for _ in range(3):
+            _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True, hint=T2)
+        torch.cuda.synchronize()
+        return
     # the variants the bench's timed Euler steps run (shooting.ShootFn, t = 1..nt-2): the fused
     # forward step writing the divergence rows zs, and the full adjoint step reusing them
+    T2 = _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True)[1]
     for _ in range(3):
         _lib.euler_step(q, p, 0.1, 0.0, 0.1, True, zs_out=zs)
         _lib.euler_adjoint_step(q, p, a, a, gd, 0.1, 0.0, 0.1, zs=zs)
-        _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True)
+        _lib.gmm_estep(q, q, w2, mu2, 0.05, 0.0, True, hint=T2)   # the EM loop's later E-steps
     torch.cuda.synchronize()
 
 

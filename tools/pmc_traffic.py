@@ -17,6 +17,7 @@ import sys
 
 # first match wins: the specific kernel names before the op names they are templated on
 NAMES = {"lse_bound_kernel": "gmm_estep_bound", "lse_fixup_kernel": "gmm_estep_fixup",
+         "OpGmmE<3, true>, 2, true>": "gmm_estep_hinted",
          "lse_finalize": "lse_finalize",
          "sym_fwd_pkn_kernelILi3ELb1ELi3": "ode_self_fwd_sym6", "sym_fwd_pkn_kernelILi3ELb1ELi4": "ode_self_fwd_sym8",
          "sym_fwd_pkn_kernel": "ode_self_fwd_symN",
