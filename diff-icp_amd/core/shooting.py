@@ -395,7 +395,7 @@ class ShootFn(torch.autograd.Function):
                 sigma, eta, nt, scheme, want_div, has_x
             ctx.save_for_backward(*hit["saved"])
             # fresh output tensors (autograd owns them); the saved ones are only read
-            return tuple(t.clone() for t in hit["outs"])
+            return _fresh(hit["outs"])
         # row-split over ranks (core/rowsplit.py): dense Euler shooting only; other schemes
         # run replicated on every rank
         if split is not None and (has_x or scheme != "Euler" or split.world == 1):
@@ -413,7 +413,7 @@ class ShootFn(torch.autograd.Function):
                 if cache is not None:
                     kept = tuple(t.detach() for t in outs)
                     cache.store(q0, p0, x0, params, kept, [t.detach() for t in saved])
-                    return tuple(t.clone() for t in kept)
+                    return _fresh(kept)
                 return outs
         M, D = q0.shape
         dev = q0.device
@@ -640,7 +640,7 @@ class ShootFn(torch.autograd.Function):
             cache.store(q0, p0, x0, params, kept, [t.detach() for t in saved])
             # the cache keeps Q, P, ... (and autograd saved them): the caller gets its own
             # copies, so an in-place write by the caller (complete_shoot) cannot reach them
-            return tuple(t.clone() for t in kept)
+            return _fresh(kept)
         return outs
 
     @staticmethod
@@ -922,18 +922,41 @@ def _capture(run, dev):
         _graph_tl.inside = False
 
 
+def _copy_many(dsts, srcs):
+    """dst.copy_(src) for every pair, as one multi-tensor launch where torch can (same device
+    and dtype, dense): the graph replays' input and output copies were ~18 separate buffer
+    copies per L-BFGS closure, a tenth of the 2k-point iteration's kernels
+    (tools/host_floor_timeline.py).  Copies are exact, so results are bitwise unchanged."""
+    if not dsts:
+        return
+    if len(dsts) == 1:
+        dsts[0].copy_(srcs[0])
+        return
+    torch._foreach_copy_(list(dsts), list(srcs))
+
+
+def _fresh(ts):
+    """tuple(t.clone() for t in ts), the copies in one launch (_copy_many)."""
+    out = tuple(torch.empty_like(t) for t in ts)
+    _copy_many(out, ts)
+    return out
+
+
 def _clone_all(ts):
     """Fresh copies of a list of tensors (None kept), each distinct tensor copied once."""
     memo = {}
-    out = []
+    out, dsts, srcs = [], [], []
     for t in ts:
         if t is None:
             out.append(None)
             continue
         c = memo.get(id(t))
         if c is None:
-            c = memo[id(t)] = t.clone()
+            c = memo[id(t)] = torch.empty_like(t)
+            dsts.append(c)
+            srcs.append(t)
         out.append(c)
+    _copy_many(dsts, srcs)
     return out
 
 
@@ -960,8 +983,7 @@ def _graph_forward(ctx, q0, p0, order, sigma, eta, nt, want_div, need_p1, params
     if ent is None:
         return None
     sq0, sp0 = ent["in"]
-    sq0.copy_(q0)
-    sp0.copy_(p0)
+    _copy_many([sq0, sp0], [q0, p0])
     ent["g"].replay()
     graph_stats["replays"] += 1
     n_out = len(ent["outs"])
@@ -996,9 +1018,8 @@ def _graph_backward(ctx, gQ, gP, gC, gH, saved, Zs):
     ent = _graph_entry(key, capture)
     if ent is None:
         return None
-    for s_, t in zip(ent["in"], ins):
-        if t is not None:
-            s_.copy_(t)
+    pairs = [(s_, t) for s_, t in zip(ent["in"], ins) if t is not None]
+    _copy_many([s_ for s_, _ in pairs], [t for _, t in pairs])
     ent["g"].replay()
     graph_stats["replays"] += 1
     out = ent["out"]

@@ -58,6 +58,12 @@ def _rowdots(A, v):
     return (A * v[None, :]).sum(1, dtype=torch.float64)
 
 
+def _absmax(v):
+    """max|v| in one reduction launch (torch's abs().max() takes two); a maximum of magnitudes
+    involves no rounding, so the value (NaN included) is bitwise the same."""
+    return torch.linalg.vector_norm(v, ord=math.inf)
+
+
 class CompactLBFGS(torch.optim.LBFGS):
     """Drop-in for torch.optim.LBFGS (same constructor and step semantics)."""
 
@@ -120,8 +126,13 @@ class CompactLBFGS(torch.optim.LBFGS):
     on_loss = None   # callback(loss: float) after every function evaluation
 
     def _read(self, *ts):
-        """Device scalars -> host floats in one transfer (float64: exact for either dtype)."""
-        return torch.stack([t.detach().reshape(()).to(torch.float64) for t in ts]).tolist()
+        """Device scalars -> host floats in one transfer (float64: exact for either dtype; scalars
+        of one dtype are stacked as they are -- the float32 -> Python float conversion is exact
+        too -- which saves a conversion launch per scalar)."""
+        ts = [t.detach().reshape(()) for t in ts]
+        if any(t.dtype != ts[0].dtype for t in ts):
+            ts = [t.to(torch.float64) for t in ts]
+        return torch.stack(ts).tolist()
 
     def _dt(self, *vals):
         """Host stand-ins of torch's 0-d tensors: numpy scalars of the parameters' dtype."""
@@ -134,11 +145,11 @@ class CompactLBFGS(torch.optim.LBFGS):
         L = closure()
         flat_grad = self._gather_flat_grad()
         if d is None:
-            loss, gmax = self._read(L, flat_grad.abs().max())
+            loss, gmax = self._read(L, _absmax(flat_grad))
             gtd = None
             (gmax,) = self._dt(gmax)
         else:
-            loss, gtd, gmax = self._read(L, flat_grad.dot(d), flat_grad.abs().max())
+            loss, gtd, gmax = self._read(L, flat_grad.dot(d), _absmax(flat_grad))
             gtd, gmax = self._dt(gtd, gmax)
         if self.on_loss is not None:
             self.on_loss(loss)
@@ -301,11 +312,11 @@ class CompactLBFGS(torch.optim.LBFGS):
 
             first = state["n_iter"] == 1
             if first:
-                gtd, d_norm, gsum = self._dt(*self._read(flat_grad.dot(d), d.abs().max(),
+                gtd, d_norm, gsum = self._dt(*self._read(flat_grad.dot(d), _absmax(d),
                                                          flat_grad.abs().sum()))
                 t = min(1.0, 1.0 / gsum) * lr
             else:
-                gtd, d_norm = self._dt(*self._read(flat_grad.dot(d), d.abs().max()))
+                gtd, d_norm = self._dt(*self._read(flat_grad.dot(d), _absmax(d)))
                 t = lr
             if gtd > -tolerance_change:
                 break
