@@ -303,8 +303,22 @@ class DiffPSR(MultiPSR):
         sig2 = torch.cat(tuple(self.GMMi[s].sigma ** 2 * torch.ones(int(self.N[k, s]))
                                for s in range(self.S))).to(**self.compspec).contiguous()
 
+        s2x = 2 * sig2[:, None]
+
         def dataloss_func(x):
-            return ((x - y) ** 2 / (2 * sig2[:, None])).sum()
+            return ((x - y) ** 2 / s2x).sum()
+
+        # the value and dL/dx without autograd (core/shooting.py shoot_loss_grad): the bits
+        # autograd forms -- DivBackward 1/s2x, PowBackward (1/s2x) * (2 (x - y)) -- with the
+        # forward's own ops for the value (tests/test_gpu_host_floor.py: bitwise)
+        inv = torch.ones_like(s2x).div(s2x)
+
+        def value_and_grad(x):
+            if y.requires_grad or s2x.requires_grad:
+                return None     # gradients into y / sigma: the autograd path
+            d = x - y
+            return (d ** 2 / s2x).sum(), inv * (2.0 * d)
+        dataloss_func.value_and_grad = value_and_grad
         return dataloss_func
 
     def _optimize_frame(self, k, nmax, tol):

@@ -92,8 +92,7 @@ class CompactLBFGS(torch.optim.LBFGS):
             SY[:-1, :-1] = SY[1:, 1:].clone()
             YY[:-1, :-1] = YY[1:, 1:].clone()
             m -= 1
-        S[m].copy_(s)
-        Y[m].copy_(y)
+        torch._foreach_copy_([S[m], Y[m]], [s, y])    # one launch for both rows
         # new column of S^T Y / Y^T Y and new row s_m^T Y: two stacked GEMVs
         a = _rowdots(torch.cat([S[:m + 1], Y[:m + 1]], 0), y)    # [S^T y; Y^T y]
         b = _rowdots(Y[:m + 1], s)                                 # y_j . s_m
