@@ -15,9 +15,9 @@ compact representation (Byrd, Nocedal & Schnabel 1994, eq. 2.6; H0 = gamma I):
     t = R^{-T} ((D + gamma Y^T Y) u - gamma Y^T v)
 
 with S, Y the (m, n) histories kept in preallocated device buffers, R = triu(S^T Y),
-D = diag(S^T Y).  Per iteration: one stacked GEMV [S; Y] v, two m x m triangular solves
-(float64) and one GEMV back; the m x m products are updated incrementally (two GEMVs per new
-pair).  Results equal torch's two-loop up to floating-point rounding.  The "GEMVs" are torch
+D = diag(S^T Y).  Per iteration: one stacked GEMV [S; Y] v on the device, the m x m products
+S^T Y, Y^T Y (updated incrementally: two GEMVs per new pair) and the two triangular solves
+(float64) on the host, one transfer of the GEMVs' 3m+2 values and one GEMV back.  Results equal torch's two-loop up to floating-point rounding.  The "GEMVs" are torch
 elementwise products + reductions, not BLAS calls: rocBLAS allows atomics by default, and the
 row-split multi-GPU mode needs bitwise-identical iterates on every rank.
 
@@ -77,48 +77,71 @@ class CompactLBFGS(torch.optim.LBFGS):
         st = self.state[self._params[0]]
         st["S"] = torch.empty((h, n), device=like.device, dtype=like.dtype)
         st["Y"] = torch.empty((h, n), device=like.device, dtype=like.dtype)
-        st["SY"] = torch.zeros((h, h), device=like.device, dtype=torch.float64)  # s_i . y_j
-        st["YY"] = torch.zeros((h, h), device=like.device, dtype=torch.float64)  # y_i . y_j
+        # the m x m algebra runs on the host (float64 CPU tensors): on the device it was ~20
+        # launches per iteration (triangle, two rocBLAS triangular solves with their index
+        # kernels, a dozen scalar ops, the slice writes) -- the largest share of the 2k-point
+        # host floor after the shootings (tools/host_floor_timeline.py); on CPU parameters the
+        # ops are the same torch CPU ops as before, bit for bit
+        st["SY"] = torch.zeros((h, h), dtype=torch.float64)   # s_i . y_j
+        st["YY"] = torch.zeros((h, h), dtype=torch.float64)   # y_i . y_j
         st["m"] = 0
+        st["pend"] = None
 
     def _hist_push(self, s, y):
         st = self.state[self._params[0]]
         h = self.param_groups[0]["history_size"]
-        S, Y, SY, YY = st["S"], st["Y"], st["SY"], st["YY"]
+        S, Y = st["S"], st["Y"]
         m = st["m"]
         if m == h:  # drop the oldest pair (torch: old_dirs.pop(0))
             S[:-1] = S[1:].clone()
             Y[:-1] = Y[1:].clone()
+            SY, YY = st["SY"], st["YY"]
             SY[:-1, :-1] = SY[1:, 1:].clone()
             YY[:-1, :-1] = YY[1:, 1:].clone()
             m -= 1
         torch._foreach_copy_([S[m], Y[m]], [s, y])    # one launch for both rows
-        # new column of S^T Y / Y^T Y and new row s_m^T Y: two stacked GEMVs
+        # new column of S^T Y / Y^T Y and new row s_m^T Y: two stacked GEMVs on the device,
+        # read together with the next _hist_apply's GEMV (one transfer)
         a = _rowdots(torch.cat([S[:m + 1], Y[:m + 1]], 0), y)    # [S^T y; Y^T y]
         b = _rowdots(Y[:m + 1], s)                                 # y_j . s_m
-        SY[:m + 1, m] = a[:m + 1].double()
-        SY[m, :m + 1] = b.double()
-        YY[:m + 1, m] = a[m + 1:].double()
-        YY[m, :m + 1] = a[m + 1:].double()
+        st["pend"] = (m, a, b)
         st["m"] = m + 1
+
+    def _hist_commit(self, pend, a, b):
+        st = self.state[self._params[0]]
+        m = pend
+        SY, YY = st["SY"], st["YY"]
+        SY[:m + 1, m] = a[:m + 1]
+        SY[m, :m + 1] = b
+        YY[:m + 1, m] = a[m + 1:]
+        YY[m, :m + 1] = a[m + 1:]
 
     def _hist_apply(self, v, gamma):
         """H v (compact form)."""
         st = self.state[self._params[0]]
         m = st["m"]
+        pend, st["pend"] = st["pend"], None
         if m == 0:
             return v * gamma
         S, Y = st["S"][:m], st["Y"][:m]
-        SY, YY = st["SY"][:m, :m], st["YY"][:m, :m]
         SY_ = torch.cat([S, Y], 0)
-        ab = _rowdots(SY_, v).double()
+        ab = _rowdots(SY_, v)
+        if pend is not None:
+            pm, pa, pb = pend
+            n_a, n_b = pa.numel(), pb.numel()
+            host = torch.cat([pa, pb, ab]).cpu()      # one transfer (a no-op on CPU)
+            self._hist_commit(pm, host[:n_a], host[n_a:n_a + n_b])
+            ab = host[n_a + n_b:]
+        else:
+            ab = ab.cpu()
+        SY, YY = st["SY"][:m, :m], st["YY"][:m, :m]
         a, b = ab[:m], ab[m:]
         g = gamma if isinstance(gamma, float) else gamma.double()
         R = torch.triu(SY)
         u = torch.linalg.solve_triangular(R, a[:, None], upper=True)[:, 0]
         w = torch.diagonal(SY) * u + g * _rowdots(YY, u) - g * b
         t = torch.linalg.solve_triangular(R.t(), w[:, None], upper=False)[:, 0]
-        coef = torch.cat([t, -g * u]).to(v.dtype)
+        coef = torch.cat([t, -g * u]).to(dtype=v.dtype).to(v.device)
         return v * gamma + (SY_ * coef[:, None]).sum(0)
 
     # ------------------------------------------------------------------------------
@@ -130,7 +153,7 @@ class CompactLBFGS(torch.optim.LBFGS):
         too -- which saves a conversion launch per scalar)."""
         ts = [t.detach().reshape(()) for t in ts]
         if any(t.dtype != ts[0].dtype for t in ts):
-            ts = [t.to(torch.float64) for t in ts]
+            ts = [t if t.dtype == torch.float64 else t.to(torch.float64) for t in ts]
         return torch.stack(ts).tolist()
 
     def _dt(self, *vals):

@@ -1,7 +1,7 @@
 """Which torch ops (by Python call site) the 2k-point PSR iteration issues -- the host floor's
 kernel count (tools/host_floor_timeline.py: ~196 device kernels per L-BFGS closure, a quarter
-of them buffer copies).  torch.profiler over one iteration after a warm-up one, CPU activity
-only, ops grouped by their top Python frames, sorted by call count.
+of them buffer copies).  a dispatch-mode counter over one iteration after two warm-up ones, ops
+grouped by their top Python frames in this repository, sorted by call count.
 
     python tools/probes/host_ops.py [--N 2000] [--top 40] [--frames 4]
 """
@@ -26,21 +26,29 @@ def main():
     workloads.psr_iteration(psr)
     workloads.psr_iteration(psr)
     torch.cuda.synchronize()
-    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], with_stack=True) as prof:
-        workloads.psr_iteration(psr)
-        torch.cuda.synchronize()
-    ka = prof.key_averages(group_by_stack_n=a.frames)
-    rows = [e for e in ka if e.key.startswith("aten::") and e.stack]
-    rows.sort(key=lambda e: -e.count)
-    tot = {}
-    for e in ka:
-        if e.key.startswith("aten::"):
-            tot[e.key] = tot.get(e.key, 0) + e.count
-    print("op totals:", sorted(tot.items(), key=lambda kv: -kv[1])[:30])
-    for e in rows[:a.top]:
-        st = " <- ".join(s.split("/")[-1] for s in e.stack[:a.frames])
-        print(f"{e.count:5d} {e.key:28s} {st}")
+    import collections
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+    cnt = collections.Counter()
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+    class Count(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            fr = [f for f in traceback.extract_stack()[:-2] if f.filename.startswith(root)
+                  or "torch/optim" in f.filename]
+            site = " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}" for f in fr[::-1][:a.frames])
+            cnt[(str(func.overloadpacket), site)] += 1
+            return func(*args, **(kwargs or {}))
+
+    with Count():
+        workloads.psr_iteration(psr)
+    torch.cuda.synchronize()
+    tot = collections.Counter()
+    for (op, _), c in cnt.items():
+        tot[op] += c
+    print("op totals:", tot.most_common(40))
+    for (op, site), c in cnt.most_common(a.top):
+        print(f"{c:5d} {op:28s} {site}")
 
 if __name__ == "__main__":
     main()
