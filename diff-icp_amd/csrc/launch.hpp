@@ -90,6 +90,20 @@ inline int64_t round_chunk(int64_t N, int64_t S) {
 }
 
 // Experiment knob (dicp_set_option "force_splits"): > 0 forces the split count.
+// dicp_set_option "min_chunk": the smallest column chunk of a split; 0 (default) = automatic:
+// kMinChunk, but 64 up to kSmallCols columns -- there the 256-column floor capped the split
+// count, hence the grid (2k points: 8 splits x 4 row blocks = 32 workgroups, ~20 us per fused
+// forward pass); 64 measured 27.1 -> 25.8 ms per 2k PSR iteration (tools/probes/min_chunk_ab.py)
+constexpr int64_t kSmallCols = 4096;
+inline int64_t& min_chunk() {
+  static int64_t s = 0;
+  return s;
+}
+inline int64_t min_chunk_for(int64_t N) {
+  if (min_chunk() > 0) return min_chunk();
+  return N <= kSmallCols ? 64 : kMinChunk;
+}
+
 inline int& force_splits() {
   static int s = 0;
   return s;
@@ -101,7 +115,8 @@ inline int num_splits_cap(int64_t M, int64_t N, int R, int64_t cap, int64_t roun
   const int64_t bx = (M + (int64_t)kBlock * R - 1) / ((int64_t)kBlock * R);
   int64_t S = (rounds_for(M, round_rows, max_rounds) * cap + bx - 1) / bx;
   if (force_splits() > 0) S = force_splits();
-  int64_t smax = (N + kMinChunk - 1) / kMinChunk;
+  const int64_t mc = min_chunk_for(N);
+  int64_t smax = (N + mc - 1) / mc;
   if (smax < 1) smax = 1;
   if (S > smax) S = smax;
   if (S < 1) S = 1;

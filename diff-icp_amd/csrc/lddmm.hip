@@ -160,6 +160,11 @@ extern "C" int dicp_set_option(const char* name, int value) {
     sym_L() = value;
     return DICP_OK;
   }
+  if (!strcmp(name, "min_chunk")) {
+    if (value != 0 && (value < 16 || value > 65536)) return DICP_ERR_INVALID;   // 0 = automatic
+    min_chunk() = value;
+    return DICP_OK;
+  }
   if (!strcmp(name, "force_splits")) {
     if (value < 0 || value > 65536) return DICP_ERR_INVALID;
     force_splits() = value;
@@ -265,6 +270,7 @@ extern "C" int dicp_get_option(const char* name, int* value) {
   if (!strcmp(name, "split_rounds")) { *value = split_rounds(); return DICP_OK; }
   if (!strcmp(name, "sym_L")) { *value = sym_L(); return DICP_OK; }
   if (!strcmp(name, "force_splits")) { *value = force_splits(); return DICP_OK; }
+  if (!strcmp(name, "min_chunk")) { *value = (int)min_chunk(); return DICP_OK; }
   if (!strcmp(name, "pk_rp")) { *value = pk_rp_force(); return DICP_OK; }
   if (!strcmp(name, "sym_rp")) { *value = sym_rp(); return DICP_OK; }
   if (!strcmp(name, "batch_share")) { *value = batch_share(); return DICP_OK; }
