@@ -90,19 +90,17 @@ inline int64_t round_chunk(int64_t N, int64_t S) {
 }
 
 // Experiment knob (dicp_set_option "force_splits"): > 0 forces the split count.
-// dicp_set_option "min_chunk": the smallest column chunk of a split; 0 (default) = automatic:
-// kMinChunk, but 64 up to kSmallCols columns -- there the 256-column floor capped the split
-// count, hence the grid (2k points: 8 splits x 4 row blocks = 32 workgroups, ~20 us per fused
-// forward pass); 64 measured 27.1 -> 25.8 ms per 2k PSR iteration (tools/probes/min_chunk_ab.py)
-constexpr int64_t kSmallCols = 4096;
+// dicp_set_option "min_chunk": the smallest column chunk of a split; 0 (default) = kMinChunk.
+// At a few thousand columns the 256 floor caps the split count, hence the grid (2k points: 8
+// splits x 4 row blocks = 32 workgroups, ~20 us per fused forward pass); 64 measured 27.7 ->
+// 26.7 ms per 2k PSR iteration (tools/probes/min_chunk_ab.py), but the changed summation split
+// moved a 400-point logdet Ralston gradient to 2.17e-5 of float64 against its 2e-5 bound
+// (tests/test_gpu_model.py), so the default stays 256 (forced only)
 inline int64_t& min_chunk() {
   static int64_t s = 0;
   return s;
 }
-inline int64_t min_chunk_for(int64_t N) {
-  if (min_chunk() > 0) return min_chunk();
-  return N <= kSmallCols ? 64 : kMinChunk;
-}
+inline int64_t min_chunk_for(int64_t) { return min_chunk() > 0 ? min_chunk() : kMinChunk; }
 
 inline int& force_splits() {
   static int s = 0;

@@ -393,8 +393,7 @@ int dicp_supports_dim(int D);
  *   "bwd_eta_alg"  eta != 0 VJP: 0 ordered, 1 symmetric, 2 symmetric packed-FP32 (default)
  *   "r_fwd" / "r_bwd"  rows per thread {1,2,4} of the ordered passes (env DICP_R_FWD / DICP_R_BWD)
  *   "split_rounds", "force_splits", "sym_L"  column-split / symmetric-chunk geometry (0 = auto)
- *   "min_chunk"    smallest column chunk of a split, 16..65536; 0 (default) automatic: 64 up to
- *                  4096 columns, else 256
+ *   "min_chunk"    smallest column chunk of a split, 16..65536; 0 (default) = 256
  *   "pk_rp"        packed row passes: row pairs per thread, 0 automatic (2 for the eta = 0 fused
  *                  forward and the packed external-point / KRed passes from 32k rows and 8k
  *                  columns, else 1), 1 or 2 forced

@@ -1,7 +1,7 @@
 """The 2k-point PSR iteration (tools/host_floor.py's workload) under several split minimum
-chunks (library option "min_chunk"; 256, the rule before round 6's last build, caps the
-ordered forward at 2k columns at 8 splits = 32 workgroups, ~20 us per pass; the automatic rule
-now takes 64 up to 4096 columns): fresh workload per measurement, settings
+chunks (library option "min_chunk", default 256: at 2k columns it caps the ordered forward at
+8 splits = 32 workgroups, ~20 us per pass; 64 is faster at 2k but stays forced-only, see
+csrc/launch.hpp): fresh workload per measurement, settings
 alternated, ms per iteration and per closure.
 
     python tools/probes/min_chunk_ab.py [--chunks 256 64 32] [--reps 3]
